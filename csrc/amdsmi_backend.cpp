@@ -1,0 +1,204 @@
+// nos amd-smi backend: a C ABI over libamd_smi for the partition agent.
+//
+// Replaces the reference's NVML/cgo client (reference pkg/gpu/nvml/client.go:31-511). On MI355X a
+// "partition change" is one amdsmi_set_gpu_compute_partition call per physical GPU (homogeneous
+// SPX/DPX/QPX/CPX) plus an optional node-wide memory-partition (NPS) change, so the reference's
+// GPU-instance/compute-instance bookkeeping and its n! creation-order search disappear.
+//
+// One amd-smi session is kept for the life of the process (the reference re-initialises NVML on
+// every call). Return codes: 0 ok, 1 generic, 2 permission, 3 not found, 4 busy.
+#include <amd_smi/amdsmi.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace {
+
+std::mutex g_mu;
+bool g_init = false;
+std::vector<amdsmi_processor_handle> g_gpus;
+thread_local std::string g_err;
+
+int map_status(amdsmi_status_t st, const char* what) {
+  if (st == AMDSMI_STATUS_SUCCESS) return 0;
+  const char* s = nullptr;
+  amdsmi_status_code_to_string(st, &s);
+  g_err = std::string(what) + ": " + (s ? s : "amdsmi error") + " (" + std::to_string(int(st)) + ")";
+  switch (st) {
+    case AMDSMI_STATUS_NO_PERM: return 2;
+    case AMDSMI_STATUS_NOT_FOUND: return 3;
+    case AMDSMI_STATUS_BUSY: return 4;
+    default: return 1;
+  }
+}
+
+int handle(uint32_t idx, amdsmi_processor_handle* h) {
+  if (!g_init) { g_err = "amdsmi not initialised"; return 1; }
+  if (idx >= g_gpus.size()) { g_err = "GPU index out of range"; return 3; }
+  *h = g_gpus[idx];
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+struct nos_gpu_info {
+  uint32_t index;
+  char uuid[64];
+  char bdf[32];
+  char market_name[64];
+  uint64_t vram_bytes;
+  uint32_t cu_count;
+  uint32_t xcds;
+};
+
+const char* nos_smi_last_error() { return g_err.c_str(); }
+
+int nos_smi_init() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_init) return 0;
+  amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_init");
+  uint32_t nsock = 0;
+  st = amdsmi_get_socket_handles(&nsock, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  st = amdsmi_get_socket_handles(&nsock, socks.data());
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
+  g_gpus.clear();
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t n = 0;
+    st = amdsmi_get_processor_handles(socks[s], &n, nullptr);
+    if (st != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> hs(n);
+    if (amdsmi_get_processor_handles(socks[s], &n, hs.data()) != AMDSMI_STATUS_SUCCESS) continue;
+    for (uint32_t i = 0; i < n; ++i) {
+      processor_type_t t;
+      if (amdsmi_get_processor_type(hs[i], &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        g_gpus.push_back(hs[i]);
+    }
+  }
+  g_init = true;
+  return 0;
+}
+
+int nos_smi_shutdown() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_init) return 0;
+  g_gpus.clear();
+  g_init = false;
+  return map_status(amdsmi_shut_down(), "amdsmi_shut_down");
+}
+
+int nos_smi_gpu_count() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_init ? int(g_gpus.size()) : -1;
+}
+
+int nos_smi_gpu_info(uint32_t idx, nos_gpu_info* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  std::memset(out, 0, sizeof(*out));
+  out->index = idx;
+  unsigned int ulen = sizeof(out->uuid);
+  amdsmi_get_gpu_device_uuid(h, &ulen, out->uuid);
+  amdsmi_bdf_t bdf;
+  if (amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+    std::snprintf(out->bdf, sizeof(out->bdf), "%04llx:%02llx:%02llx.%llx",
+                  (unsigned long long)bdf.domain_number, (unsigned long long)bdf.bus_number,
+                  (unsigned long long)bdf.device_number, (unsigned long long)bdf.function_number);
+  }
+  amdsmi_asic_info_t asic;
+  if (amdsmi_get_gpu_asic_info(h, &asic) == AMDSMI_STATUS_SUCCESS) {
+    std::snprintf(out->market_name, sizeof(out->market_name), "%.63s", asic.market_name);
+    if (asic.num_of_compute_units != 0xFFFFFFFFu) out->cu_count = asic.num_of_compute_units;
+  }
+  uint64_t total = 0;
+  if (amdsmi_get_gpu_memory_total(h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS) out->vram_bytes = total;
+  out->xcds = 8;
+  return 0;
+}
+
+int nos_smi_get_compute_partition(uint32_t idx, char* buf, uint32_t len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  return map_status(amdsmi_get_gpu_compute_partition(h, buf, len), "amdsmi_get_gpu_compute_partition");
+}
+
+int nos_smi_get_memory_partition(uint32_t idx, char* buf, uint32_t len) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  return map_status(amdsmi_get_gpu_memory_partition(h, buf, len), "amdsmi_get_gpu_memory_partition");
+}
+
+int nos_smi_set_compute_partition(uint32_t idx, const char* mode) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  amdsmi_compute_partition_type_t t = AMDSMI_COMPUTE_PARTITION_INVALID;
+  std::string m(mode);
+  if (m == "SPX") t = AMDSMI_COMPUTE_PARTITION_SPX;
+  else if (m == "DPX") t = AMDSMI_COMPUTE_PARTITION_DPX;
+  else if (m == "TPX") t = AMDSMI_COMPUTE_PARTITION_TPX;
+  else if (m == "QPX") t = AMDSMI_COMPUTE_PARTITION_QPX;
+  else if (m == "CPX") t = AMDSMI_COMPUTE_PARTITION_CPX;
+  else { g_err = "invalid compute partition " + m; return 1; }
+  return map_status(amdsmi_set_gpu_compute_partition(h, t), "amdsmi_set_gpu_compute_partition");
+}
+
+int nos_smi_set_memory_partition(uint32_t idx, const char* mode) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  amdsmi_memory_partition_type_t t = AMDSMI_MEMORY_PARTITION_UNKNOWN;
+  std::string m(mode);
+  if (m == "NPS1") t = AMDSMI_MEMORY_PARTITION_NPS1;
+  else if (m == "NPS2") t = AMDSMI_MEMORY_PARTITION_NPS2;
+  else if (m == "NPS4") t = AMDSMI_MEMORY_PARTITION_NPS4;
+  else if (m == "NPS8") t = AMDSMI_MEMORY_PARTITION_NPS8;
+  else { g_err = "invalid memory partition " + m; return 1; }
+  return map_status(amdsmi_set_gpu_memory_partition(h, t), "amdsmi_set_gpu_memory_partition");
+}
+
+int nos_smi_process_count(uint32_t idx) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (handle(idx, &h)) return -1;
+  uint32_t n = 0;
+  amdsmi_status_t st = amdsmi_get_gpu_process_list(h, &n, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) {
+    map_status(st, "amdsmi_get_gpu_process_list");
+    return -1;
+  }
+  return int(n);
+}
+
+int nos_smi_activity(uint32_t idx, uint32_t* gfx, uint32_t* umc, uint32_t* mm) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  amdsmi_engine_usage_t u;
+  int rc = map_status(amdsmi_get_gpu_activity(h, &u), "amdsmi_get_gpu_activity");
+  if (rc) return rc;
+  *gfx = u.gfx_activity; *umc = u.umc_activity; *mm = u.mm_activity;
+  return 0;
+}
+
+int nos_smi_vram(uint32_t idx, uint64_t* total, uint64_t* used) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  int rc = map_status(amdsmi_get_gpu_memory_total(h, AMDSMI_MEM_TYPE_VRAM, total), "amdsmi_get_gpu_memory_total");
+  if (rc) return rc;
+  return map_status(amdsmi_get_gpu_memory_usage(h, AMDSMI_MEM_TYPE_VRAM, used), "amdsmi_get_gpu_memory_usage");
+}
+
+}  // extern "C"

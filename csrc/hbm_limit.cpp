@@ -1,0 +1,170 @@
+// nos HBM budget shim (LD_PRELOAD) for CU-mask slices.
+//
+// The reference enforces MPS memory slices with CUDA_MPS_PINNED_DEVICE_MEM_LIMIT
+// (docs getting-started-mps.md). HIP has no MPS daemon, so a slice's HBM budget is enforced in the
+// workload process itself: this library interposes the HIP device-allocation entry points, tracks
+// live bytes per pointer and fails an allocation that would exceed NOS_HBM_LIMIT_BYTES with
+// hipErrorOutOfMemory. hipMemGetInfo is clamped to the budget so caching allocators (PyTorch's)
+// size themselves to the slice. Compute isolation comes from HSA_CU_MASK (ROCr applies it to every
+// queue the process creates, hsa_ext_amd.h:1330-1345); both variables are injected by the nos device
+// plugin at Allocate time.
+//
+// Isolation is cooperative: nothing stops a process from unsetting LD_PRELOAD (documented in
+// docs/partitioning-modes.md, as the reference documents MPS's limits).
+#include <dlfcn.h>
+
+#include <atomic>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+
+namespace {
+
+using hipErr = int;  // hipError_t is an int-sized enum
+constexpr hipErr kSuccess = 0;
+constexpr hipErr kOutOfMemory = 2;  // hipErrorOutOfMemory
+
+std::mutex g_mu;
+std::unordered_map<void*, size_t>* g_sizes = nullptr;
+std::atomic<size_t> g_live{0};
+std::atomic<size_t> g_peak{0};
+size_t g_limit = 0;
+bool g_loaded = false;
+
+void init_once() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    g_sizes = new std::unordered_map<void*, size_t>();
+    if (const char* v = std::getenv("NOS_HBM_LIMIT_BYTES")) g_limit = std::strtoull(v, nullptr, 10);
+    g_loaded = true;
+  });
+}
+
+// Resolve the real HIP entry point. RTLD_NEXT only searches the global scope; a runtime that was
+// dlopen'ed RTLD_LOCAL (PyTorch loads its bundled libamdhip64 that way) is invisible to it, so fall
+// back to the already-loaded runtime by soname. Never return null: abort with a message instead of
+// jumping to address 0.
+template <typename F>
+F next(const char* name) {
+  void* p = dlsym(RTLD_NEXT, name);
+  if (!p) {
+    void* h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("libamdhip64.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("libamdhip64.so.7", RTLD_NOW | RTLD_GLOBAL);
+    if (h) p = dlsym(h, name);
+  }
+  if (!p) {
+    std::fprintf(stderr, "nos hbm-limit shim: cannot resolve %s\n", name);
+    std::abort();
+  }
+  return reinterpret_cast<F>(p);
+}
+
+bool reserve(size_t bytes) {
+  if (g_limit == 0) {
+    g_live += bytes;
+    return true;
+  }
+  size_t cur = g_live.load();
+  while (true) {
+    if (cur + bytes > g_limit) return false;
+    if (g_live.compare_exchange_weak(cur, cur + bytes)) return true;
+  }
+}
+
+void track(void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  (*g_sizes)[p] = bytes;
+  size_t live = g_live.load();
+  if (live > g_peak.load()) g_peak = live;
+}
+
+void untrack(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_sizes->find(p);
+  if (it != g_sizes->end()) {
+    g_live -= it->second;
+    g_sizes->erase(it);
+  }
+}
+
+template <typename Alloc>
+hipErr guarded(void** ptr, size_t size, Alloc&& alloc) {
+  init_once();
+  if (!reserve(size)) {
+    if (ptr) *ptr = nullptr;
+    return kOutOfMemory;
+  }
+  hipErr rc = alloc();
+  if (rc != kSuccess || !ptr || !*ptr) {
+    g_live -= size;
+    return rc;
+  }
+  track(*ptr, size);
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+hipErr hipMalloc(void** ptr, size_t size) {
+  static auto real = next<hipErr (*)(void**, size_t)>("hipMalloc");
+  return guarded(ptr, size, [&] { return real(ptr, size); });
+}
+
+hipErr hipExtMallocWithFlags(void** ptr, size_t size, unsigned int flags) {
+  static auto real = next<hipErr (*)(void**, size_t, unsigned int)>("hipExtMallocWithFlags");
+  return guarded(ptr, size, [&] { return real(ptr, size, flags); });
+}
+
+hipErr hipMallocAsync(void** ptr, size_t size, void* stream) {
+  static auto real = next<hipErr (*)(void**, size_t, void*)>("hipMallocAsync");
+  return guarded(ptr, size, [&] { return real(ptr, size, stream); });
+}
+
+hipErr hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
+  static auto real = next<hipErr (*)(void**, size_t, unsigned int)>("hipMallocManaged");
+  return guarded(ptr, size, [&] { return real(ptr, size, flags); });
+}
+
+hipErr hipFree(void* ptr) {
+  static auto real = next<hipErr (*)(void*)>("hipFree");
+  init_once();
+  hipErr rc = real(ptr);
+  if (rc == kSuccess) untrack(ptr);
+  return rc;
+}
+
+hipErr hipFreeAsync(void* ptr, void* stream) {
+  static auto real = next<hipErr (*)(void*, void*)>("hipFreeAsync");
+  init_once();
+  hipErr rc = real(ptr, stream);
+  if (rc == kSuccess) untrack(ptr);
+  return rc;
+}
+
+hipErr hipMemGetInfo(size_t* free_b, size_t* total_b) {
+  static auto real = next<hipErr (*)(size_t*, size_t*)>("hipMemGetInfo");
+  init_once();
+  hipErr rc = real(free_b, total_b);
+  if (rc == kSuccess && g_limit > 0) {
+    size_t live = g_live.load();
+    size_t budget_free = live >= g_limit ? 0 : g_limit - live;
+    if (*total_b > g_limit) *total_b = g_limit;
+    if (*free_b > budget_free) *free_b = budget_free;
+  }
+  return rc;
+}
+
+// introspection for tests / the workload runner
+size_t nos_hbm_limit_bytes() { init_once(); return g_limit; }
+size_t nos_hbm_live_bytes() { return g_live.load(); }
+size_t nos_hbm_peak_bytes() { return g_peak.load(); }
+int nos_hbm_shim_loaded() { init_once(); return g_loaded ? 1 : 0; }
+
+}  // extern "C"

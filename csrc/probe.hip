@@ -1,0 +1,308 @@
+// nos slice probe: MFMA-saturating, LDS-resident CDNA4 kernels that measure what a GPU slice
+// (a compute partition, or a CU-masked stream) can actually deliver, plus an HBM stream probe and
+// a workgroup-placement census.  Exposed through a plain C ABI (ctypes) so the node agent can run
+// it without PyTorch; inside a PyTorch process the same HIP runtime instance is shared (one soname).
+//
+// Design (gfx950, MI355X_MICROARCH.md "Matrix cores" + "Per-instruction cycle constants"):
+//  * 256-thread workgroups = 4 waves = one wave per SIMD; default 2 workgroups per CU.
+//  * operands are staged once into LDS and re-read with ds_read_b128 every iteration (two reads
+//    per four 32x32x16 MFMAs: within the per-gap budget measured at <=3 cycles), so the loop is
+//    matrix-pipe bound, not memory bound, and the operands are random (DVFS-realistic) data.
+//  * four independent accumulators per wave; a 32x32x16 bf16 MFMA issues every 32 cycles per SIMD
+//    = 1024 FLOP/clk/SIMD -> 2.5 PF dense at 2.4 GHz on 256 CUs.
+//  * dtype variants: bf16 32x32x16, bf16 16x16x32, f32-input 32x32x2 (exact fp32, 1/16 rate),
+//    fp8 e4m3 32x32x16 (bf16 rate, non-scaled form).
+//  * census: each workgroup records HW_REG_HW_ID (CU/SE ids) and HW_REG_XCC_ID so CU-mask bit ->
+//    XCD placement can be verified on the box.
+#include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace {
+thread_local std::string g_err;
+
+int check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return int(e);
+}
+
+constexpr int kThreads = 256;
+constexpr int kLdsVec = 1024;  // uint4 entries = 16 KiB of operand tiles per workgroup
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+template <int DTYPE>
+__global__ __launch_bounds__(kThreads) void mfma_probe(const uint4* __restrict__ src, uint32_t src_len,
+                                                      float* __restrict__ out, int iters) {
+  __shared__ uint4 lds[kLdsVec];
+  const int t = threadIdx.x;
+  for (int i = t; i < kLdsVec; i += kThreads) lds[i] = src[(blockIdx.x * 131u + i) % src_len];
+  __syncthreads();
+
+  float result = 0.f;
+  if constexpr (DTYPE == 0) {  // bf16 32x32x16
+    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
+    for (int it = 0; it < iters; ++it) {
+      uint4 a = lds[(t + it * 37) & (kLdsVec - 1)];
+      uint4 b = lds[(t + it * 53 + 512) & (kLdsVec - 1)];
+      bf16x8 A = as_bf16x8(a), B = as_bf16x8(b);
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(B, A, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, A, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(B, B, c3, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
+  } else if constexpr (DTYPE == 1) {  // bf16 16x16x32
+    f32x4 c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = f32x4{0, 0, 0, 0};
+    for (int it = 0; it < iters; ++it) {
+      uint4 a = lds[(t + it * 37) & (kLdsVec - 1)];
+      uint4 b = lds[(t + it * 53 + 512) & (kLdsVec - 1)];
+      bf16x8 A = as_bf16x8(a), B = as_bf16x8(b);
+#pragma unroll
+      for (int k = 0; k < 8; k += 2) {
+        c[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, c[k], 0, 0, 0);
+        c[k + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B, A, c[k + 1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) result += c[k][0] + c[k][1] + c[k][2] + c[k][3];
+  } else if constexpr (DTYPE == 2) {  // f32-input 32x32x2 (exact fp32)
+    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
+    const float* ldsf = reinterpret_cast<const float*>(lds);
+    for (int it = 0; it < iters; ++it) {
+      float a = ldsf[(t + it * 37) & (4 * kLdsVec - 1)];
+      float b = ldsf[(t + it * 53 + 2048) & (4 * kLdsVec - 1)];
+      c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, b, c3, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
+  } else {  // fp8 e4m3 32x32x16
+    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
+    const long* ldsl = reinterpret_cast<const long*>(lds);
+    for (int it = 0; it < iters; ++it) {
+      long a = ldsl[(t + it * 37) & (2 * kLdsVec - 1)];
+      long b = ldsl[(t + it * 53 + 1024) & (2 * kLdsVec - 1)];
+      c0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c0, 0, 0, 0);
+      c1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(b, a, c1, 0, 0, 0);
+      c2 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, a, c2, 0, 0, 0);
+      c3 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(b, b, c3, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
+  }
+  out[blockIdx.x * kThreads + t] = result;
+}
+
+// FLOP per loop iteration per wave for each dtype variant
+constexpr double kFlopPerIterWave[4] = {4.0 * 2 * 32 * 32 * 16, 8.0 * 2 * 16 * 16 * 32, 4.0 * 2 * 32 * 32 * 2,
+                                        4.0 * 2 * 32 * 32 * 16};
+
+__global__ __launch_bounds__(kThreads) void hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
+  size_t i = size_t(blockIdx.x) * kThreads + threadIdx.x;
+  const size_t stride = size_t(gridDim.x) * kThreads;
+  for (; i + 3 * stride < n; i += 4 * stride) {  // 4 x 16 B in flight per lane
+    uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a; dst[i + stride] = b; dst[i + 2 * stride] = c; dst[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void fill_random(uint32_t* p, size_t n, uint32_t seed) {
+  size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t stride = size_t(gridDim.x) * blockDim.x;
+  for (; i < n; i += stride) {
+    uint32_t x = uint32_t(i) * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    // keep bf16/fp8 lanes finite and in [-1, 1): clear the top exponent bits of each 16-bit half
+    p[i] = x & 0xBF7FBF7Fu;
+  }
+}
+
+__global__ void census(uint32_t* out, int spin) {
+  if (threadIdx.x == 0) {
+    uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    out[2 * blockIdx.x] = hw;
+    out[2 * blockIdx.x + 1] = xcc;
+  }
+  // hold the CU briefly so that the dispatcher spreads the grid over every enabled CU
+  for (volatile int i = 0; i < spin; ++i) {
+  }
+}
+
+struct Scratch {
+  int device = -1;
+  uint4* src = nullptr;
+  uint32_t src_len = 0;
+  float* out = nullptr;
+  size_t out_len = 0;
+};
+thread_local Scratch g_s;
+
+int ensure_scratch(int device, int n_wg) {
+  if (g_s.device != device) {
+    g_s = Scratch{};
+    g_s.device = device;
+  }
+  if (!g_s.src) {
+    g_s.src_len = 1u << 16;  // 1 MiB of random operands
+    if (int rc = check(hipMalloc(&g_s.src, size_t(g_s.src_len) * sizeof(uint4)), "hipMalloc src")) return rc;
+    hipLaunchKernelGGL(fill_random, dim3(256), dim3(256), 0, 0, reinterpret_cast<uint32_t*>(g_s.src),
+                       size_t(g_s.src_len) * 4, 0x9E3779B9u);
+    if (int rc = check(hipGetLastError(), "fill_random")) return rc;
+  }
+  size_t need = size_t(n_wg) * kThreads;
+  if (g_s.out_len < need) {
+    if (g_s.out) hipFree(g_s.out);
+    if (int rc = check(hipMalloc(&g_s.out, need * sizeof(float)), "hipMalloc out")) return rc;
+    g_s.out_len = need;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+struct nos_probe_result {
+  double ms;       // best-of-reps kernel time
+  double flops;    // FLOP (or bytes moved for the HBM probe) per launch
+  double rate;     // TFLOP/s (or GB/s)
+  int32_t n_wg;
+};
+
+const char* nos_probe_last_error() { return g_err.c_str(); }
+
+int nos_probe_device_count(int* n) { return check(hipGetDeviceCount(n), "hipGetDeviceCount"); }
+
+int nos_probe_cu_count(int device, int* n) {
+  hipDeviceProp_t p;
+  if (int rc = check(hipGetDeviceProperties(&p, device), "hipGetDeviceProperties")) return rc;
+  *n = p.multiProcessorCount;
+  return 0;
+}
+
+// CU-masked stream (hipExtStreamCreateWithCUMask, hip_runtime_api.h:2999). n_words == 0 -> plain
+// non-blocking stream.
+int nos_stream_create(int device, const uint32_t* mask, uint32_t n_words, void** stream_out) {
+  if (int rc = check(hipSetDevice(device), "hipSetDevice")) return rc;
+  hipStream_t s = nullptr;
+  if (n_words > 0) {
+    if (int rc = check(hipExtStreamCreateWithCUMask(&s, n_words, mask), "hipExtStreamCreateWithCUMask")) return rc;
+  } else {
+    if (int rc = check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate")) return rc;
+  }
+  *stream_out = s;
+  return 0;
+}
+
+int nos_stream_get_cumask(void* stream, uint32_t n_words, uint32_t* mask) {
+  return check(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), n_words, mask), "hipExtStreamGetCUMask");
+}
+
+int nos_stream_destroy(void* stream) {
+  return check(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)), "hipStreamDestroy");
+}
+
+int nos_probe_mfma(int device, void* stream, int dtype, int n_wg, int iters, int reps, nos_probe_result* res) {
+  if (dtype < 0 || dtype > 3 || n_wg <= 0 || iters <= 0 || reps <= 0) {
+    g_err = "invalid probe arguments";
+    return -1;
+  }
+  if (int rc = check(hipSetDevice(device), "hipSetDevice")) return rc;
+  if (int rc = ensure_scratch(device, n_wg)) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  auto launch = [&]() {
+    switch (dtype) {
+      case 0: hipLaunchKernelGGL(mfma_probe<0>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
+      case 1: hipLaunchKernelGGL(mfma_probe<1>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
+      case 2: hipLaunchKernelGGL(mfma_probe<2>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
+      default: hipLaunchKernelGGL(mfma_probe<3>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
+    }
+  };
+  launch();  // warm-up (code object load, clocks)
+  if (int rc = check(hipStreamSynchronize(s), "warm-up")) return rc;
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    hipEventRecord(e0, s);
+    launch();
+    hipEventRecord(e1, s);
+    if (int rc = check(hipEventSynchronize(e1), "probe")) return rc;
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) best = ms;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  res->ms = best;
+  res->flops = kFlopPerIterWave[dtype] * double(iters) * double(n_wg) * (kThreads / 64);
+  res->rate = res->flops / (best * 1e-3) / 1e12;
+  res->n_wg = n_wg;
+  return 0;
+}
+
+int nos_probe_hbm(int device, void* stream, size_t bytes, int n_wg, int reps, nos_probe_result* res) {
+  if (int rc = check(hipSetDevice(device), "hipSetDevice")) return rc;
+  size_t n = bytes / sizeof(uint4);
+  uint4 *a = nullptr, *b = nullptr;
+  if (int rc = check(hipMalloc(&a, n * sizeof(uint4)), "hipMalloc a")) return rc;
+  if (int rc = check(hipMalloc(&b, n * sizeof(uint4)), "hipMalloc b")) { hipFree(a); return rc; }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fill_random, dim3(1024), dim3(256), 0, s, reinterpret_cast<uint32_t*>(a), n * 4, 1234u);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipLaunchKernelGGL(hbm_copy, dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+  int rc = check(hipStreamSynchronize(s), "hbm warm-up");
+  float best = 1e30f;
+  for (int r = 0; r < reps && rc == 0; ++r) {
+    hipEventRecord(e0, s);
+    hipLaunchKernelGGL(hbm_copy, dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+    hipEventRecord(e1, s);
+    rc = check(hipEventSynchronize(e1), "hbm probe");
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (ms < best) best = ms;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(a);
+  hipFree(b);
+  if (rc) return rc;
+  res->ms = best;
+  res->flops = 2.0 * double(n) * sizeof(uint4);
+  res->rate = res->flops / (best * 1e-3) / 1e9;
+  res->n_wg = n_wg;
+  return 0;
+}
+
+int nos_probe_census(int device, void* stream, int n_wg, int spin, uint32_t* host_out) {
+  if (int rc = check(hipSetDevice(device), "hipSetDevice")) return rc;
+  uint32_t* d = nullptr;
+  if (int rc = check(hipMalloc(&d, size_t(n_wg) * 2 * sizeof(uint32_t)), "hipMalloc census")) return rc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(census, dim3(n_wg), dim3(64), 0, s, d, spin);
+  int rc = check(hipStreamSynchronize(s), "census");
+  if (rc == 0) rc = check(hipMemcpy(host_out, d, size_t(n_wg) * 2 * sizeof(uint32_t), hipMemcpyDeviceToHost), "census copy");
+  hipFree(d);
+  return rc;
+}
+
+}  // extern "C"

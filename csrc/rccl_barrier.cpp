@@ -1,0 +1,96 @@
+// nos node-atomic commit barrier over RCCL (xGMI).
+//
+// After the partition agent has applied a plan to every GPU of its node it must not publish the new
+// status (the plan-ID commit marker, reference annotations.go:25-28) until every logical device is
+// alive and the fabric between them is reachable. One 4-byte ncclAllReduce(sum) over a communicator
+// spanning the node's devices is that barrier: each rank contributes 1 if its local apply+verify
+// succeeded, so the sum equals nranks iff the whole node committed.
+//
+// The communicator is created per commit and destroyed before the next mode flip, because a flip
+// re-enumerates devices and invalidates every handle. A 4-byte all-reduce is latency bound (tens of
+// microseconds), so link bandwidth (7 x ~153 GB/s xGMI per GPU) is irrelevant here.
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+namespace {
+thread_local std::string g_err;
+
+int nccl_check(ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return 0;
+  g_err = std::string(what) + ": " + ncclGetErrorString(r);
+  return int(r) + 1000;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return int(e);
+}
+
+struct Barrier {
+  ncclComm_t comm = nullptr;
+  hipStream_t stream = nullptr;
+  int32_t* dbuf = nullptr;
+  int device = 0;
+};
+}  // namespace
+
+extern "C" {
+
+const char* nos_barrier_last_error() { return g_err.c_str(); }
+
+int nos_barrier_id_size() { return int(sizeof(ncclUniqueId)); }
+
+int nos_barrier_unique_id(char* out, int len) {
+  if (len < int(sizeof(ncclUniqueId))) {
+    g_err = "buffer too small for ncclUniqueId";
+    return -1;
+  }
+  ncclUniqueId id;
+  if (int rc = nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId")) return rc;
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+int nos_barrier_init(int nranks, int rank, const char* id_bytes, int device, void** handle) {
+  auto* b = new Barrier();
+  b->device = device;
+  if (int rc = hip_check(hipSetDevice(device), "hipSetDevice")) { delete b; return rc; }
+  if (int rc = hip_check(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), "hipStreamCreate")) { delete b; return rc; }
+  if (int rc = hip_check(hipMalloc(&b->dbuf, sizeof(int32_t)), "hipMalloc")) { delete b; return rc; }
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  if (int rc = nccl_check(ncclCommInitRank(&b->comm, nranks, id, rank), "ncclCommInitRank")) {
+    (void)hipFree(b->dbuf);
+    delete b;
+    return rc;
+  }
+  *handle = b;
+  return 0;
+}
+
+// value: this rank's vote (1 = committed). result: the sum over ranks.
+int nos_barrier_allreduce(void* handle, int32_t value, int32_t* result) {
+  auto* b = static_cast<Barrier*>(handle);
+  if (int rc = hip_check(hipSetDevice(b->device), "hipSetDevice")) return rc;
+  if (int rc = hip_check(hipMemcpyAsync(b->dbuf, &value, sizeof(value), hipMemcpyHostToDevice, b->stream), "h2d")) return rc;
+  if (int rc = nccl_check(ncclAllReduce(b->dbuf, b->dbuf, 1, ncclInt32, ncclSum, b->comm, b->stream), "ncclAllReduce")) return rc;
+  if (int rc = hip_check(hipMemcpyAsync(result, b->dbuf, sizeof(int32_t), hipMemcpyDeviceToHost, b->stream), "d2h")) return rc;
+  return hip_check(hipStreamSynchronize(b->stream), "hipStreamSynchronize");
+}
+
+int nos_barrier_destroy(void* handle) {
+  auto* b = static_cast<Barrier*>(handle);
+  int rc = 0;
+  if (b->comm) rc = nccl_check(ncclCommDestroy(b->comm), "ncclCommDestroy");
+  if (b->dbuf) (void)hipFree(b->dbuf);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+  return rc;
+}
+
+}  // extern "C"

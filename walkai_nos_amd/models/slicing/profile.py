@@ -1,0 +1,90 @@
+"""CU-mask slice profiles (the MPS analogue on MI355X).
+
+Reference: ``pkg/gpu/slicing/profile.go`` (memory-only profiles ``<N>gb``, resource
+``nvidia.com/gpu-<N>gb``, regex at ``:31``) and ``constant.go:22-24`` (``MinSliceMemoryGB=1``,
+replica separator ``::``).
+
+A slice here has two dimensions:
+
+* ``<m>gb``          — an HBM budget of *m* GB, compute shared with the other shared slices
+  (exactly the reference's MPS semantics: "compute shared equally");
+* ``<c>cu.<m>gb``    — *c* dedicated CUs (a disjoint CU mask, multiple of :data:`CU_GRANULARITY`,
+  placed XCD-aligned where possible) plus *m* GB of HBM.
+
+Resource names are ``amd.com/gpu-<profile>``; profiles contain no ``-``.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass
+from functools import total_ordering
+from typing import Optional
+
+from ... import constant
+
+MIN_SLICE_MEMORY_GB = 1
+#: CU-mask granularity: one shader engine of gfx950 (256 CUs / 32 SEs)
+CU_GRANULARITY = 8
+#: CUs always left to the shared pool when memory-only slices exist
+MIN_SHARED_CUS = 8
+REPLICA_SEPARATOR = "::"
+
+_PROFILE_RE = re.compile(r"^(?:(\d+)cu\.)?(\d+)gb$")
+
+
+@total_ordering
+@dataclass(frozen=True)
+class SliceProfile:
+    memory_gb: int
+    cus: int = 0  # 0 => shared compute
+
+    @property
+    def name(self) -> str:
+        return f"{self.cus}cu.{self.memory_gb}gb" if self.cus else f"{self.memory_gb}gb"
+
+    @property
+    def resource_name(self) -> str:
+        return constant.RESOURCE_SLICE_PREFIX + self.name
+
+    @property
+    def dedicated(self) -> bool:
+        return self.cus > 0
+
+    def __lt__(self, other: "SliceProfile") -> bool:
+        return (self.memory_gb, self.cus) < (other.memory_gb, other.cus)
+
+    def __str__(self) -> str:
+        return self.name
+
+
+def parse_profile(name: str) -> SliceProfile:
+    m = _PROFILE_RE.match(name)
+    if not m:
+        raise ValueError(f"invalid slice profile {name!r}")
+    return SliceProfile(int(m.group(2)), int(m.group(1) or 0))
+
+
+def is_valid_profile(name: str) -> bool:
+    return bool(_PROFILE_RE.match(name))
+
+
+def new_profile(memory_gb: int, cus: int = 0) -> str:
+    return SliceProfile(memory_gb, cus).name
+
+
+def is_slice_resource(resource_name: str) -> bool:
+    return bool(constant.RESOURCE_SLICE_REGEX.match(resource_name))
+
+
+def extract_profile_name(resource_name: str) -> Optional[str]:
+    m = constant.RESOURCE_SLICE_REGEX.match(resource_name)
+    return m.group(1) if m else None
+
+
+def as_resource_name(profile: str) -> str:
+    return constant.RESOURCE_SLICE_PREFIX + profile
+
+
+def extract_gpu_id(device_id: str) -> str:
+    """Strip the replica suffix: ``<uuid>::<n>`` -> ``<uuid>`` (reference ``util.go:51-57``)."""
+    return device_id.split(REPLICA_SEPARATOR, 1)[0]

@@ -1,0 +1,62 @@
+"""Compute-partition node model: a :class:`PartitionedNode` built from a Node object.
+
+Reference ``pkg/gpu/mig/node.go:40-100`` builds GPUs from the status annotations grouped by index
+and then appends empty GPUs for the *count* of missing ones starting at ``len(annotated)`` —
+which silently assumes annotated indexes are ``0..n-1``.  Here missing indexes are filled exactly.
+The allowed geometries are the model's geometries for the node's current NPS mode.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Mapping
+
+from ...kube import objects as ko
+from .. import annotation as ann
+from .. import gpu_util
+from .. import resource as res
+from ..partitioned import PartitionedGPU, PartitionedNode
+from .known_configs import get_allowed_geometries
+from .profile import as_resource_name, extract_profile_name, is_xcp_resource
+
+
+def new_gpu(model: str, index: int, nps: str, used: Mapping[str, int] | None = None,
+            free: Mapping[str, int] | None = None) -> PartitionedGPU:
+    allowed = get_allowed_geometries(model, nps)
+    if allowed is None:
+        raise ValueError(f"model {model!r} is not associated with any known GPU")
+    return PartitionedGPU(model, index, allowed, dict(used or {}), dict(free or {}))
+
+
+def new_node(node: Dict[str, Any]) -> PartitionedNode:
+    model = gpu_util.get_model(node)
+    count = gpu_util.get_count(node)
+    nps = gpu_util.get_memory_partition(node)
+    status, _ = ann.parse_node_annotations(ko.annotations(node))
+    gpus: Dict[int, PartitionedGPU] = {}
+    for idx, items in sorted(ann.group_by_gpu_index(status).items()):
+        used = {a.profile: a.quantity for a in items if a.is_used()}
+        free = {a.profile: a.quantity for a in items if a.is_free()}
+        gpus[idx] = new_gpu(model, idx, nps, used, free)
+    for i in range(count):
+        if i not in gpus:
+            gpus[i] = new_gpu(model, i, nps)
+    allocatable = res.from_k8s(ko.node_allocatable(node))
+    return PartitionedNode(ko.name(node), [gpus[i] for i in sorted(gpus)], allocatable,
+                           is_resource=is_xcp_resource, as_resource=as_resource_name)
+
+
+def get_requested_profiles(pod: Dict[str, Any]) -> Dict[str, int]:
+    """Compute-partition profiles requested by a pod (reference ``GetRequestedProfiles``)."""
+    out: Dict[str, int] = {}
+    for r, q in res.compute_pod_request(pod).items():
+        p = extract_profile_name(r)
+        if p is not None and q > 0:
+            out[p] = out.get(p, 0) + q
+    return out
+
+
+def requested_profiles_list(pods: List[Dict[str, Any]]) -> Dict[str, int]:
+    out: Dict[str, int] = {}
+    for p in pods:
+        for k, v in get_requested_profiles(p).items():
+            out[k] = out.get(k, 0) + v
+    return out
