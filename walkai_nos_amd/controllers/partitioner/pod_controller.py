@@ -1,0 +1,216 @@
+"""Partitioner pod controller (reference ``internal/controllers/gpupartitioner/mig_controller.go:37-213``).
+
+Per Pod event: consider the pod only if it is Pending, unbound and ``PodScheduled=False`` with
+reason ``Unschedulable`` (B.8); read the partition profiles it requests; list the nodes opted in
+with ``nos.nebuly.com/gpu-partitioning=<kind>``; if every requested profile is already *free*
+somewhere do nothing; otherwise re-plan and write the new spec annotations with a fresh plan ID.
+
+Deliberate changes vs the reference:
+
+* Q1 — the "already present" check looks at **free** capacity; the reference also counts used
+  devices, so a pod never triggers repartitioning once every device of its profile is in use;
+* Q11 — planning is **batched**: all currently pending pods of the same kind are planned together
+  after the batch window (``batchWindowTimeoutSeconds`` / ``batchWindowIdleSeconds``), and nodes
+  are **scored** (profiles provided, then fewest GPUs whose geometry changes, then name) instead of
+  "first node that can change wins";
+* Q14 — when no node can help, the pod is requeued with back-off instead of waiting for an
+  unrelated event.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Any, Callable, Dict, List, Mapping, Optional, Tuple, Union
+
+from ...api import v1alpha1 as api
+from ...kube import objects as ko
+from ...kube.errors import NotFound
+from ...kube.runtime import Request, Result
+from ...models import annotation as ann
+from ...models.partitioned import PartitionedNode
+from ...models.slicing import gpu as slicing_gpu
+from ...models.slicing.gpu import SlicingNode
+from ...models.xcp import node as xcp_node
+from ...partitioning.planner import Partitioner, build_node_partitioning, new_plan_id
+from ...utils import pod as podutil
+from ...utils.metrics import REGISTRY
+
+log = logging.getLogger("nos.partitioner")
+
+NodeModel = Union[PartitionedNode, SlicingNode]
+
+
+def requested_profiles(kind: str, pod: Dict[str, Any]) -> Dict[str, int]:
+    if kind == api.PARTITIONING_KIND_XCP:
+        return xcp_node.get_requested_profiles(pod)
+    return slicing_gpu.get_requested_profiles(pod)
+
+
+def new_node_model(kind: str, node: Dict[str, Any]) -> NodeModel:
+    if kind == api.PARTITIONING_KIND_XCP:
+        return xcp_node.new_node(node)
+    return slicing_gpu.new_node(node)
+
+
+def _changed_gpus(before: NodeModel, after: NodeModel) -> int:
+    return sum(1 for a, b in zip(before.gpus, after.gpus) if a.geometry() != b.geometry())
+
+
+def plan_cluster(models: Mapping[str, NodeModel], required: Mapping[str, int]) -> Dict[str, NodeModel]:
+    """Greedy over nodes with a score: provided profiles desc, GPUs changed asc, node name asc."""
+    remaining = {p: q for p, q in required.items() if q > 0}
+    current = dict(models)
+    changed: Dict[str, NodeModel] = {}
+    while remaining:
+        best: Optional[Tuple[Tuple[int, int, str], str, NodeModel]] = None
+        for name, m in sorted(current.items()):
+            cand = m.clone()
+            before_free = m.free()
+            if not cand.update_geometry_for(remaining):
+                continue
+            after_free = cand.free()
+            provided = sum(min(max(0, after_free.get(p, 0) - before_free.get(p, 0)), q) for p, q in remaining.items())
+            if provided <= 0:
+                continue
+            score = (-provided, _changed_gpus(m, cand), name)
+            if best is None or score < best[0]:
+                best = (score, name, cand)
+        if best is None:
+            break
+        _, name, cand = best
+        before_free = current[name].free()
+        current[name] = cand
+        changed[name] = cand
+        after_free = cand.free()
+        for p in list(remaining):
+            remaining[p] -= max(0, after_free.get(p, 0) - before_free.get(p, 0))
+            if remaining[p] <= 0:
+                del remaining[p]
+    return changed
+
+
+class PodController:
+    def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
+                 clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
+                 retry_after: float = 5.0):
+        self.client = client
+        self.kind = kind
+        self.partitioner = partitioner or Partitioner(client)
+        self.clock = clock
+        self.batch_timeout = batch_timeout
+        self.batch_idle = batch_idle
+        self.retry_after = retry_after
+        self._window_start: Optional[float] = None
+        self._window_last: Optional[float] = None
+        self.plans_written = 0
+
+    # -- helpers -------------------------------------------------------------------------
+    def should_consider(self, pod: Dict[str, Any]) -> bool:
+        return podutil.is_pending(pod) and not podutil.is_scheduled(pod) and podutil.is_unschedulable(pod)
+
+    def list_nodes(self) -> List[Dict[str, Any]]:
+        return self.client.list("Node", label_selector=f"{api.LABEL_GPU_PARTITIONING}={self.kind}")
+
+    def pending_requests(self) -> Dict[str, int]:
+        out: Dict[str, int] = {}
+        for p in self.client.list("Pod"):
+            if not self.should_consider(p):
+                continue
+            for k, v in requested_profiles(self.kind, p).items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def _models(self, nodes: List[Dict[str, Any]]) -> Dict[str, NodeModel]:
+        out: Dict[str, NodeModel] = {}
+        for n in nodes:
+            try:
+                out[ko.name(n)] = new_node_model(self.kind, n)
+            except ValueError as e:
+                log.warning("skipping node %s: %s", ko.name(n), e)
+        return out
+
+    @staticmethod
+    def in_flight(node: Dict[str, Any]) -> bool:
+        """A plan was written but the agent has not reported it yet (spec plan != status plan).
+        The reference re-plans such nodes on every pod event, rewriting the spec
+        with a new plan ID each time; here they are left alone until the agent reports."""
+        a = ko.annotations(node)
+        spec = a.get(api.ANNOTATION_PARTITIONING_PLAN)
+        return bool(spec) and spec != a.get(api.ANNOTATION_REPORTED_PARTITIONING_PLAN)
+
+    def incoming_free(self, node: Dict[str, Any]) -> Dict[str, int]:
+        """Capacity an in-flight plan will provide: spec quantities minus what is used now."""
+        status, spec = ann.parse_node_annotations(ko.annotations(node))
+        used: Dict[Tuple[int, str], int] = {}
+        for s in status:
+            if s.is_used():
+                used[(s.index, s.profile)] = used.get((s.index, s.profile), 0) + s.quantity
+        out: Dict[str, int] = {}
+        for s in spec:
+            q = s.quantity - used.get((s.index, s.profile), 0)
+            if q > 0:
+                out[s.profile] = out.get(s.profile, 0) + q
+        return out
+
+    @staticmethod
+    def free_somewhere(models: Mapping[str, NodeModel], requested: Mapping[str, int]) -> bool:
+        for p, q in requested.items():
+            if sum(m.free().get(p, 0) for m in models.values()) < q:
+                return False
+        return True
+
+    # -- reconcile ----------------------------------------------------------------------
+    def reconcile(self, req: Request) -> Result:
+        try:
+            pod = self.client.get("Pod", req.name, req.namespace)
+        except NotFound:
+            return Result()
+        if not self.should_consider(pod):
+            return Result()
+        requested = requested_profiles(self.kind, pod)
+        if not requested:
+            return Result()
+        now = self.clock()
+        if self.batch_timeout > 0:
+            if self._window_start is None:
+                self._window_start = now
+            self._window_last = now if self._window_last is None else self._window_last
+            deadline = min(self._window_start + self.batch_timeout, self._window_last + max(self.batch_idle, 1e-9))
+            if now < deadline:
+                self._window_last = now
+                return Result(requeue_after=deadline - now)
+            self._window_start = self._window_last = None
+        t0 = time.perf_counter()
+        nodes = self.list_nodes()
+        flying = [n for n in nodes if self.in_flight(n)]
+        settled = [n for n in nodes if not self.in_flight(n)]
+        models = self._models(settled)
+        # free capacity = settled nodes' free partitions + what in-flight plans will provide
+        free_total: Dict[str, int] = {}
+        for m in models.values():
+            for p, q in m.free().items():
+                free_total[p] = free_total.get(p, 0) + q
+        for n in flying:
+            for p, q in self.incoming_free(n).items():
+                free_total[p] = free_total.get(p, 0) + q
+        if all(free_total.get(p, 0) >= q for p, q in requested.items()):
+            log.debug("pod %s/%s: requested profiles free (or incoming), nothing to do", req.namespace, req.name)
+            if flying:
+                return Result(requeue_after=self.retry_after)
+            return Result()
+        pending = self.pending_requests() or requested
+        need = {p: q - free_total.get(p, 0) for p, q in pending.items() if q - free_total.get(p, 0) > 0}
+        if not need:
+            return Result()
+        changed = plan_cluster(models, need)
+        REGISTRY.phase_seconds.labels(phase="plan").observe(time.perf_counter() - t0)
+        if not changed:
+            log.info("pod %s/%s: no node can provide %s", req.namespace, req.name, need)
+            return Result(requeue_after=self.retry_after)
+        by_name = {ko.name(n): n for n in nodes}
+        for name, model in changed.items():
+            plan_id = new_plan_id(self.clock)
+            self.partitioner.apply_partitioning(by_name[name], plan_id, build_node_partitioning(model))
+            REGISTRY.repartitions.labels(node=name, kind=self.kind).inc()
+            self.plans_written += 1
+        return Result()

@@ -1,0 +1,29 @@
+"""Wire the gpupartitioner's controllers (``cmd/gpupartitioner/gpupartitioner.go:90-104``)."""
+from __future__ import annotations
+
+from typing import Optional
+
+from ... import constant
+from ...api import v1alpha1 as api
+from ...kube.runtime import Manager, Watch
+from ...partitioning.planner import NodeInitializer, Partitioner
+from ...utils.predicates import HasLabel
+from .node_controller import NodeController
+from .pod_controller import PodController
+
+
+def setup_partitioner(mgr: Manager, kinds=(api.PARTITIONING_KIND_XCP, api.PARTITIONING_KIND_CUMASK),
+                      batch_timeout: float = 0.0, batch_idle: float = 0.0, retry_after: float = 5.0,
+                      partitioner: Optional[Partitioner] = None):
+    partitioner = partitioner or Partitioner(mgr.client)
+    pod_ctrls = []
+    for kind in kinds:
+        pc = PodController(mgr.client, kind, partitioner, clock=mgr.clock, batch_timeout=batch_timeout,
+                           batch_idle=batch_idle, retry_after=retry_after)
+        # MaxConcurrentReconciles = 1: one writer per kind (mig_controller.go:204)
+        mgr.new_controller(f"{constant.CLUSTER_PARTITIONER_CONTROLLER}-{kind}", pc.reconcile, [Watch("Pod")], 1)
+        pod_ctrls.append(pc)
+    nc = NodeController(mgr.client, NodeInitializer(mgr.client, partitioner, clock=mgr.clock))
+    mgr.new_controller(constant.NODE_INITIALIZER_CONTROLLER, nc.reconcile,
+                       [Watch("Node", [HasLabel(api.LABEL_GPU_PARTITIONING)])], 5)
+    return pod_ctrls, nc
