@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Benchmark driver contract: ``python bench.py --gpus N --steps K --warmup W``.
+
+Runs the flagship step (see :mod:`walkai_nos_amd.bench_core`): a node of N MI355X GPUs (one
+process per GPU under torchrun, RCCL over xGMI for the partition-commit barrier) serving a
+churning mix of 1/8, 1/2 and 1/1-GPU YOLOS-small inference pods through the nos control plane.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--load", type=float, default=1.25, help="offered GPU-equivalents per GPU")
+    ap.add_argument("--backend", choices=("hip", "torch"), default="hip")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=300))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using {world}", file=sys.stderr)
+    gpus = world if world > 1 else args.gpus
+    if gpus > 1 and world == 1:
+        print("multi-GPU runs are launched with torchrun (one process per GPU)", file=sys.stderr)
+        return 2
+
+    from walkai_nos_amd.bench_core import BenchConfig, run_bench
+    cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
+                      backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world)
+    res = run_bench(cfg)
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

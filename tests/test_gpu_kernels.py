@@ -1,0 +1,114 @@
+"""Numerics of the HIP workload kernels vs plain PyTorch fp32 references (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from walkai_nos_amd.ops import kernels
+    assert kernels.hip_available(), "libnos_kernels.so must be built on a GPU box"
+    kernels.set_backend("hip")
+    return kernels
+
+
+def _ref_attention(qkv, H, Dh, scale):
+    B, T, _ = qkv.shape
+    q, k, v = qkv.double().view(B, T, 3, H, Dh).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) * scale
+    p = torch.softmax(s, dim=-1)
+    return (p @ v).transpose(1, 2).reshape(B, T, H * Dh).float()
+
+
+@pytest.mark.parametrize("B,T,H", [(1, 32, 1), (1, 77, 2), (2, 300, 3), (1, 3401, 6)])
+def test_attention_matches_fp64_reference(K, B, T, H):
+    torch.manual_seed(0)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    out = K.attention_qkv(qkv, H, 64, 1.0 / 8.0)
+    torch.cuda.synchronize()
+    ref = _ref_attention(qkv, H, 64, 1.0 / 8.0)
+    err = (out - ref).abs().max().item()
+    assert err < 2e-5, err
+
+
+def test_attention_asymmetric_values_catch_transposes(K):
+    # V with distinct per-(key, dim) values and a peaked softmax: a swapped layout cannot pass
+    T, H = 96, 1
+    qkv = torch.zeros(1, T, 3 * 64, device="cuda")
+    qkv[0, :, :64] = torch.randn(T, 64, device="cuda") * 4
+    qkv[0, :, 64:128] = torch.randn(T, 64, device="cuda") * 4
+    qkv[0, :, 128:] = torch.arange(T * 64, device="cuda", dtype=torch.float32).view(T, 64) / 1000
+    out = K.attention_qkv(qkv, H, 64, 0.125)
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    assert (out - ref).abs().max().item() < 1e-4
+
+
+def test_attention_split_matches_unsplit(K):
+    import ctypes
+    torch.manual_seed(1)
+    B, T, H = 1, 1000, 2
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    L = K._L()
+    L.nos_attention_f32_split.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
+    for ns in (2, 3, 7):
+        out = torch.empty(B, T, H * 64, device="cuda")
+        rc = L.nos_attention_f32_split(qkv.data_ptr(), out.data_ptr(), B, T, H, 64, 0.125, ns,
+                                       torch.cuda.current_stream().cuda_stream)
+        assert rc == 0
+        torch.cuda.synchronize()
+        assert (out - ref).abs().max().item() < 2e-5
+
+
+@pytest.mark.parametrize("D", [384, 768, 1024])
+def test_layernorm(K, D):
+    torch.manual_seed(0)
+    x = torch.randn(3401, D, device="cuda") * 3 + 1
+    w = torch.randn(D, device="cuda")
+    b = torch.randn(D, device="cuda")
+    out = K.layernorm(x, w, b, 1e-12)
+    ref = F.layer_norm(x.double(), (D,), w.double(), b.double(), 1e-12).float()
+    assert (out - ref).abs().max().item() < 1e-4
+
+
+def test_linear_gelu(K):
+    torch.manual_seed(0)
+    x = torch.randn(3401, 384, device="cuda")
+    w = torch.randn(1536, 384, device="cuda") * 0.05
+    b = torch.randn(1536, device="cuda")
+    out = K.linear_gelu(x, w, b)
+    h = x.double() @ w.double().t() + b.double()
+    ref = (0.5 * h * (1 + torch.erf(h / math.sqrt(2)))).float()
+    assert (out - ref).abs().max().item() < 1e-3
+
+
+def test_linear_residual(K):
+    torch.manual_seed(0)
+    x = torch.randn(1, 3401, 1536, device="cuda")
+    w = torch.randn(384, 1536, device="cuda") * 0.02
+    b = torch.randn(384, device="cuda")
+    r = torch.randn(1, 3401, 384, device="cuda")
+    out = K.linear_residual(x, w, b, r)
+    ref = (r.double() + x.double() @ w.double().t() + b.double()).float()
+    assert (out - ref).abs().max().item() < 1e-3
+
+
+def test_yolos_hip_matches_torch_backend(K):
+    from walkai_nos_amd.models.workload.yolos import YolosSmall, demo_input
+    m = YolosSmall().cuda().eval()
+    x = demo_input(1, (800, 1066), "cuda")
+    with torch.no_grad():
+        K.set_backend("torch")
+        ref_l, ref_b = m(x)
+        K.set_backend("hip")
+        l, bx = m(x)
+    torch.cuda.synchronize()
+    assert (l - ref_l).abs().max().item() < 1e-3
+    assert (bx - ref_b).abs().max().item() < 1e-4

@@ -1,0 +1,96 @@
+"""Native components on a real MI355X: amd-smi backend (read-only), slice probe, CU-masked
+streams, RCCL commit barrier, HBM-limit shim (GPU only)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return 0
+
+
+def test_amdsmi_inventory_and_modes(gpu):
+    from walkai_nos_amd.device.amdsmi import COMPUTE_MODE_NAMES, MEMORY_MODE_NAMES, NativeAmdSmi
+    smi = NativeAmdSmi()
+    gpus = smi.list_gpus()
+    assert gpus, "amd-smi sees no GPU"
+    g = gpus[0]
+    assert g.cu_count in (0, 256, 304) and g.vram_bytes > 100 * 10**9
+    assert smi.get_compute_partition(g.index) in COMPUTE_MODE_NAMES
+    assert smi.get_memory_partition(g.index) in MEMORY_MODE_NAMES
+    assert smi.process_count(g.index) >= 0
+    assert smi.gpu_index_of(g.bdf) == g.index
+
+
+def test_amdsmi_set_requires_root(gpu):
+    from walkai_nos_amd.device.amdsmi import NativeAmdSmi
+    from walkai_nos_amd.models.errors import GpuError
+    if os.geteuid() == 0:
+        pytest.skip("running as root: would really flip the partition mode")
+    smi = NativeAmdSmi()
+    with pytest.raises(GpuError) as ei:
+        smi.set_compute_partition(0, "CPX")
+    assert ei.value.code == GpuError.PERMISSION
+
+
+def test_probe_rates_are_plausible(gpu):
+    from walkai_nos_amd.ops import probe
+    bf = probe.probe_mfma("bf16", iters=2048, reps=2)
+    f32 = probe.probe_mfma("fp32", iters=1024, reps=2)
+    assert 300 < bf.tflops < 2600, bf
+    assert 40 < f32.tflops < 165, f32
+    assert bf.tflops > 5 * f32.tflops
+
+
+def test_cumask_scales_and_is_xcd_symmetric(gpu):
+    from walkai_nos_amd.ops import probe
+    with probe.Stream(0, range(32)) as s32, probe.Stream(0, range(128)) as s128:
+        r32 = probe.probe_mfma("bf16", stream=s32, iters=2048, reps=2)
+        r128 = probe.probe_mfma("bf16", stream=s128, iters=2048, reps=2)
+        pl = probe.census(stream=s32, n_wg=512)
+    assert probe.distinct_cus(pl) == 32
+    assert sorted({p["xcc"] for p in pl}) == list(range(8))  # bits 0..31 -> 4 CUs on every XCD
+    assert 2.5 < r128.tflops / r32.tflops < 4.5
+
+
+def test_rccl_commit_barrier_single_rank(gpu):
+    from walkai_nos_amd.parallel.barrier import RcclBarrier
+    b = RcclBarrier(1, 0, 0, {})
+    try:
+        assert b.vote(True) is True
+        assert b.vote(False) is False
+    finally:
+        b.close()
+
+
+def test_hbm_limit_shim_enforces_budget(gpu):
+    shim = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
+    code = ("import torch\n"
+            "f, t = torch.cuda.mem_get_info()\n"
+            "assert t <= 2 * 2**30, t\n"
+            "a = torch.empty(2**30, dtype=torch.uint8, device='cuda')\n"
+            "try:\n"
+            "    b = torch.empty(3 * 2**30, dtype=torch.uint8, device='cuda')\n"
+            "    print('NOT_ENFORCED')\n"
+            "except RuntimeError:\n"
+            "    print('ENFORCED')\n")
+    env = dict(os.environ, LD_PRELOAD=shim, NOS_HBM_LIMIT_BYTES=str(2 * 2**30))
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "ENFORCED" in p.stdout and "NOT_ENFORCED" not in p.stdout
+
+
+def test_smoke_entry(gpu):
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    g.smoke()

@@ -1,0 +1,330 @@
+"""Fractional-GPU serving benchmark: the control plane and the GPU data plane in one loop.
+
+Headline metric (BASELINE.json): *aggregate GPU utilization % + schedulable pods/node under a
+mixed fractional-GPU load*, on the workload the reference publishes numbers for (YOLOS-small
+batch-1 inference pods, ``demos/gpu-sharing-comparison``).
+
+One step = one churn epoch of the node:
+
+1. pods finish / new pods arrive (deterministic seeded process; fractions 1/8, 1/2 and 1/1 GPU,
+   i.e. ``amd.com/cpx_nps1``, ``amd.com/dpx_nps1``, ``amd.com/spx_nps1``);
+2. the *real* control plane (partitioner pod/node controllers, partition agents with their
+   reporter/actuator handshake, the scheduler) runs to quiescence on the in-memory API server;
+   every partition commit is voted through the node commit barrier, which on a multi-GPU run is
+   a real RCCL all-reduce over xGMI between the GPU ranks;
+3. every running pod on this rank's GPU executes ``8 x fraction`` YOLOS-small inferences (fp32,
+   batch 1, 800x1066) on its partition: a HIP stream whose CU mask is the partition's CU set.
+
+Because the box is not root, compute-partition modes cannot be flipped on the real device; a
+CPX/QPX/DPX partition is emulated by an XCD-symmetric CU mask of the same CU count (32/64/128
+CUs; the census in ``profiles/`` shows mask bit i -> XCD i mod 8, and an XCD whose mask bits are
+all zero is NOT disabled, so every slice must span all eight XCDs).  Mode changes go through the
+fake amd-smi backend; everything else — kernels, streams, collectives — is real.
+
+``value`` = aggregate inferences/s over all GPUs of the job (whole-job aggregate, weak scaling:
+per-GPU offered load fixed).  Utilization and pods/node are reported alongside.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import random
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+from .api import v1alpha1 as api
+from .kube import objects as ko
+from .models.xcp.profile import COMPUTE_MODES, extract_profile_name
+
+# reference numbers: 1x A100-80GB PCIe, 7 pods, MPS 10 GB slices
+BASELINE_INFER_PER_S_PER_GPU = 21.89
+BASELINE_LABEL = "MPS 7-pod aggregate throughput on 1x A100-80GB (BASELINE.md), scaled by n_gpus"
+
+MIX = (("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2))
+
+
+@dataclass
+class BenchConfig:
+    gpus: int = 1
+    steps: int = 10
+    warmup: int = 2
+    seed: int = 1234
+    offered_load: float = 1.25          # offered GPU-equivalents per GPU
+    lifetime: Tuple[int, int] = (2, 6)  # steps
+    hw: Tuple[int, int] = (800, 1066)
+    backend: str = "hip"
+    graphs: bool = True
+    rank: int = 0
+    world: int = 1
+
+
+class ChurnProcess:
+    """Deterministic pod arrival/departure process (identical on every rank)."""
+
+    def __init__(self, cfg: BenchConfig):
+        self.cfg = cfg
+        self.rng = random.Random(cfg.seed)
+        self.t = 0
+        self.live: Dict[str, int] = {}  # pod name -> remaining steps once running
+        self.seq = 0
+        mean_frac = sum((1.0 / COMPUTE_MODES[p.split("_")[0]]) * w for p, w in MIX)
+        mean_life = (cfg.lifetime[0] + cfg.lifetime[1]) / 2
+        self.rate = cfg.offered_load * cfg.gpus / (mean_frac * mean_life)
+
+    def arrivals(self) -> List[str]:
+        # Poisson(rate) via inversion, seeded
+        n, p, L = 0, 1.0, math.exp(-self.rate)
+        while True:
+            p *= self.rng.random()
+            if p <= L:
+                break
+            n += 1
+        out = []
+        for _ in range(n):
+            r, acc = self.rng.random(), 0.0
+            prof = MIX[-1][0]
+            for name, w in MIX:
+                acc += w
+                if r < acc:
+                    prof = name
+                    break
+            out.append(prof)
+        return out
+
+    def lifetime(self) -> int:
+        return self.rng.randint(*self.cfg.lifetime)
+
+
+def slice_cus(profile: str, partition: int, total_cus: int = 256) -> Optional[List[int]]:
+    """XCD-symmetric CU set emulating compute partition ``partition`` of ``profile``: a contiguous
+    run of mask bits (bit i -> XCD i mod 8), i.e. total/partitions CUs spread evenly over all XCDs."""
+    n = COMPUTE_MODES[profile.split("_")[0]]
+    if n == 1:
+        return None
+    per = total_cus // n
+    return list(range(partition * per, (partition + 1) * per))
+
+
+class Slot:
+    """One partition of this rank's GPU: a CU-masked stream, a model replica and an input."""
+
+    def __init__(self, profile: str, partition: int, device: int, cfg: BenchConfig, template: Any):
+        import copy
+
+        import torch
+
+        from .ops.probe import Stream
+
+        self.profile, self.partition = profile, partition
+        self.hip_stream = Stream(device, slice_cus(profile, partition))
+        self.stream = self.hip_stream.torch_stream()
+        with torch.cuda.stream(self.stream):
+            self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
+            from .models.workload.yolos import demo_input
+            self.x = demo_input(1, cfg.hw, f"cuda:{device}", seed=partition)
+        self.graph = None
+        self.cfg = cfg
+
+    def warm(self) -> None:
+        import torch
+        with torch.no_grad(), torch.cuda.stream(self.stream):
+            for _ in range(2):
+                self.out = self.model(self.x)
+        self.stream.synchronize()
+        if self.cfg.graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad():
+                with torch.cuda.graph(g, stream=self.stream):
+                    self.out = self.model(self.x)
+            self.stream.synchronize()
+            self.graph = g
+
+    def run(self, n: int) -> None:
+        import torch
+        with torch.no_grad(), torch.cuda.stream(self.stream):
+            for _ in range(n):
+                if self.graph is not None:
+                    self.graph.replay()
+                else:
+                    self.out = self.model(self.x)
+
+
+class NodeBench:
+    """The simulated node + this rank's GPU data plane."""
+
+    def __init__(self, cfg: BenchConfig, barrier_factory=None, gpu_data_plane: bool = True):
+        from .sim.cluster import SimCluster
+
+        self.cfg = cfg
+        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0)
+        if barrier_factory is not None:
+            for sn in self.cluster.nodes.values():
+                self._set_barrier(sn, barrier_factory)
+        self.churn = ChurnProcess(cfg)
+        self.cluster.run(30)  # node initialisation (SPX everywhere)
+        self.inferences = 0
+        self.util_samples: List[float] = []
+        self.pods_samples: List[int] = []
+        self.pending_samples: List[int] = []
+        self.slots: Dict[Tuple[str, int], Slot] = {}
+        self.gpu = gpu_data_plane
+        if self.gpu:
+            import torch
+
+            from .models.workload.yolos import YolosSmall
+            from .ops import kernels as K
+            K.set_backend(cfg.backend)
+            self.device = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(self.device)
+            template = YolosSmall()
+            for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
+                for k in range(n):
+                    self.slots[(prof, k)] = Slot(prof, k, self.device, cfg, template)
+            for s in self.slots.values():
+                s.warm()
+            torch.cuda.synchronize()
+
+    @staticmethod
+    def _set_barrier(sn: Any, factory: Any) -> None:
+        for c in sn.manager.controllers:
+            actuator = getattr(c.reconciler, "__self__", None)
+            if actuator is not None and hasattr(actuator, "barrier_factory"):
+                actuator.barrier_factory = factory
+
+    # -- one epoch ------------------------------------------------------------------------
+    def control_step(self) -> None:
+        c = self.cluster
+        for name in list(self.churn.live):
+            self.churn.live[name] -= 1
+            if self.churn.live[name] <= 0:
+                del self.churn.live[name]
+                c.complete(name)
+                c.delete_pod(name)  # the owning controller garbage-collects finished pods
+        for prof in self.churn.arrivals():
+            c.submit({f"amd.com/{prof}": 1}, name=f"p{self.churn.seq}")
+            self.churn.seq += 1
+        c.run(60)
+        for p in c.running_pods():
+            n = ko.name(p)
+            if n not in self.churn.live:
+                self.churn.live[n] = self.churn.lifetime()
+        self.util_samples.append(c.utilization())
+        self.pods_samples.append(len(c.running_pods()))
+        self.pending_samples.append(len(c.pending_pods()))
+
+    def my_pods(self) -> List[Tuple[str, int, int]]:
+        """(profile, partition index, inferences this step) for pods on this rank's GPU."""
+        sn = next(iter(self.cluster.nodes.values()))
+        out = []
+        for devs in sn.kubelet.allocations.values():
+            for r, dev_id in devs:
+                prof = extract_profile_name(r)
+                if prof is None or sn.smi.gpu_index_of(dev_id) != self.cfg.rank:
+                    continue
+                part = int(dev_id.rsplit("xcp", 1)[1])
+                out.append((prof, part, 8 // COMPUTE_MODES[prof.split("_")[0]]))
+        return out
+
+    def data_step(self) -> int:
+        n = 0
+        for prof, part, work in self.my_pods():
+            if self.gpu:
+                self.slots[(prof, part)].run(work)
+            n += work
+        self.inferences += n
+        return n
+
+    def step(self) -> int:
+        self.control_step()
+        return self.data_step()
+
+
+def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
+    import torch
+    import torch.distributed as dist
+
+    from .parallel.barrier import LocalBarrier, TorchBarrier
+
+    distributed = cfg.world > 1
+    if distributed:
+        bf = lambda n: TorchBarrier()  # noqa: E731 - one vote per rank = per GPU of the node
+    else:
+        bf = lambda n: LocalBarrier(1)  # noqa: E731
+    nb = NodeBench(cfg, barrier_factory=bf)
+    for _ in range(cfg.warmup):
+        nb.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    nb.inferences = 0
+    nb.util_samples.clear()
+    nb.pods_samples.clear()
+    nb.pending_samples.clear()
+    t0 = time.perf_counter()
+    for _ in range(cfg.steps):
+        nb.step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = torch.tensor([elapsed, float(nb.inferences)], dtype=torch.float64, device=f"cuda:{nb.device}")
+    if distributed:
+        t = stats[:1].clone()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        s = stats[1:].clone()
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        elapsed, total_inf = float(t.item()), float(s.item())
+    else:
+        total_inf = float(nb.inferences)
+    value = total_inf / elapsed
+    util = sum(nb.util_samples) / max(1, len(nb.util_samples))
+    pods = sum(nb.pods_samples) / max(1, len(nb.pods_samples))
+    from .models.workload.yolos import YolosSmall
+    flops = YolosSmall().flops_per_inference(cfg.hw)
+    return {
+        "metric": "aggregate GPU utilization % + schedulable pods/node, mixed fractional-GPU load",
+        "value": round(value, 3),
+        "unit": "inferences/s (aggregate over all GPUs; YOLOS-small fp32 batch-1 pods)",
+        "n_gpus": cfg.gpus,
+        "steps": cfg.steps,
+        "warmup": cfg.warmup,
+        "ms_per_step": round(1000.0 * elapsed / cfg.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (BASELINE_INFER_PER_S_PER_GPU * cfg.gpus), 3),
+        "dtype": "fp32",
+        "data": "synthetic (seeded pod churn; random-init YOLOS-small weights; synthetic 800x1066 images)",
+        "gpu_utilization_pct": round(util, 2),
+        "pods_per_node": round(pods, 2),
+        "pods_per_gpu": round(pods / cfg.gpus, 2),
+        "pending_pods_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
+        "achieved_tflops": round(value * flops / 1e12, 2),
+        "baseline_ref": BASELINE_LABEL,
+        "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
+                   "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
+                   "parallelism": f"fractional-gpu xcp partitions, {cfg.gpus} GPU node",
+                   "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
+                   "backend": cfg.backend, "hip_graphs": cfg.graphs},
+    }
+
+
+def smoke_step() -> None:
+    """One control-plane epoch + one partition's inference on cuda:0 + one slice probe."""
+    import torch
+
+    from .ops import probe
+    r = probe.probe_mfma("fp32", iters=256, reps=1)
+    assert r.tflops > 0
+    cfg = BenchConfig(gpus=1, steps=1, warmup=0, graphs=False)
+    nb = NodeBench(cfg, barrier_factory=None, gpu_data_plane=False)
+    nb.control_step()
+    from .models.workload.yolos import YolosSmall, demo_input
+    m = YolosSmall().cuda().eval()
+    with torch.no_grad():
+        logits, boxes = m(demo_input(1, (256, 256), "cuda"))
+    torch.cuda.synchronize()
+    assert torch.isfinite(logits).all() and torch.isfinite(boxes).all()
+    print(json.dumps({"smoke": "ok", "probe_fp32_tflops": round(r.tflops, 1),
+                      "pods_running": len(nb.cluster.running_pods()), "util_pct": nb.cluster.utilization()}))

@@ -113,7 +113,7 @@ class PodController:
 
     def pending_requests(self) -> Dict[str, int]:
         out: Dict[str, int] = {}
-        for p in self.client.list("Pod"):
+        for p in self.client.list("Pod", field_selector="status.phase=Pending"):
             if not self.should_consider(p):
                 continue
             for k, v in requested_profiles(self.kind, p).items():

@@ -19,7 +19,6 @@ call back into the server.
 """
 from __future__ import annotations
 
-import copy
 import itertools
 import threading
 import time
@@ -35,10 +34,19 @@ Handler = Callable[[str, Obj, Optional[Obj]], None]
 NAMESPACED = {"Pod", "ConfigMap", "Secret", "ElasticQuota", "Lease", "Event", "DaemonSet", "Deployment"}
 
 
+def fast_copy(o: Any) -> Any:
+    """Deep copy for JSON-shaped data (dict/list/scalars); ~5x faster than ``copy.deepcopy``."""
+    if isinstance(o, dict):
+        return {k: fast_copy(v) for k, v in o.items()}
+    if isinstance(o, list):
+        return [fast_copy(v) for v in o]
+    return o
+
+
 def merge_patch(target: Any, patch: Any) -> Any:
     """RFC 7386 JSON merge patch."""
     if not isinstance(patch, dict):
-        return copy.deepcopy(patch)
+        return fast_copy(patch)
     if not isinstance(target, dict):
         target = {}
     out = dict(target)
@@ -53,19 +61,19 @@ def merge_patch(target: Any, patch: Any) -> Any:
 def create_merge_patch(original: Any, modified: Any) -> Any:
     """Compute the merge patch turning ``original`` into ``modified`` (controller-runtime MergeFrom)."""
     if not isinstance(original, dict) or not isinstance(modified, dict):
-        return copy.deepcopy(modified)
+        return fast_copy(modified)
     patch: Dict[str, Any] = {}
     for k in original:
         if k not in modified:
             patch[k] = None
     for k, v in modified.items():
         if k not in original:
-            patch[k] = copy.deepcopy(v)
+            patch[k] = fast_copy(v)
         elif original[k] != v:
             if isinstance(v, dict) and isinstance(original[k], dict):
                 patch[k] = create_merge_patch(original[k], v)
             else:
-                patch[k] = copy.deepcopy(v)
+                patch[k] = fast_copy(v)
     return patch
 
 
@@ -85,7 +93,7 @@ class InMemoryAPIServer:
     def watch(self, kind: str, handler: Handler, replay: bool = True) -> Callable[[], None]:
         with self._lock:
             self._handlers.setdefault(kind, []).append(handler)
-            existing = [copy.deepcopy(o) for (k, _, _), o in self._objs.items() if k == kind] if replay else []
+            existing = [fast_copy(o) for (k, _, _), o in self._objs.items() if k == kind] if replay else []
         for o in existing:
             handler("ADDED", o, None)
 
@@ -101,7 +109,7 @@ class InMemoryAPIServer:
         with self._lock:
             handlers = list(self._handlers.get(kind, []))
         for h in handlers:
-            h(etype, copy.deepcopy(obj), copy.deepcopy(old) if old is not None else None)
+            h(etype, fast_copy(obj), fast_copy(old) if old is not None else None)
 
     # ---- CRUD -------------------------------------------------------------------------
     @staticmethod
@@ -110,7 +118,7 @@ class InMemoryAPIServer:
 
     def create(self, obj: Obj) -> Obj:
         kind = obj["kind"]
-        o = copy.deepcopy(obj)
+        o = fast_copy(obj)
         md = ko.meta(o)
         if not md.get("name"):
             gen = md.get("generateName")
@@ -130,7 +138,7 @@ class InMemoryAPIServer:
             md.setdefault("annotations", md.get("annotations") or {})
             self._objs[k] = o
             self.stats["create"] += 1
-            out = copy.deepcopy(o)
+            out = fast_copy(o)
         self._emit(kind, "ADDED", out, None)
         return out
 
@@ -140,7 +148,7 @@ class InMemoryAPIServer:
             o = self._objs.get(self._k(kind, namespace, name))
             if o is None:
                 raise NotFound(f"{kind} {namespace}/{name} not found")
-            return copy.deepcopy(o)
+            return fast_copy(o)
 
     def list(self, kind: str, namespace: Optional[str] = None, label_selector: Optional[str] = None,
              field_selector: Optional[str] = None) -> List[Obj]:
@@ -156,7 +164,7 @@ class InMemoryAPIServer:
                     continue
                 if not ko.field_selector_matches(field_selector, o):
                     continue
-                out.append(copy.deepcopy(o))
+                out.append(fast_copy(o))
         out.sort(key=lambda o: (ko.namespace(o), ko.name(o)))
         return out
 
@@ -174,10 +182,10 @@ class InMemoryAPIServer:
             md["resourceVersion"] = old["metadata"]["resourceVersion"]
             if new == old:
                 # a no-op write neither bumps the resourceVersion nor emits a watch event
-                return copy.deepcopy(old)
+                return fast_copy(old)
             md["resourceVersion"] = str(next(self._rv))
             self._objs[k] = new
-            out, prev = copy.deepcopy(new), copy.deepcopy(old)
+            out, prev = fast_copy(new), fast_copy(old)
         self._emit(kind, "MODIFIED", out, prev)
         return out
 
@@ -191,7 +199,7 @@ class InMemoryAPIServer:
             rv = ko.resource_version(obj)
             if rv and rv != cur["metadata"]["resourceVersion"]:
                 raise Conflict(f"{kind} {k[1]}/{k[2]}: resourceVersion {rv} is stale")
-            return self._replace(kind, k, copy.deepcopy(obj), "update")
+            return self._replace(kind, k, fast_copy(obj), "update")
 
     def patch(self, kind: str, name: str, patch: Obj, namespace: str = "") -> Obj:
         """JSON merge patch (``application/merge-patch+json``)."""
@@ -203,7 +211,7 @@ class InMemoryAPIServer:
             rv = (patch.get("metadata") or {}).get("resourceVersion")
             if rv and rv != cur["metadata"]["resourceVersion"]:
                 raise Conflict(f"{kind} {namespace}/{name}: resourceVersion {rv} is stale")
-            new = merge_patch(cur, patch)
+            new = merge_patch(fast_copy(cur), patch)
             return self._replace(kind, k, new, "patch")
 
     def delete(self, kind: str, name: str, namespace: str = "") -> None:
@@ -225,7 +233,7 @@ class InMemoryAPIServer:
                 raise NotFound(f"Pod {namespace}/{pod_name} not found")
             if ko.pod_node_name(cur):
                 raise Conflict(f"pod {namespace}/{pod_name} is already bound to {ko.pod_node_name(cur)}")
-            new = copy.deepcopy(cur)
+            new = fast_copy(cur)
             new["spec"]["nodeName"] = node_name
             ko.set_condition(new, "PodScheduled", "True", "", "")
             return self._replace("Pod", k, new, "update")

@@ -1,0 +1,219 @@
+"""YOLOS-small: the fractional-GPU benchmark workload.
+
+The reference's only published performance numbers come from its GPU-sharing demo, in which every
+Pod runs ``hustvl/yolos-small`` inference at batch 1 on one COCO image in a loop
+(``demos/gpu-sharing-comparison/client/main.py:6-35``).  This module is an
+independent implementation of that architecture (ViT-S/16 encoder with 100 detection tokens and
+DETR-style MLP heads) built for the MI355X inference path:
+
+* fp32 end to end (the reference demo runs fp32 PyTorch; no precision is given up);
+* the interpolated position embeddings are computed once per input resolution and cached (the
+  upstream implementation re-interpolates on every forward);
+* the hot ops dispatch to hand-written HIP kernels (:mod:`walkai_nos_amd.ops.kernels`) on the GPU:
+  fused LayerNorm, fused bias+GELU, fused residual adds and an f32-MFMA flash attention; plain
+  GEMMs go to hipBLASLt through ``torch.nn.functional.linear``;
+* ``load_hf_state_dict`` maps a ``transformers`` ``YolosForObjectDetection`` state dict onto this
+  module, which is how numerical parity is tested (``tests/test_workload_yolos.py``) — there is
+  no network, so weights are random-init of the same architecture.
+
+Config (hustvl/yolos-small): hidden 384, 12 layers, 6 heads, MLP 1536, patch 16, 100 detection
+tokens, pre-training image size 800x1333, 91 COCO labels (+1 "no object").  The demo's 640x480
+image is resized by the YOLOS processor to 800x1066 (shortest edge 800) -> 50x66 patches ->
+3401 tokens.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ...ops import kernels as K
+
+
+@dataclass
+class YolosConfig:
+    hidden_size: int = 384
+    num_layers: int = 12
+    num_heads: int = 6
+    intermediate_size: int = 1536
+    patch_size: int = 16
+    num_channels: int = 3
+    num_detection_tokens: int = 100
+    image_size: Tuple[int, int] = (800, 1333)
+    num_labels: int = 91
+    layer_norm_eps: float = 1e-12
+    use_mid_position_embeddings: bool = False
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden_size // self.num_heads
+
+
+#: the demo's input after YolosImageProcessor (640x480 COCO image -> shortest edge 800)
+DEMO_INPUT_HW = (800, 1066)
+
+
+class _Block(nn.Module):
+    def __init__(self, c: YolosConfig):
+        super().__init__()
+        d, f = c.hidden_size, c.intermediate_size
+        self.c = c
+        self.ln1 = nn.LayerNorm(d, eps=c.layer_norm_eps)
+        self.qkv = nn.Linear(d, 3 * d)            # fused q|k|v projection
+        self.proj = nn.Linear(d, d)
+        self.ln2 = nn.LayerNorm(d, eps=c.layer_norm_eps)
+        self.fc1 = nn.Linear(d, f)
+        self.fc2 = nn.Linear(f, d)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, T, D = x.shape
+        H, Dh = self.c.num_heads, self.c.head_dim
+        h = K.layernorm(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
+        qkv = F.linear(h, self.qkv.weight, self.qkv.bias)                  # [B, T, 3D]
+        o = K.attention_qkv(qkv, H, Dh, 1.0 / math.sqrt(Dh))               # [B, T, D]
+        x = K.linear_residual(o, self.proj.weight, self.proj.bias, x)      # x + o @ Wp^T + bp
+        h = K.layernorm(x, self.ln2.weight, self.ln2.bias, self.c.layer_norm_eps)
+        h = K.linear_gelu(h, self.fc1.weight, self.fc1.bias)               # gelu(h @ W1^T + b1)
+        return K.linear_residual(h, self.fc2.weight, self.fc2.bias, x)
+
+
+class _MLPHead(nn.Module):
+    def __init__(self, d_in: int, d_hidden: int, d_out: int, n_layers: int = 3):
+        super().__init__()
+        dims = [d_in] + [d_hidden] * (n_layers - 1)
+        self.layers = nn.ModuleList(nn.Linear(a, b) for a, b in zip(dims, dims[1:] + [d_out]))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        for i, l in enumerate(self.layers):
+            x = l(x)
+            if i < len(self.layers) - 1:
+                x = F.relu(x)
+        return x
+
+
+class YolosSmall(nn.Module):
+    def __init__(self, c: Optional[YolosConfig] = None):
+        super().__init__()
+        c = c or YolosConfig()
+        self.c = c
+        d = c.hidden_size
+        gh, gw = c.image_size[0] // c.patch_size, c.image_size[1] // c.patch_size
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, d))
+        self.det_tokens = nn.Parameter(torch.zeros(1, c.num_detection_tokens, d))
+        self.pos_embed = nn.Parameter(torch.zeros(1, 1 + gh * gw + c.num_detection_tokens, d))
+        self.patch = nn.Conv2d(c.num_channels, d, kernel_size=c.patch_size, stride=c.patch_size)
+        self.mid_pos_embed = (nn.Parameter(torch.zeros(c.num_layers - 1, 1, 1 + gh * gw + c.num_detection_tokens, d))
+                              if c.use_mid_position_embeddings else None)
+        self.blocks = nn.ModuleList(_Block(c) for _ in range(c.num_layers))
+        self.ln_f = nn.LayerNorm(d, eps=c.layer_norm_eps)
+        self.cls_head = _MLPHead(d, d, c.num_labels + 1)
+        self.box_head = _MLPHead(d, d, 4)
+        self._pos_cache: Dict[Tuple[int, int, str, int], torch.Tensor] = {}
+        self.reset_parameters()
+
+    def reset_parameters(self, seed: int = 0) -> None:
+        g = torch.Generator().manual_seed(seed)
+        with torch.no_grad():
+            for p in self.parameters():
+                if p.dim() >= 2:
+                    p.copy_(torch.randn(p.shape, generator=g) * 0.02)
+                else:
+                    p.zero_()
+            for m in self.modules():
+                if isinstance(m, nn.LayerNorm):
+                    m.weight.fill_(1.0)
+
+    # -- position embeddings ---------------------------------------------------------------
+    def _interp(self, pe: torch.Tensor, hw: Tuple[int, int]) -> torch.Tensor:
+        c = self.c
+        nd = c.num_detection_tokens
+        gh, gw = c.image_size[0] // c.patch_size, c.image_size[1] // c.patch_size
+        cls_pe, patch_pe, det_pe = pe[..., :1, :], pe[..., 1:-nd, :], pe[..., -nd:, :]
+        lead = patch_pe.shape[:-2]
+        patch_pe = patch_pe.reshape(-1, gh, gw, c.hidden_size).permute(0, 3, 1, 2)
+        nh, nw = hw[0] // c.patch_size, hw[1] // c.patch_size
+        patch_pe = F.interpolate(patch_pe, size=(nh, nw), mode="bicubic", align_corners=False)
+        patch_pe = patch_pe.flatten(2).transpose(1, 2).reshape(*lead, nh * nw, c.hidden_size)
+        return torch.cat((cls_pe, patch_pe, det_pe), dim=-2)
+
+    def position_embeddings(self, hw: Tuple[int, int]) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        key = (hw[0], hw[1], str(self.pos_embed.device), self.pos_embed._version)
+        if key not in self._pos_cache:
+            with torch.no_grad():
+                pe = self._interp(self.pos_embed, hw).contiguous()
+                mid = self._interp(self.mid_pos_embed, hw).contiguous() if self.mid_pos_embed is not None else None
+            self._pos_cache.clear()
+            self._pos_cache[key] = (pe, mid)
+        return self._pos_cache[key]
+
+    def invalidate_cache(self) -> None:
+        self._pos_cache.clear()
+
+    # -- forward -------------------------------------------------------------------------
+    def forward(self, pixels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        B, _, Hh, Ww = pixels.shape
+        x = self.patch(pixels).flatten(2).transpose(1, 2)                   # [B, P, D]
+        pe, mid = self.position_embeddings((Hh, Ww))
+        x = torch.cat((self.cls_token.expand(B, -1, -1), x, self.det_tokens.expand(B, -1, -1)), dim=1) + pe
+        for i, blk in enumerate(self.blocks):
+            x = blk(x)
+            if mid is not None and i < self.c.num_layers - 1:
+                x = x + mid[i]
+        det = x[:, -self.c.num_detection_tokens:, :]
+        det = K.layernorm(det.contiguous(), self.ln_f.weight, self.ln_f.bias, self.c.layer_norm_eps)
+        return self.cls_head(det), torch.sigmoid(self.box_head(det))
+
+    def flops_per_inference(self, hw: Tuple[int, int] = DEMO_INPUT_HW) -> float:
+        c = self.c
+        T = 1 + (hw[0] // c.patch_size) * (hw[1] // c.patch_size) + c.num_detection_tokens
+        d, f = c.hidden_size, c.intermediate_size
+        per_layer = 2 * T * (3 * d * d + d * d + 2 * d * f) + 4 * T * T * d
+        patch = 2 * (T - 1 - c.num_detection_tokens) * d * c.num_channels * c.patch_size ** 2
+        return float(c.num_layers * per_layer + patch)
+
+    # -- weights ------------------------------------------------------------------------
+    def load_hf_state_dict(self, sd: Dict[str, torch.Tensor]) -> None:
+        """Map ``transformers`` YolosForObjectDetection weights onto this module."""
+        own: Dict[str, torch.Tensor] = {
+            "cls_token": sd["vit.embeddings.cls_token"],
+            "det_tokens": sd["vit.embeddings.detection_tokens"],
+            "pos_embed": sd["vit.embeddings.position_embeddings"],
+            "patch.weight": sd["vit.embeddings.patch_embeddings.projection.weight"],
+            "patch.bias": sd["vit.embeddings.patch_embeddings.projection.bias"],
+            "ln_f.weight": sd["vit.layernorm.weight"],
+            "ln_f.bias": sd["vit.layernorm.bias"],
+        }
+        if self.mid_pos_embed is not None:
+            own["mid_pos_embed"] = sd["vit.encoder.mid_position_embeddings"]
+        for i in range(self.c.num_layers):
+            p = f"vit.encoder.layer.{i}."
+            a = p + "attention."
+            own[f"blocks.{i}.qkv.weight"] = torch.cat([sd[a + f"attention.{n}.weight"] for n in ("query", "key", "value")])
+            own[f"blocks.{i}.qkv.bias"] = torch.cat([sd[a + f"attention.{n}.bias"] for n in ("query", "key", "value")])
+            own[f"blocks.{i}.proj.weight"] = sd[a + "output.dense.weight"]
+            own[f"blocks.{i}.proj.bias"] = sd[a + "output.dense.bias"]
+            own[f"blocks.{i}.ln1.weight"] = sd[p + "layernorm_before.weight"]
+            own[f"blocks.{i}.ln1.bias"] = sd[p + "layernorm_before.bias"]
+            own[f"blocks.{i}.ln2.weight"] = sd[p + "layernorm_after.weight"]
+            own[f"blocks.{i}.ln2.bias"] = sd[p + "layernorm_after.bias"]
+            own[f"blocks.{i}.fc1.weight"] = sd[p + "intermediate.dense.weight"]
+            own[f"blocks.{i}.fc1.bias"] = sd[p + "intermediate.dense.bias"]
+            own[f"blocks.{i}.fc2.weight"] = sd[p + "output.dense.weight"]
+            own[f"blocks.{i}.fc2.bias"] = sd[p + "output.dense.bias"]
+        for head, hf in (("cls_head", "class_labels_classifier"), ("box_head", "bbox_predictor")):
+            for j in range(3):
+                own[f"{head}.layers.{j}.weight"] = sd[f"{hf}.layers.{j}.weight"]
+                own[f"{head}.layers.{j}.bias"] = sd[f"{hf}.layers.{j}.bias"]
+        missing, unexpected = self.load_state_dict(own, strict=True), None
+        del missing, unexpected
+        self.invalidate_cache()
+
+
+def demo_input(batch: int = 1, hw: Tuple[int, int] = DEMO_INPUT_HW, device: str = "cpu", seed: int = 0) -> torch.Tensor:
+    """A normalised image tensor of the demo's processed shape (synthetic; no dataset access)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(batch, 3, hw[0], hw[1], generator=g).to(device)

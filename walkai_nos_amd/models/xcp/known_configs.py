@@ -132,10 +132,11 @@ def get_model_spec(model: str) -> Optional[GpuModelSpec]:
 
 
 def get_allowed_geometries(model: str, nps: Optional[str] = None) -> Optional[List[Geometry]]:
-    s = get_model_spec(model)
-    if s is None:
-        return None
-    return s.geometries_for_nps(nps)
+    with _lock:
+        s = _known.get(normalize_model(model))
+        if s is None:
+            return None
+        return s.geometries_for_nps(nps)
 
 
 def load_known_geometries(data: str) -> Dict[str, GpuModelSpec]:

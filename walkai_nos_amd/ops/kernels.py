@@ -1,0 +1,138 @@
+"""Hot-op dispatch for the workload model: hand-written HIP kernels on the GPU, PyTorch reference
+math on the CPU.
+
+On a GPU tensor the HIP path is mandatory unless the caller explicitly selects the ``torch``
+backend (used only as the measured baseline in the benchmark's A/B mode): a missing
+``libnos_kernels.so`` raises instead of silently falling back.
+
+Kernels (``csrc/kernels.hip``):
+
+* ``layernorm``        — one wave per row, fp32, vectorised float4 loads, two-pass mean/var in
+  registers (rows of 384 floats = 6 floats per lane);
+* ``linear_gelu``      — hipBLASLt GEMM (``F.linear``) + fused bias+erf-GELU epilogue kernel;
+* ``linear_residual``  — hipBLASLt GEMM with the residual folded in as the GEMM's C input
+  (``torch.addmm`` beta=1), no extra pass;
+* ``attention_qkv``    — flash attention over the packed ``[B, T, 3*D]`` QKV tensor on
+  ``v_mfma_f32_32x32x2_f32`` (exact fp32 MFMA), online softmax, one workgroup per
+  (batch*head, 64-query tile); writes ``[B, T, D]`` directly so no transpose pass is needed.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import threading
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .native import NativeUnavailable, available, load
+
+LIB = "libnos_kernels.so"
+_backend = threading.local()
+_lib: Optional[ctypes.CDLL] = None
+_lock = threading.Lock()
+
+
+def set_backend(name: str) -> None:
+    """``hip`` (default) or ``torch`` (reference math, GPU A/B baseline only)."""
+    if name not in ("hip", "torch"):
+        raise ValueError(name)
+    _backend.name = name
+
+
+def get_backend() -> str:
+    return getattr(_backend, "name", "hip")
+
+
+def hip_available() -> bool:
+    return available(LIB)
+
+
+def _L() -> ctypes.CDLL:
+    global _lib
+    with _lock:
+        if _lib is None:
+            L = load(LIB)
+            vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+            L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, i32, i32, f32, vp]
+            L.nos_bias_gelu_f32.argtypes = [vp, vp, i32, i32, vp]
+            L.nos_attention_f32.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
+            L.nos_kernels_last_error.restype = ctypes.c_char_p
+            _lib = L
+        return _lib
+
+
+def _use_hip(t: torch.Tensor) -> bool:
+    if not t.is_cuda:
+        return False
+    if get_backend() == "torch":
+        return False
+    if not hip_available():
+        raise NativeUnavailable(f"{LIB} is not built but a GPU tensor reached the HIP op path")
+    return True
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError(f"nos kernel failed: {_L().nos_kernels_last_error().decode()} (rc={rc})")
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    if not _use_hip(x) or x.dtype != torch.float32:
+        return F.layer_norm(x, (x.shape[-1],), w, b, eps)
+    x = x.contiguous()
+    D = x.shape[-1]
+    rows = x.numel() // D
+    if D % 4 != 0 or D > 64 * 4 * 8:
+        return F.layer_norm(x, (D,), w, b, eps)
+    out = torch.empty_like(x)
+    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), rows, D, eps, _stream()))
+    return out
+
+
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    if not _use_hip(x) or x.dtype != torch.float32:
+        return F.gelu(F.linear(x, w, b))
+    y = torch.matmul(x, w.t())  # bias + GELU fused in the epilogue kernel below
+    N = y.shape[-1]
+    rows = y.numel() // N
+    if N % 4 != 0:
+        return F.gelu(y + b)
+    _check(_L().nos_bias_gelu_f32(y.data_ptr(), b.data_ptr(), rows, N, _stream()))
+    return y
+
+
+def linear_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+    """``res + x @ w^T + b`` with the residual and bias folded into one GEMM call."""
+    if not x.is_cuda or get_backend() == "torch":
+        return res + F.linear(x, w, b)
+    shp = res.shape
+    c = (res + b).reshape(-1, shp[-1])  # one fused elementwise pass; GEMM accumulates onto it
+    out = torch.addmm(c, x.reshape(-1, x.shape[-1]), w.t())
+    return out.view(shp)
+
+
+def attention_ref(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
+    B, T, _ = qkv.shape
+    q, k, v = qkv.view(B, T, 3, heads, head_dim).permute(2, 0, 3, 1, 4)
+    o = F.scaled_dot_product_attention(q, k, v, scale=scale)
+    return o.transpose(1, 2).reshape(B, T, heads * head_dim)
+
+
+def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
+    if not _use_hip(qkv) or qkv.dtype != torch.float32 or head_dim != 64:
+        return attention_ref(qkv, heads, head_dim, scale)
+    qkv = qkv.contiguous()
+    B, T, _ = qkv.shape
+    out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
+    _check(_L().nos_attention_f32(qkv.data_ptr(), out.data_ptr(), B, T, heads, head_dim, scale, _stream()))
+    return out
+
+
+def gelu_ref(x: torch.Tensor) -> torch.Tensor:
+    return 0.5 * x * (1.0 + torch.erf(x / math.sqrt(2.0)))

@@ -134,7 +134,7 @@ class SimScheduler:
         self.bound = 0
 
     def reconcile(self, req: Request) -> Result:
-        pods = [p for p in self.api.list("Pod") if podutil.is_pending(p) and not podutil.is_scheduled(p)
+        pods = [p for p in self.api.list("Pod", field_selector="status.phase=Pending") if not podutil.is_scheduled(p)
                 and p["spec"].get("schedulerName", "default-scheduler") == "default-scheduler"]
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
         for p in pods:
@@ -257,10 +257,10 @@ class SimCluster:
 
     # -- metrics ------------------------------------------------------------------------
     def running_pods(self) -> List[Dict[str, Any]]:
-        return [p for p in self.api.list("Pod") if podutil.is_running(p) and ko.namespace(p) != DP_NAMESPACE]
+        return [p for p in self.api.list("Pod", field_selector="status.phase=Running") if ko.namespace(p) != DP_NAMESPACE]
 
     def pending_pods(self) -> List[Dict[str, Any]]:
-        return [p for p in self.api.list("Pod") if podutil.is_pending(p) and ko.namespace(p) != DP_NAMESPACE]
+        return [p for p in self.api.list("Pod", field_selector="status.phase=Pending") if ko.namespace(p) != DP_NAMESPACE]
 
     def gpu_allocated_fraction(self) -> Dict[Tuple[str, int], float]:
         out: Dict[Tuple[str, int], float] = {}
