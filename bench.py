@@ -26,6 +26,8 @@ def main() -> int:
     ap.add_argument("--load", type=float, default=1.25, help="offered GPU-equivalents per GPU")
     ap.add_argument("--backend", choices=("hip", "torch"), default="hip")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--preroll", type=int, default=20,
+                    help="control-plane-only churn epochs before warmup, so timing starts in steady state")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -45,7 +47,8 @@ def main() -> int:
 
     from walkai_nos_amd.bench_core import BenchConfig, run_bench
     cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
-                      backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world)
+                      backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
+                      preroll=args.preroll)
     res = run_bench(cfg)
     if rank == 0:
         line = json.dumps(res)

@@ -287,12 +287,24 @@ int nos_bias_gelu_f32(float* y, const float* b, int rows, int N, void* stream) {
   return check_launch("bias_gelu_f32");
 }
 
-// workspace for split-key attention (grown on demand, per device)
-static float* g_ws = nullptr;
-static size_t g_ws_bytes = 0;
+// keys per split (rounded to the 32-key block) and the effective split count
+static void split_plan(int T, int nsplit, int* kps, int* ns) {
+  *kps = ((T + nsplit - 1) / nsplit + 31) / 32 * 32;
+  *ns = (T + *kps - 1) / *kps;
+}
 
-int nos_attention_f32_split(const float* qkv, float* out, int B, int T, int H, int head_dim, float scale, int nsplit,
-                            void* stream) {
+// bytes of caller-provided workspace for a split launch (0 when nsplit <= 1). The workspace comes
+// from the caller's stream-ordered allocator, so concurrent slices never share scratch and a launch
+// inside graph capture never allocates.
+size_t nos_attention_ws_bytes(int B, int T, int H, int nsplit) {
+  if (nsplit <= 1) return 0;
+  int kps, ns;
+  split_plan(T, nsplit, &kps, &ns);
+  return size_t(ns) * B * H * T * (HD + 2) * sizeof(float);
+}
+
+int nos_attention_f32_split(const float* qkv, float* out, float* ws, int B, int T, int H, int head_dim, float scale,
+                            int nsplit, void* stream) {
   if (head_dim != HD) {
     g_err = "attention: head_dim must be 64";
     return -1;
@@ -305,22 +317,14 @@ int nos_attention_f32_split(const float* qkv, float* out, int B, int T, int H, i
                        scale_log2e, T, 1);
     return check_launch("attn_fwd_f32");
   }
-  // keys per split rounded to the 32-key block
-  int kps = ((T + nsplit - 1) / nsplit + 31) / 32 * 32;
-  nsplit = (T + kps - 1) / kps;
-  const size_t need = size_t(nsplit) * B * H * T * (HD + 2) * sizeof(float);
-  if (need > g_ws_bytes) {
-    if (g_ws) (void)hipFree(g_ws);
-    if (hipMalloc(&g_ws, need) != hipSuccess) {
-      g_ws = nullptr;
-      g_ws_bytes = 0;
-      g_err = "attention: workspace allocation failed";
-      return -1;
-    }
-    g_ws_bytes = need;
+  int kps;
+  split_plan(T, nsplit, &kps, &nsplit);
+  if (ws == nullptr) {
+    g_err = "attention: split launch needs a workspace (nos_attention_ws_bytes)";
+    return -1;
   }
-  float* part_o = g_ws;
-  float* part_ml = g_ws + size_t(nsplit) * B * H * T * HD;
+  float* part_o = ws;
+  float* part_ml = ws + size_t(nsplit) * B * H * T * HD;
   hipLaunchKernelGGL(attn_fwd_f32<true>, dim3(qtiles, H, B * nsplit), dim3(64), 0, s, qkv, out, part_o, part_ml, T, H,
                      scale_log2e, kps, nsplit);
   if (int rc = check_launch("attn_fwd_f32<split>")) return rc;
@@ -331,7 +335,7 @@ int nos_attention_f32_split(const float* qkv, float* out, int B, int T, int H, i
 }
 
 int nos_attention_f32(const float* qkv, float* out, int B, int T, int H, int head_dim, float scale, void* stream) {
-  return nos_attention_f32_split(qkv, out, B, T, H, head_dim, scale, 1, stream);
+  return nos_attention_f32_split(qkv, out, nullptr, B, T, H, head_dim, scale, 1, stream);
 }
 
 }  // extern "C"

@@ -50,21 +50,36 @@ def test_attention_asymmetric_values_catch_transposes(K):
 
 
 def test_attention_split_matches_unsplit(K):
-    import ctypes
     torch.manual_seed(1)
     B, T, H = 1, 1000, 2
     qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
     ref = _ref_attention(qkv, H, 64, 0.125)
-    L = K._L()
-    L.nos_attention_f32_split.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_void_p]
-    for ns in (2, 3, 7):
+    for ns in (1, 2, 3, 7):
         out = torch.empty(B, T, H * 64, device="cuda")
-        rc = L.nos_attention_f32_split(qkv.data_ptr(), out.data_ptr(), B, T, H, 64, 0.125, ns,
-                                       torch.cuda.current_stream().cuda_stream)
-        assert rc == 0
+        K.attention_split(qkv, out, H, 64, 0.125, ns)
         torch.cuda.synchronize()
         assert (out - ref).abs().max().item() < 2e-5
+
+
+def test_attention_concurrent_streams_with_splits(K):
+    # two slices running split launches at once must not share scratch
+    torch.manual_seed(2)
+    qa = torch.randn(1, 700, 3 * 2 * 64, device="cuda")
+    qb = torch.randn(1, 900, 3 * 2 * 64, device="cuda")
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(sa):
+            oa = K.attention_split(qa, torch.empty(1, 700, 128, device="cuda"), 2, 64, 0.125, 3)
+        with torch.cuda.stream(sb):
+            ob = K.attention_split(qb, torch.empty(1, 900, 128, device="cuda"), 2, 64, 0.125, 4)
+        outs.append((oa, ob))
+    torch.cuda.synchronize()
+    ra, rb = _ref_attention(qa, 2, 64, 0.125), _ref_attention(qb, 2, 64, 0.125)
+    for oa, ob in outs:
+        assert (oa - ra).abs().max().item() < 2e-5
+        assert (ob - rb).abs().max().item() < 2e-5
 
 
 @pytest.mark.parametrize("D", [384, 768, 1024])

@@ -56,6 +56,7 @@ class BenchConfig:
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"
     graphs: bool = True
+    preroll: int = 20                   # control-plane-only epochs before warmup (steady state)
     rank: int = 0
     world: int = 1
 
@@ -127,8 +128,16 @@ class Slot:
         self.graph = None
         self.cfg = cfg
 
+    @property
+    def n_cus(self) -> int:
+        cus = slice_cus(self.profile, self.partition)
+        return 256 if cus is None else len(cus)
+
     def warm(self) -> None:
         import torch
+
+        from .ops import kernels as K
+        K.set_slice_cus(self.n_cus)
         with torch.no_grad(), torch.cuda.stream(self.stream):
             for _ in range(2):
                 self.out = self.model(self.x)
@@ -141,8 +150,21 @@ class Slot:
             self.stream.synchronize()
             self.graph = g
 
+    def close(self) -> None:
+        self.graph = None
+        self.model = None
+        self.x = None
+        self.out = None
+        self.stream = None
+        if self.hip_stream is not None:
+            self.hip_stream.close()
+            self.hip_stream = None
+
     def run(self, n: int) -> None:
         import torch
+
+        from .ops import kernels as K
+        K.set_slice_cus(self.n_cus)
         with torch.no_grad(), torch.cuda.stream(self.stream):
             for _ in range(n):
                 if self.graph is not None:
@@ -240,6 +262,25 @@ class NodeBench:
         self.control_step()
         return self.data_step()
 
+    def close(self) -> None:
+        """Release graphs, model replicas and CU-masked streams before interpreter teardown (a
+        graph destroyed after the HIP runtime has been finalised crashes the process at exit)."""
+        if not self.gpu:
+            return
+        import gc
+
+        import torch
+        torch.cuda.synchronize()
+        for s in self.slots.values():
+            s.graph = None
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        for s in self.slots.values():
+            s.close()
+        self.slots.clear()
+        gc.collect()
+
 
 def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     import torch
@@ -253,6 +294,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     else:
         bf = lambda n: LocalBarrier(1)  # noqa: E731
     nb = NodeBench(cfg, barrier_factory=bf)
+    for _ in range(cfg.preroll):
+        nb.control_step()
     for _ in range(cfg.warmup):
         nb.step()
     torch.cuda.synchronize()
@@ -278,6 +321,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         elapsed, total_inf = float(t.item()), float(s.item())
     else:
         total_inf = float(nb.inferences)
+    nb.close()
     value = total_inf / elapsed
     util = sum(nb.util_samples) / max(1, len(nb.util_samples))
     pods = sum(nb.pods_samples) / max(1, len(nb.pods_samples))

@@ -46,9 +46,9 @@ def requested_profiles(kind: str, pod: Dict[str, Any]) -> Dict[str, int]:
     return slicing_gpu.get_requested_profiles(pod)
 
 
-def new_node_model(kind: str, node: Dict[str, Any]) -> NodeModel:
+def new_node_model(kind: str, node: Dict[str, Any], scoring: str = "fraction") -> NodeModel:
     if kind == api.PARTITIONING_KIND_XCP:
-        return xcp_node.new_node(node)
+        return xcp_node.new_node(node, scoring)
     return slicing_gpu.new_node(node)
 
 
@@ -62,14 +62,16 @@ def plan_cluster(models: Mapping[str, NodeModel], required: Mapping[str, int]) -
     current = dict(models)
     changed: Dict[str, NodeModel] = {}
     while remaining:
-        best: Optional[Tuple[Tuple[int, int, str], str, NodeModel]] = None
+        best: Optional[Tuple[Tuple[float, int, str], str, NodeModel]] = None
         for name, m in sorted(current.items()):
             cand = m.clone()
             before_free = m.free()
             if not cand.update_geometry_for(remaining):
                 continue
             after_free = cand.free()
-            provided = sum(min(max(0, after_free.get(p, 0) - before_free.get(p, 0)), q) for p, q in remaining.items())
+            w = getattr(cand, "weight", None)
+            provided = sum(min(max(0, after_free.get(p, 0) - before_free.get(p, 0)), q) * (1.0 if w is None else w(p))
+                           for p, q in remaining.items())
             if provided <= 0:
                 continue
             score = (-provided, _changed_gpus(m, cand), name)
@@ -92,9 +94,10 @@ def plan_cluster(models: Mapping[str, NodeModel], required: Mapping[str, int]) -
 class PodController:
     def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
                  clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
-                 retry_after: float = 5.0):
+                 retry_after: float = 5.0, scoring: str = "fraction"):
         self.client = client
         self.kind = kind
+        self.scoring = scoring
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -124,7 +127,7 @@ class PodController:
         out: Dict[str, NodeModel] = {}
         for n in nodes:
             try:
-                out[ko.name(n)] = new_node_model(self.kind, n)
+                out[ko.name(n)] = new_node_model(self.kind, n, self.scoring)
             except ValueError as e:
                 log.warning("skipping node %s: %s", ko.name(n), e)
         return out

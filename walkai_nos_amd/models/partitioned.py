@@ -71,8 +71,9 @@ class PartitionedGPU:
             raise ValueError("no allowed geometries")
         self.apply_geometry(g)
 
-    def _provided(self, candidate: Mapping[str, int], required: Mapping[str, int], current: Mapping[str, int]) -> int:
-        provided = 0
+    def _provided(self, candidate: Mapping[str, int], required: Mapping[str, int], current: Mapping[str, int],
+                  weight: Optional[Callable[[str], float]] = None) -> float:
+        provided = 0.0
         for p, rq in required.items():
             fr = self.free.get(p, 0)
             if fr >= rq:
@@ -81,17 +82,20 @@ class PartitionedGPU:
             extra = candidate.get(p, 0) - current.get(p, 0)
             if extra <= 0:
                 continue
-            provided += min(extra, needed)
+            provided += min(extra, needed) * (1.0 if weight is None else weight(p))
         return provided
 
-    def update_geometry_for(self, required: Mapping[str, int]) -> bool:
+    def update_geometry_for(self, required: Mapping[str, int], weight: Optional[Callable[[str], float]] = None) -> bool:
+        """B.1.  ``weight`` scores each provided profile (None = count pods, the reference score;
+        the MI355X planner passes the GPU fraction of the profile so that a free GPU is flipped to
+        the mode that puts the most *capacity* to use, not the most pods)."""
         current = self.geometry()
         best: Optional[Geometry] = None
-        best_score: Optional[Tuple[int, int, int, str]] = None
+        best_score: Optional[Tuple[float, int, int, str]] = None
         for cand in self.allowed_geometries:
             if not self.can_apply_geometry(cand)[0]:
                 continue
-            provided = self._provided(cand, required, current)
+            provided = self._provided(cand, required, current, weight)
             if provided <= 0:
                 continue
             # higher is better: provided desc, slices desc, distance asc, id asc
@@ -122,7 +126,7 @@ class PartitionedGPU:
         return sum(q / partitions_of(p) for p, q in self.used.items())
 
 
-def _better(a: Tuple[int, int, int, str], b: Tuple[int, int, int, str]) -> bool:
+def _better(a: Tuple[float, int, int, str], b: Tuple[float, int, int, str]) -> bool:
     if a[0] != b[0]:
         return a[0] > b[0]
     if a[1] != b[1]:
@@ -139,10 +143,11 @@ class PartitionedNode:
     allocatable: Dict[str, int] = field(default_factory=dict)
     is_resource: Callable[[str], bool] = lambda r: False
     as_resource: Callable[[str], str] = lambda p: p
+    weight: Optional[Callable[[str], float]] = None
 
     def clone(self) -> "PartitionedNode":
         return PartitionedNode(self.name, [g.clone() for g in self.gpus], dict(self.allocatable),
-                               self.is_resource, self.as_resource)
+                               self.is_resource, self.as_resource, self.weight)
 
     def geometry(self) -> Geometry:
         out: Geometry = {}
@@ -174,7 +179,7 @@ class PartitionedNode:
         remaining = dict(required)
         any_updated = False
         for g in self.gpus:
-            updated = g.update_geometry_for(remaining)
+            updated = g.update_geometry_for(remaining, self.weight)
             any_updated = any_updated or updated
             for p, q in g.free.items():
                 if p in remaining:

@@ -26,7 +26,15 @@ def new_gpu(model: str, index: int, nps: str, used: Mapping[str, int] | None = N
     return PartitionedGPU(model, index, allowed, dict(used or {}), dict(free or {}))
 
 
-def new_node(node: Dict[str, Any]) -> PartitionedNode:
+def fraction_weight(profile: str) -> float:
+    from .profile import parse_profile
+    return 1.0 / parse_profile(profile).partitions
+
+
+SCORING = {"pods": None, "fraction": fraction_weight}
+
+
+def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode:
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
     nps = gpu_util.get_memory_partition(node)
@@ -41,7 +49,7 @@ def new_node(node: Dict[str, Any]) -> PartitionedNode:
             gpus[i] = new_gpu(model, i, nps)
     allocatable = res.from_k8s(ko.node_allocatable(node))
     return PartitionedNode(ko.name(node), [gpus[i] for i in sorted(gpus)], allocatable,
-                           is_resource=is_xcp_resource, as_resource=as_resource_name)
+                           is_resource=is_xcp_resource, as_resource=as_resource_name, weight=SCORING[scoring])
 
 
 def get_requested_profiles(pod: Dict[str, Any]) -> Dict[str, int]:

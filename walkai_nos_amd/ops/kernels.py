@@ -34,6 +34,29 @@ _lib: Optional[ctypes.CDLL] = None
 _lock = threading.Lock()
 
 
+_slice = threading.local()
+
+
+def set_slice_cus(n: Optional[int]) -> None:
+    """Tell the kernels how many CUs the current stream may use (its CU mask / partition size), so
+    launch decompositions fit the slice instead of assuming the whole 256-CU device."""
+    _slice.cus = n
+
+
+def slice_cus() -> int:
+    return getattr(_slice, "cus", None) or 256
+
+
+def attention_splits(B: int, T: int, H: int, cus: int) -> int:
+    """Key splits so that a launch has >= 2 waves per SIMD of the slice (4 SIMDs per CU)."""
+    waves = B * H * ((T + 31) // 32)
+    target = 2 * 4 * cus
+    ns = 1
+    while waves * ns < target and ns < 8 and T // (32 * (ns + 1)) >= 4:
+        ns += 1
+    return ns
+
+
 def set_backend(name: str) -> None:
     """``hip`` (default) or ``torch`` (reference math, GPU A/B baseline only)."""
     if name not in ("hip", "torch"):
@@ -58,6 +81,9 @@ def _L() -> ctypes.CDLL:
             L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, i32, i32, f32, vp]
             L.nos_bias_gelu_f32.argtypes = [vp, vp, i32, i32, vp]
             L.nos_attention_f32.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
+            L.nos_attention_f32_split.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_ws_bytes.argtypes = [i32, i32, i32, i32]
+            L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             _lib = L
         return _lib
@@ -130,7 +156,17 @@ def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) ->
     qkv = qkv.contiguous()
     B, T, _ = qkv.shape
     out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
-    _check(_L().nos_attention_f32(qkv.data_ptr(), out.data_ptr(), B, T, heads, head_dim, scale, _stream()))
+    ns = attention_splits(B, T, heads, slice_cus())
+    return attention_split(qkv, out, heads, head_dim, scale, ns)
+
+
+def attention_split(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float, ns: int) -> torch.Tensor:
+    B, T, _ = qkv.shape
+    L = _L()
+    nbytes = L.nos_attention_ws_bytes(B, T, heads, ns)
+    ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=qkv.device) if nbytes else None
+    _check(L.nos_attention_f32_split(qkv.data_ptr(), out.data_ptr(), ws.data_ptr() if ws is not None else None,
+                                     B, T, heads, head_dim, scale, ns, _stream()))
     return out
 
 

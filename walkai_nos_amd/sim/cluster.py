@@ -165,7 +165,8 @@ class SimScheduler:
 class SimCluster:
     def __init__(self, n_nodes: int = 1, gpus_per_node: int = 8, model: str = "MI355X",
                  kind: str = api.PARTITIONING_KIND_XCP, refresh_interval: float = 10.0,
-                 batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None):
+                 batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None,
+                 scoring: str = "fraction"):
         self.clock = clock or SimClock()
         self.api = InMemoryAPIServer(clock=self.clock)
         self.kind = kind
@@ -176,7 +177,7 @@ class SimCluster:
         # control plane
         self.partitioner_mgr = Manager(self.api, clock=self.clock)
         self.pod_controllers, _ = setup_partitioner(self.partitioner_mgr, kinds=(kind,), batch_timeout=batch_timeout,
-                                                    batch_idle=batch_idle)
+                                                    batch_idle=batch_idle, scoring=scoring)
         self.scheduler_mgr = Manager(self.api, clock=self.clock)
         self.scheduler = SimScheduler(self.api, self.nodes, self._on_bind)
         self.scheduler_mgr.new_controller("sim-scheduler", self.scheduler.reconcile,
