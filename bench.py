@@ -23,7 +23,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--load", type=float, default=1.25, help="offered GPU-equivalents per GPU")
+    ap.add_argument("--load", type=float, default=1.0, help="offered GPU-equivalents per GPU")
     ap.add_argument("--backend", choices=("hip", "torch"), default="hip")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--preroll", type=int, default=20,

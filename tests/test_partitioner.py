@@ -1,0 +1,153 @@
+"""Cluster-side partitioner: pod controller (B1), node initialiser (B2), spec writer (C4)."""
+from walkai_nos_amd import constant
+from walkai_nos_amd.api import v1alpha1 as api
+from walkai_nos_amd.controllers.partitioner.node_controller import NodeController
+from walkai_nos_amd.controllers.partitioner.pod_controller import PodController, plan_cluster, plan_cluster_fifo
+from walkai_nos_amd.kube import objects as ko
+from walkai_nos_amd.kube.memory import InMemoryAPIServer
+from walkai_nos_amd.kube.runtime import Request, SimClock
+from walkai_nos_amd.models.xcp import node as xcp_node
+from walkai_nos_amd.partitioning.planner import (NodeInitializer, Partitioner, build_node_partitioning, new_plan_id,
+                                                 spec_annotations)
+
+
+def xnode(name="n0", gpus=2, anns=None):
+    return ko.new_node(name, {api.LABEL_GPU_PARTITIONING: "xcp", constant.LABEL_AMD_GPU_PRODUCT: "AMD_Instinct_MI355X",
+                              constant.LABEL_AMD_GPU_COUNT: str(gpus)}, anns or {})
+
+
+def unschedulable_pod(name, req, ns="default"):
+    p = ko.new_pod(name, ns, requests=req)
+    ko.set_condition(p, "PodScheduled", "False", "Unschedulable")
+    return p
+
+
+def test_plan_ids_are_unique_and_increasing():
+    clock = SimClock(5)
+    a, b = new_plan_id(clock), new_plan_id(clock)
+    assert int(b) > int(a)
+
+
+def test_partitioner_replaces_spec_family_and_sets_plan():
+    api_ = InMemoryAPIServer()
+    api_.create(xnode(anns={"nos.nebuly.com/spec-gpu-5-cpx_nps1": "8", "keep": "me"}))
+    model = xcp_node.new_node(api_.get("Node", "n0"))
+    for g in model.gpus:
+        g.init_geometry()
+    Partitioner(api_).apply_partitioning(api_.get("Node", "n0"), "99", build_node_partitioning(model))
+    a = ko.annotations(api_.get("Node", "n0"))
+    assert a["nos.nebuly.com/spec-gpu-0-spx_nps1"] == "1" and a["nos.nebuly.com/spec-gpu-1-spx_nps1"] == "1"
+    assert "nos.nebuly.com/spec-gpu-5-cpx_nps1" not in a and a["keep"] == "me"
+    assert a[api.ANNOTATION_PARTITIONING_PLAN] == "99"
+
+
+def test_node_controller_initialises_once_and_requires_labels():
+    api_ = InMemoryAPIServer()
+    api_.create(xnode())
+    nc = NodeController(api_, NodeInitializer(api_))
+    nc.reconcile(Request("n0"))
+    n = api_.get("Node", "n0")
+    assert NodeController.is_initialized(n)
+    plan = ko.annotations(n)[api.ANNOTATION_PARTITIONING_PLAN]
+    nc.reconcile(Request("n0"))
+    assert ko.annotations(api_.get("Node", "n0"))[api.ANNOTATION_PARTITIONING_PLAN] == plan
+    bare = ko.new_node("bare", {api.LABEL_GPU_PARTITIONING: "xcp"})
+    api_.create(bare)
+    nc.reconcile(Request("bare"))
+    assert api.ANNOTATION_PARTITIONING_PLAN not in ko.annotations(api_.get("Node", "bare"))
+
+
+def _settled(api_, status):
+    anns = dict(status)
+    anns[api.ANNOTATION_PARTITIONING_PLAN] = "1"
+    anns[api.ANNOTATION_REPORTED_PARTITIONING_PLAN] = "1"
+    api_.patch("Node", "n0", {"metadata": {"annotations": anns}})
+
+
+def test_pod_controller_ignores_schedulable_or_unrelated_pods():
+    api_ = InMemoryAPIServer()
+    api_.create(xnode())
+    pc = PodController(api_)
+    api_.create(ko.new_pod("plain", requests={"amd.com/cpx_nps1": 1}))  # not marked unschedulable
+    api_.create(unschedulable_pod("cpu-only", {"cpu": "1"}))
+    assert pc.map_pod(api_.get("Pod", "plain", "default")) == []
+    assert pc.map_pod(api_.get("Pod", "cpu-only", "default")) == []
+    pc.reconcile(Request("plain", "default"))
+    pc.reconcile(Request("cpu-only", "default"))
+    assert pc.plans_written == 0
+
+
+def test_pod_controller_flips_free_gpu_and_skips_when_free_capacity_exists():
+    api_ = InMemoryAPIServer()
+    api_.create(xnode())
+    _settled(api_, {"nos.nebuly.com/status-gpu-0-spx_nps1-free": "1", "nos.nebuly.com/status-gpu-1-spx_nps1-used": "1"})
+    pc = PodController(api_)
+    api_.create(unschedulable_pod("p", {"amd.com/cpx_nps1": 1}))
+    pc.reconcile(pc.plan_key)
+    a = ko.annotations(api_.get("Node", "n0"))
+    assert a["nos.nebuly.com/spec-gpu-0-cpx_nps1"] == "8" and a["nos.nebuly.com/spec-gpu-1-spx_nps1"] == "1"
+    assert pc.plans_written == 1
+    # a plan is in flight (spec plan != status plan): no re-planning, capacity counted as incoming
+    api_.create(unschedulable_pod("p2", {"amd.com/cpx_nps1": 1}))
+    pc.reconcile(Request("p2", "default"))
+    assert pc.plans_written == 1
+
+
+def test_q1_fix_repartitions_when_every_partition_of_the_profile_is_used():
+    # reference bug Q1: "profile exists somewhere (free or used)" suppressed repartitioning
+    api_ = InMemoryAPIServer()
+    api_.create(xnode())
+    _settled(api_, {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8", "nos.nebuly.com/status-gpu-1-spx_nps1-free": "1"})
+    pc = PodController(api_)
+    api_.create(unschedulable_pod("p", {"amd.com/cpx_nps1": 1}))
+    pc.reconcile(pc.plan_key)
+    a = ko.annotations(api_.get("Node", "n0"))
+    assert a["nos.nebuly.com/spec-gpu-1-cpx_nps1"] == "8"
+
+
+def test_q14_requeue_when_nothing_can_help():
+    api_ = InMemoryAPIServer()
+    api_.create(xnode(gpus=1))
+    _settled(api_, {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8"})
+    pc = PodController(api_, retry_after=7)
+    api_.create(unschedulable_pod("p", {"amd.com/spx_nps1": 1}))
+    res = pc.reconcile(pc.plan_key)
+    assert res.requeue_after == 7 and pc.plans_written == 0
+
+
+def test_batch_window_defers_planning():
+    api_ = InMemoryAPIServer()
+    clock = SimClock(0)
+    api_.create(xnode())
+    pc = PodController(api_, clock=clock, batch_timeout=10, batch_idle=3)
+    api_.create(unschedulable_pod("p", {"amd.com/cpx_nps1": 1}))
+    res = pc.reconcile(pc.plan_key)
+    assert 0 < res.requeue_after <= 3 and pc.plans_written == 0
+    clock.advance(3)
+    pc.reconcile(pc.plan_key)
+    assert pc.plans_written == 1
+
+
+def test_plan_cluster_scores_nodes_and_fifo_is_head_of_line():
+    api_ = InMemoryAPIServer()
+    for n in ("a", "b"):
+        api_.create(xnode(n, gpus=1, anns={"nos.nebuly.com/status-gpu-0-spx_nps1-free": "1"}))
+    models = {n: xcp_node.new_node(api_.get("Node", n)) for n in ("a", "b")}
+    changed = plan_cluster(models, {"cpx_nps1": 9})
+    assert set(changed) == {"a", "b"}  # 8 + 1 partitions need both GPUs
+    # head pod reserves a free SPX GPU; the 1/8 pod behind it flips the *other* GPU
+    changed = plan_cluster_fifo(models, [{"spx_nps1": 1}, {"cpx_nps1": 1}])
+    assert list(changed) == ["b"] and changed["b"].gpus[0].geometry() == {"cpx_nps1": 8}
+    # two SPX pods take both GPUs: a 1/8 pod cannot be helped
+    assert plan_cluster_fifo(models, [{"spx_nps1": 1}, {"spx_nps1": 1}, {"cpx_nps1": 1}]) == {}
+    # one GPU flipped to CPX serves both 1/8 pods, the other stays SPX for the whole-GPU pod
+    changed = plan_cluster_fifo(models, [{"cpx_nps1": 1}, {"cpx_nps1": 1}, {"spx_nps1": 1}])
+    assert len(changed) == 1
+    (name, model), = changed.items()
+    assert model.gpus[0].geometry() == {"cpx_nps1": 8}
+
+
+def test_spec_annotations_sum_per_gpu_profile():
+    from walkai_nos_amd.partitioning.state import GPUPartitioning, NodePartitioning
+    np_ = NodePartitioning([GPUPartitioning(0, {"amd.com/cpx_nps1": 8}), GPUPartitioning(1, {"amd.com/gpu-8cu.4gb": 2})])
+    assert spec_annotations(np_) == {"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", "nos.nebuly.com/spec-gpu-1-8cu.4gb": "2"}

@@ -51,7 +51,7 @@ class BenchConfig:
     steps: int = 10
     warmup: int = 2
     seed: int = 1234
-    offered_load: float = 1.25          # offered GPU-equivalents per GPU
+    offered_load: float = 1.0           # offered GPU-equivalents per GPU (= capacity)
     lifetime: Tuple[int, int] = (2, 6)  # steps
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"

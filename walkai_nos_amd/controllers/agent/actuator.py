@@ -85,6 +85,11 @@ class Actuator:
                     log.debug("plan already applied and status unchanged")
                     return Result()
                 err = self.apply(plan)
+                if err is not None:
+                    # a failed plan is retried (with the runtime's back-off) instead of being
+                    # remembered as applied: the reference records it anyway (defer at
+                    # actuator.go:106) and then skips the identical retry until the status changes
+                    plan = None
             finally:
                 self.last_applied_plan, self.last_applied_status = plan, status
             self.shared.on_apply_done()

@@ -91,13 +91,67 @@ def plan_cluster(models: Mapping[str, NodeModel], required: Mapping[str, int]) -
     return changed
 
 
+def plan_cluster_fifo(models: Mapping[str, NodeModel], pending: List[Dict[str, int]],
+                      incoming: Optional[Mapping[str, int]] = None) -> Dict[str, NodeModel]:
+    """Head-of-line planning: walk the pending pods in arrival order.  A pod that fits existing free
+    capacity *reserves* it in the model (so a later flip cannot destroy it); capacity that in-flight
+    plans will provide (``incoming``) is consumed next; otherwise the best node is re-planned for
+    exactly that pod (fewest GPUs changed, then name) and the partitions the new geometry creates
+    are offered to the pods behind it.  Fair to the oldest request, and a freshly split GPU is
+    filled from the queue instead of being split again."""
+    current = {n: m.clone() for n, m in models.items()}
+    changed: Dict[str, NodeModel] = {}
+    extra = {p: q for p, q in (incoming or {}).items() if q > 0}
+    hopeless = set()  # profiles no node can provide in this pass (capacity only shrinks within a pass)
+    for req in pending:
+        placed = False
+        for name in sorted(current):
+            try:
+                current[name].add_pod(req)
+                placed = True
+                break
+            except ValueError:
+                continue
+        if not placed and all(extra.get(p, 0) >= q for p, q in req.items()):
+            for p, q in req.items():
+                extra[p] -= q
+            placed = True
+        if placed:
+            continue
+        key = tuple(sorted(req.items()))
+        if key in hopeless:
+            continue
+        best: Optional[Tuple[Tuple[int, str], str, NodeModel]] = None
+        for name, m in sorted(current.items()):
+            cand = m.clone()
+            if not cand.update_geometry_for(req):
+                continue
+            try:
+                cand.add_pod(req)
+            except ValueError:
+                continue
+            score = (_changed_gpus(m, cand), name)
+            if best is None or score < best[0]:
+                best = (score, name, cand)
+        if best is None:
+            hopeless.add(key)
+            continue  # this pod cannot be helped now; later pods may still be
+        _, name, cand = best
+        current[name] = cand
+        changed[name] = cand
+    return changed
+
+
 class PodController:
     def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
                  clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
-                 retry_after: float = 5.0, scoring: str = "fraction"):
+                 retry_after: float = 5.0, scoring: str = "fraction", policy: str = "fifo"):
         self.client = client
         self.kind = kind
         self.scoring = scoring
+        if policy not in ("fifo", "batch"):
+            raise ValueError(f"unknown planning policy {policy!r}")
+        self.policy = policy
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -113,6 +167,17 @@ class PodController:
 
     def list_nodes(self) -> List[Dict[str, Any]]:
         return self.client.list("Node", label_selector=f"{api.LABEL_GPU_PARTITIONING}={self.kind}")
+
+    def pending_pods(self) -> List[Dict[str, int]]:
+        """Per-pod requested profiles of the unschedulable pods, highest priority then oldest first."""
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending") if self.should_consider(p)]
+        pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
+        out = []
+        for p in pods:
+            r = requested_profiles(self.kind, p)
+            if r:
+                out.append(r)
+        return out
 
     def pending_requests(self) -> Dict[str, int]:
         out: Dict[str, int] = {}
@@ -162,17 +227,35 @@ class PodController:
                 return False
         return True
 
+    # -- watch mapping ------------------------------------------------------------------
+    @property
+    def plan_key(self) -> Request:
+        return Request(f"plan-{self.kind}", "")
+
+    def map_pod(self, pod: Dict[str, Any]) -> List[Request]:
+        """Every relevant pod event enqueues the same key, so a burst of pending pods is planned
+        in one pass (the queue de-duplicates) instead of one full re-plan per pod."""
+        if self.should_consider(pod) and requested_profiles(self.kind, pod):
+            return [self.plan_key]
+        return []
+
     # -- reconcile ----------------------------------------------------------------------
     def reconcile(self, req: Request) -> Result:
-        try:
-            pod = self.client.get("Pod", req.name, req.namespace)
-        except NotFound:
-            return Result()
-        if not self.should_consider(pod):
-            return Result()
-        requested = requested_profiles(self.kind, pod)
-        if not requested:
-            return Result()
+        if req == self.plan_key:
+            pending = self.pending_pods()
+            if not pending:
+                return Result()
+            requested = pending[0]
+        else:
+            try:
+                pod = self.client.get("Pod", req.name, req.namespace)
+            except NotFound:
+                return Result()
+            if not self.should_consider(pod):
+                return Result()
+            requested = requested_profiles(self.kind, pod)
+            if not requested:
+                return Result()
         now = self.clock()
         if self.batch_timeout > 0:
             if self._window_start is None:
@@ -196,19 +279,27 @@ class PodController:
         for n in flying:
             for p, q in self.incoming_free(n).items():
                 free_total[p] = free_total.get(p, 0) + q
-        if all(free_total.get(p, 0) >= q for p, q in requested.items()):
+        if req != self.plan_key and all(free_total.get(p, 0) >= q for p, q in requested.items()):
             log.debug("pod %s/%s: requested profiles free (or incoming), nothing to do", req.namespace, req.name)
             if flying:
                 return Result(requeue_after=self.retry_after)
             return Result()
-        pending = self.pending_requests() or requested
-        need = {p: q - free_total.get(p, 0) for p, q in pending.items() if q - free_total.get(p, 0) > 0}
-        if not need:
-            return Result()
-        changed = plan_cluster(models, need)
+        if self.policy == "fifo":
+            incoming: Dict[str, int] = {}
+            for n in flying:
+                for p, q in self.incoming_free(n).items():
+                    incoming[p] = incoming.get(p, 0) + q
+            changed = plan_cluster_fifo(models, self.pending_pods() or [requested], incoming)
+            need = requested
+        else:
+            pending = self.pending_requests() or requested
+            need = {p: q - free_total.get(p, 0) for p, q in pending.items() if q - free_total.get(p, 0) > 0}
+            if not need:
+                return Result()
+            changed = plan_cluster(models, need)
         REGISTRY.phase_seconds.labels(phase="plan").observe(time.perf_counter() - t0)
         if not changed:
-            log.info("pod %s/%s: no node can provide %s", req.namespace, req.name, need)
+            log.debug("%s: no node can provide %s now", req.name, need)
             return Result(requeue_after=self.retry_after)
         by_name = {ko.name(n): n for n in nodes}
         for name, model in changed.items():
@@ -216,4 +307,4 @@ class PodController:
             self.partitioner.apply_partitioning(by_name[name], plan_id, build_node_partitioning(model))
             REGISTRY.repartitions.labels(node=name, kind=self.kind).inc()
             self.plans_written += 1
-        return Result()
+        return Result(requeue_after=self.retry_after) if req == self.plan_key else Result()

@@ -166,7 +166,7 @@ class SimCluster:
     def __init__(self, n_nodes: int = 1, gpus_per_node: int = 8, model: str = "MI355X",
                  kind: str = api.PARTITIONING_KIND_XCP, refresh_interval: float = 10.0,
                  batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None,
-                 scoring: str = "fraction"):
+                 scoring: str = "fraction", policy: str = "fifo"):
         self.clock = clock or SimClock()
         self.api = InMemoryAPIServer(clock=self.clock)
         self.kind = kind
@@ -177,7 +177,7 @@ class SimCluster:
         # control plane
         self.partitioner_mgr = Manager(self.api, clock=self.clock)
         self.pod_controllers, _ = setup_partitioner(self.partitioner_mgr, kinds=(kind,), batch_timeout=batch_timeout,
-                                                    batch_idle=batch_idle, scoring=scoring)
+                                                    batch_idle=batch_idle, scoring=scoring, policy=policy)
         self.scheduler_mgr = Manager(self.api, clock=self.clock)
         self.scheduler = SimScheduler(self.api, self.nodes, self._on_bind)
         self.scheduler_mgr.new_controller("sim-scheduler", self.scheduler.reconcile,
