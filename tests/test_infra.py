@@ -1,0 +1,158 @@
+"""Infrastructure: kubelet PodResources gRPC (real unix socket), commit barriers (threads, and a
+2-rank gloo process group), batcher, utilities, metrics, workload parity."""
+import os
+import tempfile
+import threading
+
+import pytest
+
+from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+from walkai_nos_amd.device.partition_client import PartitionClient
+from walkai_nos_amd.device.podresources import PodResourcesClient, PodResourcesServer
+from walkai_nos_amd.parallel.barrier import LocalBarrier
+from walkai_nos_amd.utils.batcher import Batcher
+from walkai_nos_amd.utils.util import hash_fnv32a, local_endpoint, unordered_equal
+
+
+def test_podresources_grpc_roundtrip_and_partition_client():
+    smi = FakeAmdSmi(n_gpus=2)
+    smi.set_compute_partition(1, "QPX")
+    alloc = [(f"amd.com/{d.compute_mode.lower()}_{d.memory_mode.lower()}", d.device_id) for d in smi.logical_devices()]
+    used_id = alloc[2][1]  # first QPX partition of GPU 1
+    with tempfile.TemporaryDirectory() as d:
+        sock = os.path.join(d, "kubelet.sock")
+        srv = PodResourcesServer(sock, used=lambda: [("w", "ns", [(alloc[2][0], [used_id])])],
+                                 allocatable=lambda: [(r, [i]) for r, i in alloc]).start()
+        try:
+            c = PodResourcesClient(sock, timeout=5)
+            used = c.get_used_devices()
+            assert [(x.resource_name, x.device_id, x.status) for x in used] == [("amd.com/qpx_nps1", used_id, "used")]
+            assert len(c.get_allocatable_devices()) == 5  # 1 SPX + 4 QPX
+            devs = PartitionClient(c, smi).get_partition_devices()
+            by = {(x.gpu_index, x.status) for x in devs}
+            assert by == {(0, "free"), (1, "used"), (1, "free")}
+            assert sum(1 for x in devs if x.gpu_index == 1 and x.is_free()) == 3
+            c.close()
+        finally:
+            srv.stop()
+
+
+def test_local_barrier_threads_all_or_nothing():
+    b = LocalBarrier(3, timeout=5)
+    results = []
+
+    def voter(ok):
+        results.append(b.vote(ok))
+
+    ts = [threading.Thread(target=voter, args=(v,)) for v in (True, True, True)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert results == [True, True, True]
+    results.clear()
+    ts = [threading.Thread(target=voter, args=(v,)) for v in (True, False, True)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert results == [False, False, False]
+
+
+def _gloo_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from walkai_nos_amd.parallel.barrier import TorchBarrier
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        b = TorchBarrier()
+        ok_all = b.vote(True)
+        veto = b.vote(rank != 1)
+        q.put((rank, ok_all, veto))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_torch_barrier_two_ranks_gloo():
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_worker, args=(r, 2, port, q)) for r in range(2)]
+    [p.start() for p in ps]
+    [p.join(120) for p in ps]
+    out = sorted(q.get(timeout=10) for _ in range(2))
+    assert out == [(0, True, False), (1, True, False)]
+
+
+def test_batcher_timeout_and_idle_windows():
+    t = [0.0]
+    b = Batcher(timeout_s=10, idle_s=3, clock=lambda: t[0])
+    assert not b.add(1)  # not started -> dropped
+    b.start()
+    assert b.add(1)
+    t[0] = 2
+    b.add(2)
+    t[0] = 4.9
+    assert b.ready() is None
+    t[0] = 5.0  # idle window (3 s after the last add) expired
+    assert b.ready() == [1, 2]
+    b.add(3)
+    for k in range(1, 11):  # keep adding within the idle window; the 10 s timeout still fires
+        t[0] = 5.0 + k
+        b.add(k)
+    assert b.ready() is not None
+    assert b.flush() == []
+
+
+def test_utils():
+    assert unordered_equal([1, 2, 2], [2, 1, 2]) and not unordered_equal([1, 2], [1, 2, 2])
+    assert unordered_equal([{"a": 1}, {"b": 2}], [{"b": 2}, {"a": 1}])
+    assert hash_fnv32a("") == 0x811C9DC5 and hash_fnv32a("a") == 0xE40C292C
+    assert local_endpoint("/tmp/x.sock") == "unix:///tmp/x.sock"
+
+
+def test_metrics_render():
+    from walkai_nos_amd.utils.metrics import Metrics
+    m = Metrics()
+    m.node_utilization.labels(node="n").set(87.5)
+    m.probe_tflops_per_cu.labels(node="n", gpu="0", slice="cpx0", dtype="fp32").set(0.5)
+    out = m.render().decode()
+    assert 'nos_node_gpu_utilization_percent{node="n"} 87.5' in out
+    assert "nos_probe_tflops_per_cu" in out
+
+
+def test_yolos_matches_transformers_reference():
+    torch = pytest.importorskip("torch")
+    transformers = pytest.importorskip("transformers")
+    from walkai_nos_amd.models.workload.yolos import YolosConfig, YolosSmall, demo_input
+    cfg = transformers.YolosConfig(hidden_size=384, num_hidden_layers=2, num_attention_heads=6,
+                                   intermediate_size=1536, image_size=[800, 1333], num_labels=91,
+                                   use_mid_position_embeddings=False)
+    torch.manual_seed(0)
+    hf = transformers.YolosForObjectDetection(cfg).eval()
+    m = YolosSmall(YolosConfig(num_layers=2)).eval()
+    m.load_hf_state_dict(hf.state_dict())
+    x = demo_input(1, (160, 224))
+    with torch.no_grad():
+        ref = hf(pixel_values=x)
+        logits, boxes = m(x)
+    assert (ref.logits - logits).abs().max().item() < 1e-5
+    assert (ref.pred_boxes - boxes).abs().max().item() < 1e-5
+    assert YolosSmall().flops_per_inference() == pytest.approx(359.6e9, rel=1e-3)
+
+
+def test_bench_control_plane_and_slice_masks():
+    from walkai_nos_amd.bench_core import BenchConfig, ChurnProcess, NodeBench, slice_cus
+    assert slice_cus("spx_nps1", 0) is None
+    assert slice_cus("cpx_nps1", 3) == list(range(96, 128))
+    assert len(slice_cus("dpx_nps1", 1)) == 128
+    # every CPX slice covers all 8 XCDs (bit i -> XCD i mod 8)
+    assert {c % 8 for c in slice_cus("cpx_nps1", 5)} == set(range(8))
+    a, b = ChurnProcess(BenchConfig(seed=7)), ChurnProcess(BenchConfig(seed=7))
+    assert [a.arrivals() for _ in range(20)] == [b.arrivals() for _ in range(20)]
+    nb = NodeBench(BenchConfig(gpus=2), gpu_data_plane=False)
+    for _ in range(10):
+        nb.control_step()
+        nb.data_step()
+    assert nb.inferences > 0 and max(nb.util_samples) > 0

@@ -1,0 +1,114 @@
+"""CU-mask slicing: B.7 geometry update (reference pkg/gpu/slicing/gpu_test.go:122-343 vectors),
+2-D budgets, XCD-symmetric CU placement, the slice agent plan and the cumask end-to-end path."""
+import pytest
+
+from walkai_nos_amd.controllers.sliceagent.agent import plan_slices
+from walkai_nos_amd.kube import objects as ko
+from walkai_nos_amd.models.annotation import SpecAnnotation
+from walkai_nos_amd.models.errors import GpuError
+from walkai_nos_amd.models.slicing.cumask import Slice, cus_of, hsa_cu_mask, mask_hex, place
+from walkai_nos_amd.models.slicing.gpu import SlicingGPU, SlicingNode
+from walkai_nos_amd.models.slicing.profile import (SliceProfile, extract_gpu_id, extract_profile_name, new_profile,
+                                                   parse_profile)
+from walkai_nos_amd.sim.cluster import SimCluster
+
+
+def sg(mem, used=None, free=None, cus=256):
+    g = SlicingGPU("MI355X", 0, mem, cus, dict(used or {}), dict(free or {}))
+    g.validate()
+    return g
+
+
+@pytest.mark.parametrize("gpu,required,expected,updated", [
+    (sg(40, {"10gb": 2}, {"20gb": 1}), {}, {"10gb": 2, "20gb": 1}, False),
+    (sg(40, {}, {"20gb": 2}), {"20gb": 2}, {"20gb": 2}, False),
+    (sg(40, {"20gb": 2}), {"10gb": 1, "20gb": 1}, {"20gb": 2}, False),                      # full GPU
+    (sg(60, {"10gb": 1}), {"10gb": 1, "20gb": 2}, {"10gb": 2, "20gb": 2}, True),           # spare capacity
+    (sg(40), {"10gb": 5}, {"10gb": 4}, True),                                              # capped by memory
+    (sg(40), {"20gb": 2, "10gb": 2, "5gb": 2}, {"5gb": 2, "10gb": 2}, True),                # smaller first
+    (sg(40, {"20gb": 1}, {"10gb": 2}), {"20gb": 1}, {"20gb": 2}, True),                     # delete free to fit
+])
+def test_update_geometry_for_reference_vectors(gpu, required, expected, updated):
+    assert gpu.update_geometry_for(required) is updated
+    assert gpu.geometry() == expected
+
+
+def test_free_slices_kept_when_spare_capacity_suffices():
+    g = sg(40, {"10gb": 2}, {"5gb": 1})
+    assert g.update_geometry_for({"10gb": 1})
+    assert g.geometry() == {"10gb": 3, "5gb": 1}
+
+
+def test_validation_and_cu_budget():
+    with pytest.raises(ValueError):
+        sg(40, {"30gb": 2})
+    with pytest.raises(ValueError):
+        SlicingGPU("MI355X", 0, 288, 256, {"12cu.10gb": 1}).validate()  # not a multiple of 8 CUs
+    g = SlicingGPU.full("MI355X", 0, 288, 256)
+    assert g.update_geometry_for({"128cu.100gb": 3})
+    assert g.geometry() == {"128cu.100gb": 2}  # 256 dedicated CUs max
+    g2 = SlicingGPU.full("MI355X", 0, 288, 256)
+    g2.create_slices("10gb", 1)  # a shared slice reserves 8 CUs for the shared pool
+    assert not g2.create_slices("256cu.10gb", 1)
+    assert g2.create_slices("248cu.10gb", 1)
+
+
+def test_profiles():
+    assert parse_profile("32cu.36gb") == SliceProfile(36, 32)
+    assert parse_profile("10gb") == SliceProfile(10, 0) and not parse_profile("10gb").dedicated
+    assert new_profile(36, 32) == "32cu.36gb"
+    assert extract_profile_name("amd.com/gpu-32cu.36gb") == "32cu.36gb"
+    assert extract_profile_name("amd.com/gpu") is None and extract_profile_name("amd.com/cpx_nps1") is None
+    assert extract_gpu_id("0000:a4:00.0::s3") == "0000:a4:00.0"
+    assert parse_profile("32cu.36gb") < parse_profile("32cu.40gb") < parse_profile("8cu.64gb")
+
+
+def test_cumask_rows_are_xcd_symmetric_and_used_slices_stay():
+    keep = [Slice("g::s0", "128cu.144gb", list(range(16)))]
+    placed = place(keep, [("g::s1", "32cu.36gb"), ("g::s2", "64cu.72gb")], 256)
+    by = {s.id: s for s in placed}
+    assert by["g::s2"].rows == [16, 17, 18, 19, 20, 21, 22, 23]  # largest first, contiguous
+    assert by["g::s1"].rows == [24, 25, 26, 27]
+    for s in placed:
+        assert {c % 8 for c in s.cus} == set(range(8))  # every XCD
+    assert hsa_cu_mask(by["g::s1"].cus) == "0:192-223"
+    assert mask_hex(range(32)) == "ffffffff," + ",".join(["00000000"] * 7)
+    shared = Slice("g::s3", "10gb")
+    assert len(cus_of(shared, keep + placed + [shared], 256)) == 256 - 128 - 32 - 64
+    with pytest.raises(ValueError):
+        place(keep + placed, [("g::s4", "128cu.10gb")], 256)
+
+
+def test_slice_plan_deletes_free_keeps_used_and_checks_budgets():
+    cur = {0: [Slice("g::s0", "256cu.288gb", list(range(32)))]}
+    plan = plan_slices(cur, set(), [SpecAnnotation("32cu.36gb", 0, 3)], {0: "g"}, 288, 256)
+    assert plan.deleted == ["g::s0"] and len(plan.created) == 3
+    assert [s.profile for s in plan.new[0]] == ["32cu.36gb"] * 3
+    # a used slice is never deleted even if the spec drops it
+    cur = {0: [Slice("g::s0", "64cu.72gb", list(range(8)))]}
+    plan = plan_slices(cur, {"g::s0"}, [SpecAnnotation("32cu.36gb", 0, 1)], {0: "g"}, 288, 256)
+    assert plan.deleted == [] and plan.blocked and len(plan.new[0]) == 2
+    with pytest.raises(GpuError):
+        plan_slices({}, set(), [SpecAnnotation("32cu.100gb", 0, 3)], {0: "g"}, 288, 256)
+
+
+def test_cumask_end_to_end_heterogeneous_slices_on_one_gpu():
+    c = SimCluster(n_nodes=1, gpus_per_node=1, kind="cumask")
+    c.run(30)
+    a = ko.annotations(c.api.get("Node", "node-0"))
+    assert a["nos.nebuly.com/status-gpu-0-256cu.288gb-free"] == "1"
+    for _ in range(4):
+        c.submit({"amd.com/gpu-32cu.36gb": 1})
+    c.submit({"amd.com/gpu-128cu.144gb": 1})
+    c.run(60)
+    assert len(c.running_pods()) == 5 and c.utilization() == 100.0
+    slices = c.nodes["node-0"].plugin.store.load()[0]
+    rows = [r for s in slices for r in s.rows]
+    assert len(rows) == len(set(rows)) == 32  # disjoint, every CU owned once
+
+
+def test_slicing_node_greedy():
+    n = SlicingNode("n", [SlicingGPU.full("MI355X", 0, 288), SlicingGPU.full("MI355X", 1, 288)])
+    assert n.update_geometry_for({"32cu.36gb": 10})
+    assert n.gpus[0].geometry() == {"32cu.36gb": 8} and n.gpus[1].geometry() == {"32cu.36gb": 2}
+    assert n.allocatable["amd.com/gpu-32cu.36gb"] == 10

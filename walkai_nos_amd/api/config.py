@@ -1,0 +1,204 @@
+"""``config.nos.nebuly.com/v1alpha1`` ComponentConfigs and the capacity-scheduling plugin args.
+
+Field names follow the reference (``pkg/api/nos.nebuly.com/config/v1alpha1/*``,
+``config/*/manager/*_config.yaml``) so existing config files load unchanged:
+
+* ``GpuPartitionerConfig`` — manager options plus ``batchWindowTimeoutSeconds``,
+  ``batchWindowIdleSeconds``, ``knownMigGeometriesFile`` (alias ``knownGeometriesFile``),
+  ``schedulerConfigFile``, ``devicePluginConfigMap{name,namespace}``, ``devicePluginDelaySeconds``;
+  MI355X additions ``planningPolicy`` (``fifo``|``batch``) and ``scoring`` (``fraction``|``pods``);
+* ``MigAgentConfig`` (the partition agent; also accepted as ``PartitionAgentConfig``) and
+  ``GpuAgentConfig`` (the CU-mask slice agent; also ``SliceAgentConfig``) with
+  ``reportConfigIntervalSeconds``;
+* ``CapacitySchedulingArgs`` with ``nvidiaGpuResourceMemoryGB`` (reference name, kept) and its AMD
+  alias ``amdGpuResourceMemoryGB``.
+
+Unlike the reference, ``validate()`` is actually called by every entry point and an
+omitted report interval means the documented 10 s rather than "no periodic report" (Q5).
+"""
+from __future__ import annotations
+
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, Optional, Type, TypeVar
+
+import yaml
+
+from .. import constant
+
+API_VERSION = "config.nos.nebuly.com/v1alpha1"
+
+
+@dataclass
+class LeaderElection:
+    leaderElect: bool = False
+    resourceName: str = ""
+    resourceNamespace: str = "nos-system"
+    leaseDurationSeconds: float = 15.0
+    renewDeadlineSeconds: float = 10.0
+    retryPeriodSeconds: float = 2.0
+    leaderElectionReleaseOnCancel: bool = False
+
+
+@dataclass
+class ManagerConfig:
+    healthProbeBindAddress: str = ":8081"
+    metricsBindAddress: str = "127.0.0.1:8080"
+    webhookPort: int = 9443
+    leaderElection: LeaderElection = field(default_factory=LeaderElection)
+
+    def validate(self) -> None:
+        le = self.leaderElection
+        if le.leaderElect and not le.resourceName:
+            raise ValueError("leaderElection.resourceName is required when leaderElect is true")
+        if le.leaderElect and not (le.leaseDurationSeconds > le.renewDeadlineSeconds > le.retryPeriodSeconds > 0):
+            raise ValueError("leaderElection durations must satisfy leaseDuration > renewDeadline > retryPeriod > 0")
+
+
+@dataclass
+class NamespacedObject:
+    name: str = ""
+    namespace: str = ""
+
+
+@dataclass
+class GpuPartitionerConfig(ManagerConfig):
+    schedulerConfigFile: str = ""
+    knownMigGeometriesFile: str = ""
+    batchWindowTimeoutSeconds: float = 60.0
+    batchWindowIdleSeconds: float = 10.0
+    devicePluginConfigMap: NamespacedObject = field(default_factory=lambda: NamespacedObject(
+        constant.DEFAULT_DEVICE_PLUGIN_CONFIGMAP_NAME, constant.DEFAULT_DEVICE_PLUGIN_CONFIGMAP_NAMESPACE))
+    devicePluginDelaySeconds: float = 5.0
+    planningPolicy: str = "fifo"
+    scoring: str = "fraction"
+
+    def validate(self) -> None:
+        super().validate()
+        if self.batchWindowTimeoutSeconds <= 0:
+            raise ValueError("batchWindowTimeoutSeconds must be greater than 0")
+        if self.batchWindowIdleSeconds <= 0:
+            raise ValueError("batchWindowIdleSeconds must be greater than 0")
+        if self.devicePluginDelaySeconds <= 0:
+            raise ValueError("devicePluginDelaySeconds must be greater than 0")
+        if self.planningPolicy not in ("fifo", "batch"):
+            raise ValueError("planningPolicy must be 'fifo' or 'batch'")
+        if self.scoring not in ("fraction", "pods"):
+            raise ValueError("scoring must be 'fraction' or 'pods'")
+
+
+@dataclass
+class AgentConfig(ManagerConfig):
+    reportConfigIntervalSeconds: float = 10.0
+    amdSmiBackend: str = "native"           # native | fake
+    devicePluginLabel: str = constant.DEFAULT_DEVICE_PLUGIN_LABEL
+    devicePluginNamespace: str = ""
+    podResourcesSocket: str = constant.DEFAULT_POD_RESOURCES_SOCKET
+    commitBarrier: str = "rccl"             # rccl | none
+    probeOnCommit: bool = True
+
+    def validate(self) -> None:
+        super().validate()
+        if self.reportConfigIntervalSeconds <= 0:
+            raise ValueError("reportConfigIntervalSeconds must be greater than 0")
+        if self.amdSmiBackend not in ("native", "fake"):
+            raise ValueError("amdSmiBackend must be 'native' or 'fake'")
+        if self.commitBarrier not in ("rccl", "none"):
+            raise ValueError("commitBarrier must be 'rccl' or 'none'")
+
+
+@dataclass
+class MigAgentConfig(AgentConfig):
+    """Partition agent configuration (kind kept from the reference for config compatibility)."""
+
+
+@dataclass
+class GpuAgentConfig(AgentConfig):
+    """CU-mask slice agent configuration (kind kept from the reference)."""
+    hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
+
+
+@dataclass
+class CapacitySchedulingArgs:
+    nvidiaGpuResourceMemoryGB: int = constant.DEFAULT_GPU_RESOURCE_MEMORY_GB
+
+    def validate(self) -> None:
+        if self.nvidiaGpuResourceMemoryGB <= 0:
+            raise ValueError("GPU resource memory must be greater than 0")
+
+
+KINDS: Dict[str, Type[Any]] = {
+    "GpuPartitionerConfig": GpuPartitionerConfig,
+    "MigAgentConfig": MigAgentConfig,
+    "PartitionAgentConfig": MigAgentConfig,
+    "GpuAgentConfig": GpuAgentConfig,
+    "SliceAgentConfig": GpuAgentConfig,
+    "CapacitySchedulingArgs": CapacitySchedulingArgs,
+}
+
+T = TypeVar("T")
+
+
+def _flatten(doc: Dict[str, Any]) -> Dict[str, Any]:
+    """controller-runtime nests manager options; flatten them onto the dataclass fields."""
+    out = dict(doc)
+    health = out.pop("health", None) or {}
+    if "healthProbeBindAddress" in health:
+        out["healthProbeBindAddress"] = health["healthProbeBindAddress"]
+    metrics = out.pop("metrics", None) or {}
+    if "bindAddress" in metrics:
+        out["metricsBindAddress"] = metrics["bindAddress"]
+    webhook = out.pop("webhook", None) or {}
+    if "port" in webhook:
+        out["webhookPort"] = webhook["port"]
+    if "knownGeometriesFile" in out:
+        out["knownMigGeometriesFile"] = out.pop("knownGeometriesFile")
+    if "amdGpuResourceMemoryGB" in out:
+        out["nvidiaGpuResourceMemoryGB"] = out.pop("amdGpuResourceMemoryGB")
+    for dur in ("leaseDuration", "renewDeadline", "retryPeriod"):
+        le = out.get("leaderElection")
+        if isinstance(le, dict) and dur in le:
+            v = str(le.pop(dur)).rstrip("s")
+            le[dur + "Seconds"] = float(v)
+    return out
+
+
+def _build(cls: Type[T], data: Dict[str, Any]) -> T:
+    kwargs = {}
+    fields = getattr(cls, "__dataclass_fields__", {})
+    for k, v in data.items():
+        if k not in fields:
+            raise ValueError(f"{cls.__name__}: unknown field {k!r}")
+        ftype = fields[k].type
+        if k == "leaderElection" and isinstance(v, dict):
+            v = _build(LeaderElection, v)
+        elif k == "devicePluginConfigMap" and isinstance(v, dict):
+            v = _build(NamespacedObject, v)
+        kwargs[k] = v
+        del ftype
+    return cls(**kwargs)
+
+
+def load_config(text: str, expected_kind: Optional[str] = None, validate: bool = True) -> Any:
+    doc = yaml.safe_load(text) or {}
+    kind = doc.pop("kind", expected_kind)
+    api_version = doc.pop("apiVersion", API_VERSION)
+    if api_version not in (API_VERSION, "kubescheduler.config.k8s.io/v1beta3", "nos.nebuly.com/v1alpha1"):
+        raise ValueError(f"unsupported apiVersion {api_version!r}")
+    if kind not in KINDS:
+        raise ValueError(f"unknown config kind {kind!r}")
+    if expected_kind and KINDS[kind] is not KINDS[expected_kind]:
+        raise ValueError(f"expected kind {expected_kind}, got {kind}")
+    cfg = _build(KINDS[kind], _flatten(doc))
+    if validate:
+        cfg.validate()
+    return cfg
+
+
+def load_config_file(path: str, expected_kind: Optional[str] = None) -> Any:
+    with open(path) as f:
+        return load_config(f.read(), expected_kind)
+
+
+def dump_config(cfg: Any, kind: str) -> str:
+    d = asdict(cfg)
+    return yaml.safe_dump({"apiVersion": API_VERSION, "kind": kind, **d}, sort_keys=False)

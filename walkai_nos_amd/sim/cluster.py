@@ -30,7 +30,16 @@ from ..kube.errors import Conflict, NotFound
 from ..kube.memory import InMemoryAPIServer
 from ..kube.runtime import Manager, Request, Result, SimClock, Watch, run_until_idle
 from ..models import resource as res
+from ..controllers.sliceagent.agent import setup_slice_agent
+from ..device.slicing_client import MemorySliceStore, SlicingClient
+from ..models.slicing.profile import as_resource_name as slice_resource
+from ..models.slicing.profile import extract_profile_name as slice_profile_name
+from ..models.slicing.profile import is_slice_resource, parse_profile as parse_slice_profile
 from ..models.xcp.profile import COMPUTE_MODES, extract_profile_name, is_xcp_resource
+
+
+def is_managed(r: str) -> bool:
+    return is_xcp_resource(r) or is_slice_resource(r)
 from ..parallel.barrier import LocalBarrier
 from ..utils import pod as podutil
 
@@ -41,16 +50,23 @@ DP_LABEL_KEY, DP_LABEL_VALUE = constant.DEFAULT_DEVICE_PLUGIN_LABEL.split("=")
 
 
 class SimDevicePlugin:
-    """Advertises one device per logical partition of each GPU (AMD device plugin, mixed naming)."""
+    """xcp: one device per logical partition of each GPU (AMD device plugin, mixed naming);
+    cumask: one device per slice of the slice store (the nos device plugin)."""
 
-    def __init__(self, smi: FakeAmdSmi):
+    def __init__(self, smi: FakeAmdSmi, store: Optional[MemorySliceStore] = None):
         self.smi = smi
+        self.store = store
         self.advertised: Dict[str, List[str]] = {}
         self.registrations = 0
         self.reregister()
 
     def current(self) -> Dict[str, List[str]]:
         out: Dict[str, List[str]] = defaultdict(list)
+        if self.store is not None:
+            for g, slices in sorted(self.store.load().items()):
+                for s in slices:
+                    out[slice_resource(s.profile)].append(s.id)
+            return dict(out)
         for d in self.smi.logical_devices():
             out[f"amd.com/{d.compute_mode.lower()}_{d.memory_mode.lower()}"].append(d.device_id)
         return dict(out)
@@ -77,14 +93,14 @@ class SimKubelet:
         return [i for i in self.plugin.advertised.get(resource, []) if i not in used]
 
     def can_fit(self, req: Dict[str, int]) -> bool:
-        return all(len(self.free_devices(r)) >= q for r, q in req.items() if is_xcp_resource(r))
+        return all(len(self.free_devices(r)) >= q for r, q in req.items() if is_managed(r))
 
     def allocate(self, pod_key: Tuple[str, str], req: Dict[str, int]) -> List[Tuple[str, str]]:
         """GetPreferredAllocation semantics: pack onto the GPU that already has the most partitions
         in use, so whole GPUs stay idle for future mode flips (fragmentation control)."""
         out: List[Tuple[str, str]] = []
         for r, q in req.items():
-            if not is_xcp_resource(r):
+            if not is_managed(r):
                 continue
             free = self.free_devices(r)
             used_per_gpu: Dict[int, int] = defaultdict(int)
@@ -190,20 +206,27 @@ class SimCluster:
     # -- topology -----------------------------------------------------------------------
     def add_node(self, name: str, n_gpus: int, model: str, refresh_interval: float) -> SimNode:
         smi = FakeAmdSmi(n_gpus=n_gpus, model=model)
-        plugin = SimDevicePlugin(smi)
+        store = MemorySliceStore() if self.kind == api.PARTITIONING_KIND_CUMASK else None
+        plugin = SimDevicePlugin(smi, store)
         kubelet = SimKubelet(name, plugin, smi)
         labels = {api.LABEL_GPU_PARTITIONING: self.kind, constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}",
-                  constant.LABEL_AMD_GPU_COUNT: str(n_gpus)}
+                  constant.LABEL_AMD_GPU_COUNT: str(n_gpus), constant.LABEL_AMD_GPU_VRAM: "288G",
+                  constant.LABEL_AMD_GPU_CU_COUNT: "256"}
         self.api.create(ko.new_node(name, labels, allocatable=kubelet.allocatable()))
         mgr = Manager(self.api, clock=self.clock)
         sn = SimNode(name, smi, plugin, kubelet, mgr)
         self.nodes[name] = sn
         self._create_dp_pod(sn)
-        pc = PartitionClient(kubelet.resource_client(), smi)
         dp = DevicePluginClient(self.api, namespace=DP_NAMESPACE, poll_interval=0.5, sleep=lambda s: self.clock.advance(s),
                                 clock=self.clock)
-        setup_partition_agent(mgr, name, pc, device_plugin=dp, barrier_factory=lambda n: LocalBarrier(n),
+        if store is not None:
+            sc = SlicingClient(kubelet.resource_client(), smi)
+            setup_slice_agent(mgr, name, sc, store, device_plugin=dp, barrier_factory=lambda n: LocalBarrier(n),
                               refresh_interval=refresh_interval)
+        else:
+            pc = PartitionClient(kubelet.resource_client(), smi)
+            setup_partition_agent(mgr, name, pc, device_plugin=dp, barrier_factory=lambda n: LocalBarrier(n),
+                                  refresh_interval=refresh_interval)
         return sn
 
     def _create_dp_pod(self, sn: SimNode) -> None:
@@ -270,10 +293,15 @@ class SimCluster:
                 out[(sn.name, g.index)] = 0.0
             for r, i in ((r, i) for devs in sn.kubelet.allocations.values() for r, i in devs):
                 p = extract_profile_name(r)
-                if p is None:
+                if p is not None:
+                    out[(sn.name, sn.smi.gpu_index_of(i))] += 1.0 / COMPUTE_MODES[p.split("_", 1)[0]]
                     continue
-                mode = p.split("_", 1)[0]
-                out[(sn.name, sn.smi.gpu_index_of(i))] += 1.0 / COMPUTE_MODES[mode]
+                sp = slice_profile_name(r)
+                if sp is not None:
+                    prof = parse_slice_profile(sp)
+                    spec = sn.smi.list_gpus()[0]
+                    frac = max(prof.cus / spec.cu_count, prof.memory_gb * 1e9 / spec.vram_bytes)
+                    out[(sn.name, sn.smi.gpu_index_of(i))] += frac
         return out
 
     def utilization(self) -> float:
