@@ -1,0 +1,111 @@
+"""Elastic Resource Quota: calculator, fair-share arithmetic (key-concepts.md worked example),
+operator status/labels, and the nos-scheduler borrowing + preemption across 8 simulated MI355X."""
+import pytest
+
+from walkai_nos_amd.api import v1alpha1 as api
+from walkai_nos_amd.kube import objects as ko
+from walkai_nos_amd.kube.memory import InMemoryAPIServer
+from walkai_nos_amd.kube.runtime import Request
+from walkai_nos_amd.quota.elasticquota import QuotaInfo, QuotaSet, capacity_labels, validate_cluster, validate_quota
+from walkai_nos_amd.quota.gpu_memory import GpuMemoryCalculator
+from walkai_nos_amd.quota.operator import QuotaOperator
+from walkai_nos_amd.sim.cluster import SimCluster
+
+GM = api.RESOURCE_GPU_MEMORY
+
+
+def eq(name, ns, mn, mx=None, kind=api.KIND_ELASTIC_QUOTA, namespaces=None):
+    spec = {"min": {k: str(v) for k, v in mn.items()}}
+    if mx is not None:
+        spec["max"] = {k: str(v) for k, v in mx.items()}
+    if namespaces is not None:
+        spec["namespaces"] = namespaces
+    return {"apiVersion": api.API_VERSION, "kind": kind, "metadata": {"name": name, "namespace": ns}, "spec": spec}
+
+
+def test_gpu_memory_calculator():
+    c = GpuMemoryCalculator(gpu_resource_memory_gb=288)
+    assert c.required_gb({"amd.com/gpu": 1}) == 288
+    assert c.required_gb({"amd.com/cpx_nps1": 2}) == 72
+    assert c.required_gb({"amd.com/dpx_nps1": 1, "amd.com/gpu-32cu.36gb": 1, "amd.com/gpu-10gb": 2}) == 144 + 36 + 20
+    # the reference docs' example: 1g.10gb + 1 nvidia.com/gpu (32 GB) = 42
+    assert c.required_gb({"nvidia.com/mig-1g.10gb": 1, "nvidia.com/gpu": 1}) == 42
+    pod = ko.new_pod("p", requests={"amd.com/cpx_nps1": 1, "cpu": "2"})
+    assert c.pod_request(pod)[GM] == 36
+
+
+def test_fair_share_worked_example():
+    qa = QuotaInfo("a", "a", {"a"}, {GM: 40}, None, {GM: 40})
+    qb = QuotaInfo("b", "b", {"b"}, {GM: 10}, None, {GM: 40})
+    qc = QuotaInfo("c", "c", {"c"}, {GM: 30}, None, {GM: 0})
+    qs = QuotaSet([qa, qb, qc])
+    assert qs.available_over_quota(GM) == 30
+    assert qs.guaranteed_over_quota(qa, GM) == pytest.approx(15)
+    assert qs.guaranteed_over_quota(qb, GM) == pytest.approx(3.75)  # 10/80*30 (docs round to 3)
+    assert qs.may_preempt(qa, {GM: 10}, qb)          # 40+10 <= 40+15 and 30 > 3.75
+    assert not qs.may_preempt(qa, {GM: 20}, qb)      # 40+20 > 55
+    assert not qs.may_preempt(qb, {GM: 10}, qa)      # A is not over its guaranteed share
+    assert qs.can_borrow(qc, {GM: 10})               # within min
+    assert not qs.can_borrow(qb, {GM: 10})           # B already over min, and 80+10 > 80
+
+
+def test_validation():
+    assert validate_quota(eq("q", "ns", {GM: 10}, {GM: 5}))
+    assert not validate_quota(eq("q", "ns", {GM: 10}, {GM: 20}))
+    a = QuotaInfo.from_object(eq("a", "ns1", {GM: 1}))
+    c = QuotaInfo.from_object(eq("c", "x", {GM: 1}, kind=api.KIND_COMPOSITE_ELASTIC_QUOTA, namespaces=["ns1", "ns2"]))
+    assert validate_cluster([a, c]) and not validate_cluster([a])
+
+
+def test_capacity_labels_creation_order_then_smaller_request():
+    q = QuotaInfo("q", "ns", {"ns"}, {GM: 50}, None)
+    pods = []
+    for name, ts, gm in (("old", "2024-01-01T00:00:00Z", 36), ("tie-big", "2024-01-02T00:00:00Z", 36),
+                         ("tie-small", "2024-01-02T00:00:00Z", 10), ("pending", "2024-01-03T00:00:00Z", 10)):
+        p = ko.new_pod(name, "ns", requests={GM: gm}, phase="Running" if name != "pending" else "Pending")
+        p["metadata"]["creationTimestamp"] = ts
+        pods.append(p)
+    labels = capacity_labels(pods, q, lambda p: {GM: int(p["spec"]["containers"][0]["resources"]["requests"][GM])})
+    assert labels == {"ns/old": "in-quota", "ns/tie-small": "in-quota", "ns/tie-big": "over-quota"}
+
+
+def test_operator_updates_used_and_labels():
+    a = InMemoryAPIServer()
+    a.create(eq("qa", "team-a", {GM: 36}))
+    for i, phase in enumerate(("Running", "Running", "Pending")):
+        a.create(ko.new_pod(f"p{i}", "team-a", requests={"amd.com/cpx_nps1": 1}, phase=phase))
+    op = QuotaOperator(a)
+    op.reconcile(Request(f"{api.KIND_ELASTIC_QUOTA}|qa", "team-a"))
+    q = a.get(api.KIND_ELASTIC_QUOTA, "qa", "team-a")
+    assert q["status"]["used"] == {GM: "72"}
+    assert q["status"]["conditions"][0]["status"] == "True"
+    lbl = {ko.name(p): ko.labels(p).get(api.LABEL_CAPACITY_INFO) for p in a.list("Pod", namespace="team-a")}
+    assert lbl == {"p0": "in-quota", "p1": "over-quota", "p2": None}
+
+
+def test_two_namespaces_borrow_and_reclaim_on_eight_gpus():
+    c = SimCluster(n_nodes=1, gpus_per_node=8, kind="cumask", elastic_quota=True)
+    c.run(30)
+    # each team is guaranteed half of the node's 8 x 288 GB of HBM
+    for team in ("team-a", "team-b"):
+        c.api.create(eq(f"q-{team}", team, {GM: 4 * 288}))
+    c.run(10)
+    slice_ = {"amd.com/gpu-128cu.144gb": 1}  # half a GPU
+    for i in range(16):  # team-a fills the whole node: 8 slices in quota, 8 borrowed
+        c.submit(slice_, name=f"a{i}", namespace="team-a", scheduler_name="nos-scheduler")
+    c.run(300)
+    running_a = [p for p in c.running_pods() if ko.namespace(p) == "team-a"]
+    assert len(running_a) == 16
+    over = [p for p in running_a if ko.labels(p).get(api.LABEL_CAPACITY_INFO) == "over-quota"]
+    assert len(over) == 8
+    qa = c.api.get(api.KIND_ELASTIC_QUOTA, "q-team-a", "team-a")
+    assert qa["status"]["used"][GM] == str(16 * 144)
+    # team-b claims back its guaranteed share: over-quota pods of team-a are preempted
+    for i in range(4):
+        c.submit(slice_, name=f"b{i}", namespace="team-b", scheduler_name="nos-scheduler")
+    c.run(300)
+    running_b = [p for p in c.running_pods() if ko.namespace(p) == "team-b"]
+    assert len(running_b) == 4
+    assert c.nos_scheduler.preempted >= 4
+    assert len([p for p in c.running_pods() if ko.namespace(p) == "team-a"]) == 12
+    assert c.utilization() == 100.0

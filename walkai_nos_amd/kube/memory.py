@@ -31,7 +31,8 @@ from .errors import AlreadyExists, Conflict, NotFound
 Obj = Dict[str, Any]
 Handler = Callable[[str, Obj, Optional[Obj]], None]
 
-NAMESPACED = {"Pod", "ConfigMap", "Secret", "ElasticQuota", "Lease", "Event", "DaemonSet", "Deployment"}
+NAMESPACED = {"Pod", "ConfigMap", "Secret", "ElasticQuota", "CompositeElasticQuota", "Lease", "Event", "DaemonSet",
+              "Deployment"}
 
 
 def fast_copy(o: Any) -> Any:

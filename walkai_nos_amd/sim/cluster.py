@@ -171,8 +171,6 @@ class SimScheduler:
                 self.api.bind(ko.name(p), ko.namespace(p), target.name)
             except (Conflict, NotFound):
                 continue
-            target.kubelet.allocate(ko.key(p), reqs)
-            self.api.patch("Pod", ko.name(p), {"status": {"phase": "Running"}}, ko.namespace(p))
             self.bound += 1
             self.on_bind(p, target.name)
         return Result()
@@ -182,7 +180,7 @@ class SimCluster:
     def __init__(self, n_nodes: int = 1, gpus_per_node: int = 8, model: str = "MI355X",
                  kind: str = api.PARTITIONING_KIND_XCP, refresh_interval: float = 10.0,
                  batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None,
-                 scoring: str = "fraction", policy: str = "fifo"):
+                 scoring: str = "fraction", policy: str = "fifo", elastic_quota: bool = False):
         self.clock = clock or SimClock()
         self.api = InMemoryAPIServer(clock=self.clock)
         self.kind = kind
@@ -200,6 +198,14 @@ class SimCluster:
                                           [Watch("Pod", mapper=lambda o: [SimScheduler.KEY]),
                                            Watch("Node", mapper=lambda o: [SimScheduler.KEY])])
         self.api.watch("Pod", self._on_pod_event, replay=False)
+        self.quota_mgr: Optional[Manager] = None
+        self.nos_scheduler = None
+        if elastic_quota:
+            from ..quota.operator import setup_quota_operator
+            from ..quota.scheduler import setup_nos_scheduler
+            self.quota_mgr = Manager(self.api, clock=self.clock)
+            setup_quota_operator(self.quota_mgr)
+            self.nos_scheduler = setup_nos_scheduler(self.quota_mgr, on_bind=self._on_bind)
         for i in range(n_nodes):
             self.add_node(f"node-{i}", gpus_per_node, model, refresh_interval)
 
@@ -254,13 +260,18 @@ class SimCluster:
         self.api.patch("Node", sn.name, {"status": {"allocatable": alloc, "capacity": alloc}})
 
     def _on_bind(self, pod: Dict[str, Any], node: str) -> None:
+        """kubelet side of a binding: allocate devices (preferred allocation) and start the pod."""
+        self.nodes[node].kubelet.allocate(ko.key(pod), res.compute_pod_request(pod))
+        self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Running"}}, ko.namespace(pod))
         self.binds.append((self.clock(), ko.key(pod)[1], node))
 
     # -- workload -----------------------------------------------------------------------
     def submit(self, requests: Dict[str, int], name: Optional[str] = None, namespace: str = "default",
-               labels: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+               labels: Optional[Dict[str, str]] = None, scheduler_name: str = "default-scheduler",
+               priority: int = 0) -> Dict[str, Any]:
         name = name or f"pod-{next(self.pod_seq)}"
-        return self.api.create(ko.new_pod(name, namespace, requests=requests, labels_=labels))
+        return self.api.create(ko.new_pod(name, namespace, requests=requests, labels_=labels,
+                                          scheduler_name=scheduler_name, priority=priority))
 
     def complete(self, name: str, namespace: str = "default", phase: str = "Succeeded") -> None:
         pod = self.api.get("Pod", name, namespace)
@@ -274,7 +285,8 @@ class SimCluster:
 
     # -- driving ------------------------------------------------------------------------
     def managers(self) -> List[Manager]:
-        return [self.scheduler_mgr, self.partitioner_mgr] + [n.manager for n in self.nodes.values()]
+        extra = [self.quota_mgr] if self.quota_mgr is not None else []
+        return [self.scheduler_mgr, self.partitioner_mgr] + extra + [n.manager for n in self.nodes.values()]
 
     def run(self, horizon: float = 30.0) -> float:
         return run_until_idle(self.managers(), self.clock, horizon=horizon)
