@@ -1,0 +1,131 @@
+"""Cluster-info collector/exporter (pkg/clusterinfo/collector_test.go behaviour), telemetry exporter
+(cmd/metricsexporter/metrics/metrics_test.go behaviour) and the nos device plugin over gRPC."""
+import json
+import os
+import tempfile
+
+import grpc
+
+from walkai_nos_amd.device.protos import dp
+from walkai_nos_amd.device.slicing_client import MemorySliceStore
+from walkai_nos_amd.deviceplugin.server import PluginManager, RegistrationServer, SliceDevicePlugin
+from walkai_nos_amd.exporters.clusterinfo import Collector, Exporter, format_profiles, pod_status
+from walkai_nos_amd.exporters.telemetry import Metrics, filter_labels, run
+from walkai_nos_amd.kube import objects as ko
+from walkai_nos_amd.kube.memory import InMemoryAPIServer
+from walkai_nos_amd.models.slicing.cumask import Slice
+
+
+def test_collector_inventory_from_annotations_and_pod_summaries():
+    a = InMemoryAPIServer(clock=lambda: 1700000000.0)
+    a.create(ko.new_node("n1", annotations_={"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "3",
+                                            "nos.nebuly.com/status-gpu-0-cpx_nps1-free": "5",
+                                            "nos.nebuly.com/status-gpu-1-spx_nps1-free": "1"}))
+    p = ko.new_pod("b", "ns2", requests={"amd.com/cpx_nps1": 2}, phase="Running")
+    p["status"]["containerStatuses"] = [{"state": {"waiting": {"reason": "ContainerCreating"}}}]
+    a.create(p)
+    a.create(ko.new_pod("a", "ns1", requests={"amd.com/spx_nps1": 1, "amd.com/cpx_nps1": 1}, phase="Pending"))
+    a.create(ko.new_pod("cpu", "ns1", requests={"cpu": "1"}))
+    snap = Collector(a, clock=lambda: 1700000000.0).collect()
+    assert [(g.gpu, g.allocated, g.available) for g in snap.gpus] == [("cpx_nps1", 3, 5), ("spx_nps1", 0, 1)]
+    assert [(s.namespace, s.name, s.status, s.gpu) for s in snap.pods] == [
+        ("ns1", "a", "Pending", "cpx_nps1, spx_nps1"), ("ns2", "b", "ContainerCreating", "cpx_nps1 x2")]
+    assert snap.ts == "2023-11-14T22:13:20Z"
+    assert snap.utilization["gpu_allocated_percent"] == round(100 * (3 / 8) / 2, 3)
+    doc = json.loads(snap.to_json())
+    assert set(doc) >= {"ts", "gpus", "pods"} and set(doc["pods"][0]) == {"name", "namespace", "status", "gpu",
+                                                                         "start_time", "finish_time"}
+
+
+def test_collector_capacity_fallback_caps_at_capacity():
+    a = InMemoryAPIServer()
+    a.create(ko.new_node("n1", allocatable={"amd.com/cpx_nps1": "8"}))
+    for i in range(10):
+        a.create(ko.new_pod(f"p{i}", requests={"amd.com/cpx_nps1": 1}))
+    snap = Collector(a).collect()
+    assert [(g.gpu, g.allocated, g.available) for g in snap.gpus] == [("cpx_nps1", 8, 0)]
+
+
+def test_pod_status_and_finish_time():
+    p = ko.new_pod("x", phase="Succeeded")
+    p["status"]["containerStatuses"] = [
+        {"state": {"terminated": {"reason": "Completed", "finishedAt": "2024-01-01T00:00:05Z"}}},
+        {"state": {"terminated": {"reason": "Completed", "finishedAt": "2024-01-01T00:00:09Z"}}}]
+    p["spec"]["containers"][0]["resources"] = {"requests": {"amd.com/gpu-32cu.36gb": "1"}}
+    a = InMemoryAPIServer()
+    a.create(p)
+    s = Collector(a).collect().pods[0]
+    assert s.status == "Completed" and s.finish_time == "2024-01-01T00:00:09Z"
+    assert format_profiles({"b": 1, "a": 3}) == "a x3, b"
+    assert pod_status({"status": {}}) == "Unknown"
+
+
+def test_exporter_posts_with_bearer_and_fails_on_error_status():
+    a = InMemoryAPIServer()
+    sent = []
+
+    def post(url, body, headers, timeout):
+        sent.append((url, json.loads(body), headers))
+        return 204 if len(sent) == 1 else 500
+
+    ex = Exporter(Collector(a), "https://api.example/clusters", api_token="tok", post=post)
+    assert ex.send_snapshot() == 204
+    assert sent[0][2]["Authorization"] == "Bearer tok"
+    try:
+        ex.send_snapshot()
+        raise AssertionError("expected failure")
+    except RuntimeError:
+        pass
+
+
+def test_telemetry_never_fails_and_filters_labels():
+    assert run("/nonexistent/metrics.yaml", "http://x") == 0
+    with tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False) as f:
+        f.write("installationUUID: abc\nnodes:\n- name: n1\n  labels: {amd.com/gpu.product-name: MI355X}\n"
+                "components: {nosGpuPartitioner: true}\nchartValues: {x: 1}\n")
+    got = []
+    assert run(f.name, "http://x", post=lambda url, body: got.append(json.loads(body)) or 500) == 0
+    os.unlink(f.name)
+    assert got[0]["installationUUID"] == "abc" and got[0]["components"]["nosGpuPartitioner"] is True
+    assert Metrics.from_yaml("{}").installationUUID == ""
+    assert filter_labels({"amd.com/x": "1", "foo": "2", "node.kubernetes.io/instance-type": "t"}) == {
+        "amd.com/x": "1", "node.kubernetes.io/instance-type": "t"}
+
+
+def test_device_plugin_list_and_watch_allocate_and_register():
+    store = MemorySliceStore()
+    store.save({0: [Slice("g0::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9),
+                    Slice("g0::s1", "32cu.36gb", [4, 5, 6, 7], 36 * 10**9),
+                    Slice("g0::s2", "10gb", [], 10 * 10**9)]})
+    with tempfile.TemporaryDirectory() as d:
+        reg = RegistrationServer(os.path.join(d, "kubelet.sock")).start()
+        mgr = PluginManager(store, {0: "/dev/dri/renderD128"}, socket_dir=d, kubelet_socket=reg.socket)
+        try:
+            mgr.sync()
+            assert sorted(r.resource_name for r in reg.registered) == ["amd.com/gpu-10gb", "amd.com/gpu-32cu.36gb"]
+            plug = mgr.plugins["amd.com/gpu-32cu.36gb"]
+            with grpc.insecure_channel("unix://" + plug.socket) as ch:
+                law = ch.unary_stream(f"/{dp.SERVICE}/ListAndWatch", request_serializer=dp.Empty.SerializeToString,
+                                      response_deserializer=dp.ListAndWatchResponse.FromString)
+                stream = law(dp.Empty(), timeout=5)
+                first = next(stream)
+                assert [x.ID for x in first.devices] == ["g0::s0", "g0::s1"]
+                stream.cancel()
+                alloc = ch.unary_unary(f"/{dp.SERVICE}/Allocate", request_serializer=dp.AllocateRequest.SerializeToString,
+                                       response_deserializer=dp.AllocateResponse.FromString)
+                req = dp.AllocateRequest()
+                req.container_requests.add(devicesIDs=["g0::s1"])
+                resp = alloc(req, timeout=5)
+                envs = dict(resp.container_responses[0].envs)
+                assert envs["HSA_CU_MASK"] == "0:32-63"
+                assert envs["NOS_HBM_LIMIT_BYTES"] == str(36 * 10**9)
+                assert envs["LD_PRELOAD"].endswith("libnos_hbmlimit.so")
+                assert [x.host_path for x in resp.container_responses[0].devices] == ["/dev/kfd", "/dev/dri/renderD128"]
+            shared = SliceDevicePlugin("amd.com/gpu-10gb", store, {}, socket_dir=d)
+            req = dp.AllocateRequest()
+            req.container_requests.add(devicesIDs=["g0::s2"])
+            envs = dict(shared.Allocate(req, None).container_responses[0].envs)
+            assert envs["HSA_CU_MASK"] == "0:64-255"  # shared pool = rows no dedicated slice owns
+        finally:
+            mgr.stop()
+            reg.stop()
