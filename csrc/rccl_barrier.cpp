@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 namespace {
 thread_local std::string g_err;
@@ -89,6 +90,69 @@ int nos_barrier_destroy(void* handle) {
   if (b->comm) rc = nccl_check(ncclCommDestroy(b->comm), "ncclCommDestroy");
   if (b->dbuf) (void)hipFree(b->dbuf);
   if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+  return rc;
+}
+
+// ---- single-process node barrier: one communicator clique over every local device ------------
+// The partition agent is one process per node; ncclCommInitAll gives it one rank per local GPU
+// (logical device after the mode flip), and a grouped all-reduce sums the per-device votes.
+struct NodeBarrier {
+  int n = 0;
+  std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> streams;
+  std::vector<int32_t*> bufs;
+  std::vector<int> devs;
+};
+
+int nos_barrier_init_all(int ndev, const int* devlist, void** handle) {
+  auto* b = new NodeBarrier();
+  b->n = ndev;
+  b->devs.assign(devlist, devlist + ndev);
+  b->comms.resize(ndev);
+  b->streams.resize(ndev);
+  b->bufs.resize(ndev);
+  for (int i = 0; i < ndev; ++i) {
+    if (int rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice")) { delete b; return rc; }
+    if (int rc = hip_check(hipStreamCreateWithFlags(&b->streams[i], hipStreamNonBlocking), "hipStreamCreate")) { delete b; return rc; }
+    if (int rc = hip_check(hipMalloc(&b->bufs[i], sizeof(int32_t)), "hipMalloc")) { delete b; return rc; }
+  }
+  if (int rc = nccl_check(ncclCommInitAll(b->comms.data(), ndev, b->devs.data()), "ncclCommInitAll")) {
+    delete b;
+    return rc;
+  }
+  *handle = b;
+  return 0;
+}
+
+int nos_barrier_allreduce_all(void* handle, const int32_t* votes, int32_t* result) {
+  auto* b = static_cast<NodeBarrier*>(handle);
+  for (int i = 0; i < b->n; ++i) {
+    if (int rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice")) return rc;
+    if (int rc = hip_check(hipMemcpyAsync(b->bufs[i], &votes[i], sizeof(int32_t), hipMemcpyHostToDevice, b->streams[i]), "h2d")) return rc;
+  }
+  if (int rc = nccl_check(ncclGroupStart(), "ncclGroupStart")) return rc;
+  for (int i = 0; i < b->n; ++i) {
+    if (int rc = nccl_check(ncclAllReduce(b->bufs[i], b->bufs[i], 1, ncclInt32, ncclSum, b->comms[i], b->streams[i]), "ncclAllReduce")) return rc;
+  }
+  if (int rc = nccl_check(ncclGroupEnd(), "ncclGroupEnd")) return rc;
+  for (int i = 0; i < b->n; ++i) {
+    if (int rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice")) return rc;
+    if (int rc = hip_check(hipStreamSynchronize(b->streams[i]), "hipStreamSynchronize")) return rc;
+  }
+  if (int rc = hip_check(hipSetDevice(b->devs[0]), "hipSetDevice")) return rc;
+  return hip_check(hipMemcpy(result, b->bufs[0], sizeof(int32_t), hipMemcpyDeviceToHost), "d2h");
+}
+
+int nos_barrier_destroy_all(void* handle) {
+  auto* b = static_cast<NodeBarrier*>(handle);
+  int rc = 0;
+  for (int i = 0; i < b->n; ++i) {
+    if (b->comms[i]) rc |= nccl_check(ncclCommDestroy(b->comms[i]), "ncclCommDestroy");
+    (void)hipSetDevice(b->devs[i]);
+    if (b->bufs[i]) (void)hipFree(b->bufs[i]);
+    if (b->streams[i]) (void)hipStreamDestroy(b->streams[i]);
+  }
   delete b;
   return rc;
 }

@@ -94,3 +94,14 @@ def test_smoke_entry(gpu):
     sys.path.insert(0, ROOT)
     import __graft_entry__ as g
     g.smoke()
+
+
+def test_rccl_node_barrier_all_local_devices(gpu):
+    import torch
+    from walkai_nos_amd.parallel.node_barrier import RcclNodeBarrier
+    b = RcclNodeBarrier(torch.cuda.device_count())
+    try:
+        assert b.vote_all([True] * torch.cuda.device_count()) is True
+        assert b.vote_all([False] + [True] * (torch.cuda.device_count() - 1)) is False
+    finally:
+        b.close()

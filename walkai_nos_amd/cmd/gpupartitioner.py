@@ -1,0 +1,36 @@
+"""gpupartitioner: control-plane partitioner (reference ``cmd/gpupartitioner/gpupartitioner.go:49-132``).
+
+Loads ``GpuPartitionerConfig`` (validated), optionally the known-geometries YAML (validated, then
+installed globally), registers the node initialiser and the pod controllers for both partitioning
+kinds, serves health/metrics and runs with leader election.
+"""
+from __future__ import annotations
+
+import logging
+import sys
+
+from ..api.config import GpuPartitionerConfig, load_config_file
+from ..controllers.partitioner.setup import setup_partitioner
+from ..models.xcp.known_configs import load_known_geometries_file, set_known_geometries
+from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+
+log = logging.getLogger("nos.gpupartitioner")
+
+
+def main(argv=None) -> int:
+    args = base_parser("nos GPU partitioner").parse_args(argv)
+    setup_logging(args.log_level)
+    cfg = load_config_file(args.config, "GpuPartitionerConfig") if args.config else GpuPartitionerConfig()
+    if cfg.knownMigGeometriesFile:
+        set_known_geometries(load_known_geometries_file(cfg.knownMigGeometriesFile))
+        log.info("loaded known geometries from %s", cfg.knownMigGeometriesFile)
+    client = make_client(args.kubeconfig)
+    mgr = make_manager(client, cfg, "gpupartitioner")
+    setup_partitioner(mgr, batch_timeout=cfg.batchWindowTimeoutSeconds, batch_idle=cfg.batchWindowIdleSeconds,
+                      scoring=cfg.scoring, policy=cfg.planningPolicy)
+    serve_endpoints(mgr, cfg)
+    return run_until_signal(mgr)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,59 @@
+"""Partition agent (the mig-agent; reference ``cmd/migagent/migagent.go:56-199``).
+
+Per-node DaemonSet: reads ``NODE_NAME``; builds the kubelet PodResources client (its error is
+fatal here), one amd-smi session and the partition client; at startup checks that the
+node has at least one compute-partition-capable GPU; then runs the reporter and the actuator
+sharing a :class:`SharedState`, with the RCCL node commit barrier over all local GPUs.
+"""
+from __future__ import annotations
+
+import logging
+import sys
+
+from .. import constant
+from ..api.config import MigAgentConfig, load_config_file
+from ..controllers.agent.setup import setup_partition_agent
+from ..device.amdsmi import new_backend
+from ..device.deviceplugin_client import DevicePluginClient
+from ..device.partition_client import PartitionClient
+from ..device.podresources import PodResourcesClient
+from ..utils.util import get_env_or_panic
+from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+
+log = logging.getLogger("nos.partitionagent")
+
+
+def node_barrier_factory(smi):
+    """One RCCL communicator over every local GPU, created per commit (a flip re-enumerates)."""
+    from ..parallel.barrier import LocalBarrier
+    try:
+        from ..parallel.node_barrier import RcclNodeBarrier
+    except ImportError:  # pragma: no cover
+        return lambda n: LocalBarrier(n)
+    return lambda n: RcclNodeBarrier(len(smi.list_gpus()))
+
+
+def main(argv=None) -> int:
+    args = base_parser("nos partition agent").parse_args(argv)
+    setup_logging(args.log_level)
+    cfg = load_config_file(args.config, "MigAgentConfig") if args.config else MigAgentConfig()
+    node = get_env_or_panic(constant.ENV_NODE_NAME)
+    client = make_client(args.kubeconfig)
+    smi = new_backend(cfg.amdSmiBackend)
+    gpus = smi.list_gpus()
+    if not gpus:
+        log.error("no AMD GPU found on node %s", node)
+        return 1
+    resources = PodResourcesClient(cfg.podResourcesSocket)
+    pc = PartitionClient(resources, smi)
+    dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
+    mgr = make_manager(client, cfg, "partitionagent")
+    bf = node_barrier_factory(smi) if cfg.commitBarrier == "rccl" else None
+    setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
+                          refresh_interval=cfg.reportConfigIntervalSeconds)
+    serve_endpoints(mgr, cfg)
+    return run_until_signal(mgr)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

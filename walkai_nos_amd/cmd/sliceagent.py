@@ -1,0 +1,60 @@
+"""CU-mask slice agent (the gpu-agent; reference ``cmd/gpuagent/gpuagent.go:54-152``).
+
+Refuses to run on a GPU that is not in SPX mode (the reference refuses MIG-enabled GPUs): CU
+masks are applied within one logical device.  Runs the slice reporter/actuator and the nos device
+plugin manager for the node's slices.
+"""
+from __future__ import annotations
+
+import logging
+import sys
+import threading
+
+from .. import constant
+from ..api.config import GpuAgentConfig, load_config_file
+from ..controllers.sliceagent.agent import setup_slice_agent
+from ..device.amdsmi import new_backend
+from ..device.podresources import PodResourcesClient
+from ..device.slicing_client import ConfigMapSliceStore, SlicingClient
+from ..deviceplugin.server import PluginManager, render_nodes_from_sysfs, run_forever
+from ..utils.util import get_env_or_panic
+from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+
+log = logging.getLogger("nos.sliceagent")
+
+
+def any_partitioned_gpu(smi) -> bool:
+    return any(smi.get_compute_partition(g.index) != "SPX" for g in smi.list_gpus())
+
+
+def main(argv=None) -> int:
+    args = base_parser("nos CU-mask slice agent").parse_args(argv)
+    setup_logging(args.log_level)
+    cfg = load_config_file(args.config, "GpuAgentConfig") if args.config else GpuAgentConfig()
+    node = get_env_or_panic(constant.ENV_NODE_NAME)
+    client = make_client(args.kubeconfig)
+    smi = new_backend(cfg.amdSmiBackend)
+    if any_partitioned_gpu(smi):
+        log.error("CU-mask slicing needs every GPU in SPX mode; use the partition agent on this node")
+        return 1
+    gpus = smi.list_gpus()
+    store = ConfigMapSliceStore(client, node)
+    sc = SlicingClient(PodResourcesClient(cfg.podResourcesSocket), smi)
+    mgr = make_manager(client, cfg, "sliceagent")
+    plugins = PluginManager(store, render_nodes_from_sysfs(), cu_count=gpus[0].cu_count or 256,
+                            shim_path=cfg.hbmLimitShimPath)
+
+    class Notify:
+        def restart(self, node_name, timeout=60):
+            plugins.sync()
+
+    setup_slice_agent(mgr, node, sc, store, device_plugin=Notify(), refresh_interval=cfg.reportConfigIntervalSeconds,
+                      cu_count=gpus[0].cu_count or 256, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288)
+    stop = threading.Event()
+    threading.Thread(target=run_forever, args=(plugins, 2.0, stop), daemon=True).start()
+    serve_endpoints(mgr, cfg)
+    return run_until_signal(mgr, stop)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -241,6 +241,8 @@ class Controller:
         self.metrics = metrics or REGISTRY
         self._threads: List[threading.Thread] = []
         self._stop = threading.Event()
+        #: workers only process items while this returns True (leader election)
+        self.gate: Optional[Callable[[], bool]] = None
 
     def handler_for(self, w: Watch) -> Callable[[str, Obj, Optional[Obj]], None]:
         def handle(etype: str, obj: Obj, old: Optional[Obj]) -> None:
@@ -288,6 +290,9 @@ class Controller:
 
     def _worker(self) -> None:
         while not self._stop.is_set():
+            if self.gate is not None and not self.gate():
+                self._stop.wait(0.2)
+                continue
             req = self.queue.get(timeout=0.1)
             if req is not None:
                 self.process_one(req)
@@ -403,6 +408,7 @@ class Manager:
         if self.leader_election is not None:
             self.leader_election.start_background()
         for c in self.controllers:
+            c.gate = self.is_leader
             c.start()
         t = threading.Thread(target=self._runnable_loop, name="runnables", daemon=True)
         t.start()
