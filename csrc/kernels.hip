@@ -9,9 +9,9 @@
 //    operand, cdna_hip_programming.md §3), so P never leaves registers. Head-dim -> MFMA K-slot
 //    assignment is dim = 32*half + step, which makes every lane's Q and K fragment one contiguous
 //    128-byte run (8 x dwordx4). K/V of one head (3401 x 64 x 4 B x 2 = 1.7 MB) stays L2-resident
-//    across the query tiles of that head. Optional key split (nsplit > 1) writes per-split
-//    (O, m, l) partials that attn_combine_f32 merges, so a whole-GPU launch has enough waves for
-//    1024 SIMDs while a 32-CU slice runs unsplit.
+//    across the query tiles of that head. The production launch is stream-K (attn_fwd_sk): a
+//    persistent grid sized to the slice's resident-wave capacity splits the (query tile x key
+//    block) work evenly, so a 32-CU CPX slice and the whole 256-CU GPU are both tail-free.
 //  * layernorm_f32: one wave per row, values kept in registers (two-pass mean/variance), wave64
 //    shuffles.
 //  * bias_gelu_f32: in-place exact (erf) GELU(y + b) epilogue, dwordx4 vectorised.
@@ -99,20 +99,18 @@ constexpr int HD = 64;
 
 __device__ __forceinline__ int key_of(int reg, int half) { return (reg & 3) + 8 * (reg >> 2) + 4 * half; }
 
-template <bool SPLIT>
-__global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ qkv, float* __restrict__ out,
-                                                      float* __restrict__ part_o, float* __restrict__ part_ml, int T,
-                                                      int H, float scale_log2e, int keys_per_split, int nsplit) {
-  const int lane = threadIdx.x;
-  const int j = lane & 31;   // query column owned by this lane
-  const int hf = lane >> 5;  // lane half
-  const int qt = blockIdx.x, head = blockIdx.y;
-  const int b = SPLIT ? blockIdx.z / nsplit : blockIdx.z;
-  const int split = SPLIT ? blockIdx.z % nsplit : 0;
-  const int D = H * HD, ld = 3 * D;
-  const float* base = qkv + size_t(b) * T * ld;
-  const int q0 = qt * 32;
+// Online-softmax flash attention over key blocks [kb0, kb1) (32 keys each) for the 32 queries
+// q0..q0+31 of one head. Returns the unnormalised O^T accumulators and the running (m, l).
+struct AttnAcc {
+  f32x16 o0, o1;
+  float m, l;
+};
 
+__device__ __forceinline__ AttnAcc attn_segment(const float* __restrict__ base, int q0, int head, int kb0, int kb1,
+                                                int T, int D, float scale_log2e) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, hf = lane >> 5;
+  const int ld = 3 * D;
   // Q^T fragment: Q[q0 + j][32*hf + s], s = 0..31, pre-scaled into the log2 domain
   float qreg[32];
   {
@@ -127,16 +125,16 @@ __global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ 
       qreg[4 * s4 + 3] = v.w * scale_log2e;
     }
   }
-
-  const int k_begin = split * keys_per_split;
-  const int k_end = min(T, k_begin + keys_per_split);
-
-  f32x16 o0 = {0}, o1 = {0};
-  float m = -INFINITY, l = 0.f;
+  AttnAcc a;
+  a.o0 = f32x16{0};
+  a.o1 = f32x16{0};
+  a.m = -INFINITY;
+  a.l = 0.f;
   const float* kbase = base + D + head * HD + 32 * hf;
   const float* vbase = base + 2 * D + head * HD + j;
 
-  for (int kb = k_begin; kb < k_end; kb += 32) {
+  for (int blk = kb0; blk < kb1; ++blk) {
+    const int kb = blk * 32;
     // K fragment: K[kb + j][32*hf + s]
     float kreg[32];
     {
@@ -164,17 +162,17 @@ __global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ 
 #pragma unroll
     for (int st = 0; st < 32; ++st) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[st], qreg[st], s, 0, 0, 0);
 
-    if (kb + 32 > k_end) {
+    if (kb + 32 > T) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        if (kb + key_of(r, hf) >= k_end) s[r] = -INFINITY;
+        if (kb + key_of(r, hf) >= T) s[r] = -INFINITY;
     }
     float mx = s[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+    const float m_new = fmaxf(a.m, mx);
+    const float alpha = __builtin_amdgcn_exp2f(a.m - m_new);
     float psum = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -182,75 +180,148 @@ __global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ 
       psum += s[r];
     }
     psum += __shfl_xor(psum, 32, 64);
-    l = l * alpha + psum;
-    m = m_new;
+    a.l = a.l * alpha + psum;
+    a.m = m_new;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      o0[r] *= alpha;
-      o1[r] *= alpha;
+      a.o0[r] *= alpha;
+      a.o1[r] *= alpha;
     }
     // O^T[d][query] += sum_key V^T[d][key] P^T[key][query]; P^T register t is key key_of(t, hf)
 #pragma unroll
     for (int t = 0; t < 16; ++t) {
-      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0[t], s[t], o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1[t], s[t], o1, 0, 0, 0);
+      a.o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0[t], s[t], a.o0, 0, 0, 0);
+      a.o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1[t], s[t], a.o1, 0, 0, 0);
     }
   }
+  return a;
+}
 
+__device__ __forceinline__ void attn_store_out(const AttnAcc& a, float* __restrict__ out, int b, int q0, int head,
+                                               int T, int D) {
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, hf = lane >> 5;
   const int q = q0 + j;
   if (q >= T) return;
-  if (!SPLIT) {
-    const float inv = 1.f / l;
-    float* orow = out + (size_t(b) * T + q) * D + head * HD;
+  const float inv = 1.f / a.l;
+  float* orow = out + (size_t(b) * T + q) * D + head * HD;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = key_of(r, hf);
-      orow[d] = o0[r] * inv;
-      orow[32 + d] = o1[r] * inv;
-    }
-  } else {
-    // partials: part_o[split][b][head][q][64] (unnormalised), part_ml[split][b][head][q][2] = (m, l)
-    const size_t idx = ((size_t(blockIdx.z) * H + head) * T + q);
-    float* po = part_o + idx * HD;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = key_of(r, hf);
-      po[d] = o0[r];
-      po[32 + d] = o1[r];
-    }
-    if (hf == 0) {
-      part_ml[idx * 2 + 0] = m;
-      part_ml[idx * 2 + 1] = l;
-    }
+  for (int r = 0; r < 16; ++r) {
+    const int d = key_of(r, hf);
+    orow[d] = a.o0[r] * inv;
+    orow[32 + d] = a.o1[r] * inv;
   }
 }
 
-// merge nsplit partials: one thread per (b, head, q, d)
-__global__ __launch_bounds__(256) void attn_combine_f32(const float* __restrict__ part_o,
-                                                        const float* __restrict__ part_ml, float* __restrict__ out,
-                                                        int B, int T, int H, int nsplit) {
-  const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
-  const size_t total = size_t(B) * H * T * HD;
-  if (i >= total) return;
-  const int d = int(i % HD);
-  size_t r = i / HD;
-  const int q = int(r % T);
-  r /= T;
-  const int head = int(r % H);
-  const int b = int(r / H);
-  float mmax = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) {
-    const size_t idx = ((size_t(b * nsplit + s) * H + head) * T + q);
-    mmax = fmaxf(mmax, part_ml[idx * 2]);
+// One wave per (query tile, head, batch): the whole key range, normalised output. Used when no
+// workspace is available (nos_attention_f32).
+__global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ qkv, float* __restrict__ out, int T,
+                                                      int H, float scale_log2e) {
+  const int qt = blockIdx.x, head = blockIdx.y, b = blockIdx.z;
+  const int D = H * HD;
+  const AttnAcc a = attn_segment(qkv + size_t(b) * T * 3 * D, qt * 32, head, 0, (T + 31) / 32, T, D, scale_log2e);
+  attn_store_out(a, out, b, qt * 32, head, T, D);
+}
+
+// ---- stream-K attention ----------------------------------------------------------------------
+// The work is U = B*H*QT*NK units (one 32-query x 32-key block each, QT = NK = ceil(T/32)), laid out
+// tile-major so consecutive units share a head's K/V. A persistent grid of exactly P waves (slice
+// CUs x resident waves per CU) gives wave w the contiguous range [w*U/P, (w+1)*U/P): every SIMD of
+// the slice gets the same number of MFMAs, so there is no wave-quantisation tail whatever the slice
+// size (a fixed split count leaves 1.25 or 2.5 "rounds" for 256 or 32 CUs). Segments covering a
+// whole tile are normalised and stored directly; a wave's first and last segments may be partial
+// and go to its two workspace slots, merged by attn_sk_fixup (a second launch on the same stream,
+// so no inter-wave spin-waits exist). Logical wave ids are XCD-major: hardware round-robins
+// workgroups over the 8 XCDs, so remapping keeps each XCD on a contiguous run of units and its
+// 4 MB L2 holds at most two heads' K/V (1.7 MB each at T=3401) instead of all of them.
+__device__ __forceinline__ long long sk_begin(long long w, long long U, long long P) { return w * U / P; }
+
+__device__ __forceinline__ int sk_logical(int phys, int P) {
+  return (P % 8 == 0) ? (phys % 8) * (P / 8) + phys / 8 : phys;
+}
+
+template <int WPE>
+__global__ __launch_bounds__(64, WPE) void attn_fwd_sk(const float* __restrict__ qkv, float* __restrict__ out,
+                                                     float* __restrict__ part_o, float* __restrict__ part_ml, int B,
+                                                     int T, int H, float scale_log2e, int P) {
+  const int w = sk_logical(blockIdx.x, P);
+  const int NK = (T + 31) / 32, QT = NK;
+  const long long U = (long long)B * H * QT * NK;
+  long long u = sk_begin(w, U, P);
+  const long long u1 = sk_begin(w + 1, U, P);
+  const int D = H * HD;
+  const int lane = threadIdx.x & 63;
+  const int j = lane & 31, hf = lane >> 5;
+  bool first = true;
+  while (u < u1) {
+    const long long tile = u / NK;
+    const int kb0 = int(u - tile * NK);
+    const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
+    const int qt = int(tile % QT);
+    const int head = int((tile / QT) % H);
+    const int b = int(tile / ((long long)QT * H));
+    const AttnAcc a = attn_segment(qkv + size_t(b) * T * 3 * D, qt * 32, head, kb0, kb1, T, D, scale_log2e);
+    if (kb0 == 0 && kb1 == NK) {
+      attn_store_out(a, out, b, qt * 32, head, T, D);
+    } else {
+      // slot layout: part_o[slot][d][32 queries] (lane-contiguous stores), part_ml[slot][2][32]
+      const size_t slot = size_t(w) * 2 + (first ? 0 : 1);
+      float* po = part_o + slot * (HD * 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = key_of(r, hf);
+        po[d * 32 + j] = a.o0[r];
+        po[(32 + d) * 32 + j] = a.o1[r];
+      }
+      if (hf == 0) {
+        part_ml[slot * 64 + j] = a.m;
+        part_ml[slot * 64 + 32 + j] = a.l;
+      }
+    }
+    u += kb1 - kb0;
+    first = false;
   }
-  float num = 0.f, den = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
-    const size_t idx = ((size_t(b * nsplit + s) * H + head) * T + q);
-    const float sc = __builtin_amdgcn_exp2f(part_ml[idx * 2] - mmax);
-    num += part_o[idx * HD + d] * sc;
-    den += part_ml[idx * 2 + 1] * sc;
+}
+
+// Merge the partial segments of every tile that more than one wave touched. One 256-thread block
+// per tile: thread = (query quad, d); contributors are the waves whose ranges intersect the tile.
+__global__ __launch_bounds__(256) void attn_sk_fixup(const float* __restrict__ part_o,
+                                                     const float* __restrict__ part_ml, float* __restrict__ out,
+                                                     int B, int T, int H, int P) {
+  const int NK = (T + 31) / 32, QT = NK;
+  const long long U = (long long)B * H * QT * NK;
+  const long long tile = blockIdx.x;
+  const long long t0 = tile * NK, t1 = t0 + NK;  // unit range of this tile
+  // wave containing unit u: largest w with w*U/P <= u
+  const long long w_lo = ((t0 + 1) * P + U - 1) / U - 1;
+  const long long w_hi = (t1 * P + U - 1) / U - 1;
+  if (w_lo == w_hi) return;  // one wave did the whole tile and stored it normalised
+  const int qt = int(tile % QT);
+  const int head = int((tile / QT) % H);
+  const int b = int(tile / ((long long)QT * H));
+  const int D = H * HD;
+  const int d = threadIdx.x & 63;
+  for (int jq = threadIdx.x >> 6; jq < 32; jq += 4) {
+    const int q = qt * 32 + jq;
+    if (q >= T) break;
+    float mmax = -INFINITY;
+    for (long long w = w_lo; w <= w_hi; ++w) {
+      const long long s = w * U / P;
+      if (s == (w + 1) * U / P) continue;
+      const size_t slot = size_t(w) * 2 + (s >= t0 ? 0 : 1);
+      mmax = fmaxf(mmax, part_ml[slot * 64 + jq]);
+    }
+    float num = 0.f, den = 0.f;
+    for (long long w = w_lo; w <= w_hi; ++w) {
+      const long long s = w * U / P;
+      if (s == (w + 1) * U / P) continue;
+      const size_t slot = size_t(w) * 2 + (s >= t0 ? 0 : 1);
+      const float sc = __builtin_amdgcn_exp2f(part_ml[slot * 64 + jq] - mmax);
+      num += part_o[slot * (HD * 32) + d * 32 + jq] * sc;
+      den += part_ml[slot * 64 + 32 + jq] * sc;
+    }
+    out[(size_t(b) * T + q) * D + head * HD + d] = num / den;
   }
-  out[(size_t(b) * T + q) * (H * HD) + head * HD + d] = num / den;
 }
 
 }  // namespace
@@ -287,55 +358,65 @@ int nos_bias_gelu_f32(float* y, const float* b, int rows, int N, void* stream) {
   return check_launch("bias_gelu_f32");
 }
 
-// keys per split (rounded to the 32-key block) and the effective split count
-static void split_plan(int T, int nsplit, int* kps, int* ns) {
-  *kps = ((T + nsplit - 1) / nsplit + 31) / 32 * 32;
-  *ns = (T + *kps - 1) / *kps;
+// Resident attention waves per CU (occupancy of attn_fwd_sk); the persistent grid is this times
+// the slice's CU count.
+// Variant: 2 or 3 resident waves per SIMD (register budget 256 or 168 VGPRs).
+static int g_wpe = 3;
+
+int nos_attention_set_variant(int wpe) {
+  if (wpe != 2 && wpe != 3) return -1;
+  g_wpe = wpe;
+  return 0;
 }
 
-// bytes of caller-provided workspace for a split launch (0 when nsplit <= 1). The workspace comes
+int nos_attention_waves_per_cu() {
+  int n = 0;
+  const hipError_t e = g_wpe == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<3>, 64, 0)
+                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<2>, 64, 0);
+  if (e != hipSuccess || n <= 0) n = 4 * g_wpe;
+  return n;
+}
+
+// bytes of caller-provided workspace for a stream-K launch of `waves` waves. The workspace comes
 // from the caller's stream-ordered allocator, so concurrent slices never share scratch and a launch
 // inside graph capture never allocates.
-size_t nos_attention_ws_bytes(int B, int T, int H, int nsplit) {
-  if (nsplit <= 1) return 0;
-  int kps, ns;
-  split_plan(T, nsplit, &kps, &ns);
-  return size_t(ns) * B * H * T * (HD + 2) * sizeof(float);
-}
+size_t nos_attention_ws_bytes(int waves) { return size_t(waves) * 2 * (HD * 32 + 64) * sizeof(float); }
 
-int nos_attention_f32_split(const float* qkv, float* out, float* ws, int B, int T, int H, int head_dim, float scale,
-                            int nsplit, void* stream) {
+int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, int H, int head_dim, float scale,
+                         int waves, void* stream) {
   if (head_dim != HD) {
     g_err = "attention: head_dim must be 64";
     return -1;
   }
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const float scale_log2e = scale * 1.4426950408889634f;
-  const int qtiles = (T + 31) / 32;
-  if (nsplit <= 1) {
-    hipLaunchKernelGGL(attn_fwd_f32<false>, dim3(qtiles, H, B), dim3(64), 0, s, qkv, out, nullptr, nullptr, T, H,
-                       scale_log2e, T, 1);
-    return check_launch("attn_fwd_f32");
-  }
-  int kps;
-  split_plan(T, nsplit, &kps, &nsplit);
-  if (ws == nullptr) {
-    g_err = "attention: split launch needs a workspace (nos_attention_ws_bytes)";
+  if (ws == nullptr || waves <= 0) {
+    g_err = "attention: stream-K launch needs waves > 0 and a workspace (nos_attention_ws_bytes)";
     return -1;
   }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const float scale_log2e = scale * 1.4426950408889634f;
+  const int NK = (T + 31) / 32;
   float* part_o = ws;
-  float* part_ml = ws + size_t(nsplit) * B * H * T * HD;
-  hipLaunchKernelGGL(attn_fwd_f32<true>, dim3(qtiles, H, B * nsplit), dim3(64), 0, s, qkv, out, part_o, part_ml, T, H,
-                     scale_log2e, kps, nsplit);
-  if (int rc = check_launch("attn_fwd_f32<split>")) return rc;
-  const size_t total = size_t(B) * H * T * HD;
-  hipLaunchKernelGGL(attn_combine_f32, dim3((total + 255) / 256), dim3(256), 0, s, part_o, part_ml, out, B, T, H,
-                     nsplit);
-  return check_launch("attn_combine_f32");
+  float* part_ml = ws + size_t(waves) * 2 * HD * 32;
+  if (g_wpe == 3)
+    hipLaunchKernelGGL(attn_fwd_sk<3>, dim3(waves), dim3(64), 0, s, qkv, out, part_o, part_ml, B, T, H, scale_log2e,
+                       waves);
+  else
+    hipLaunchKernelGGL(attn_fwd_sk<2>, dim3(waves), dim3(64), 0, s, qkv, out, part_o, part_ml, B, T, H, scale_log2e,
+                       waves);
+  if (int rc = check_launch("attn_fwd_sk")) return rc;
+  hipLaunchKernelGGL(attn_sk_fixup, dim3(B * H * NK), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves);
+  return check_launch("attn_sk_fixup");
 }
 
 int nos_attention_f32(const float* qkv, float* out, int B, int T, int H, int head_dim, float scale, void* stream) {
-  return nos_attention_f32_split(qkv, out, nullptr, B, T, H, head_dim, scale, 1, stream);
+  if (head_dim != HD) {
+    g_err = "attention: head_dim must be 64";
+    return -1;
+  }
+  const int qtiles = (T + 31) / 32;
+  hipLaunchKernelGGL(attn_fwd_f32, dim3(qtiles, H, B), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), qkv, out,
+                     T, H, scale * 1.4426950408889634f);
+  return check_launch("attn_fwd_f32");
 }
 
 }  // extern "C"

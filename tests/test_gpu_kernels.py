@@ -49,20 +49,25 @@ def test_attention_asymmetric_values_catch_transposes(K):
     assert (out - ref).abs().max().item() < 1e-4
 
 
-def test_attention_split_matches_unsplit(K):
+@pytest.mark.parametrize("T,H,B", [(1000, 2, 1), (3401, 6, 1), (77, 1, 2)])
+def test_attention_stream_k_any_grid_matches_reference(K, T, H, B):
+    # every grid size exercises a different partial-segment pattern: a wave inside one tile,
+    # waves spanning tile boundaries, more waves than units, one wave doing everything
     torch.manual_seed(1)
-    B, T, H = 1, 1000, 2
     qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
     ref = _ref_attention(qkv, H, 64, 0.125)
-    for ns in (1, 2, 3, 7):
-        out = torch.empty(B, T, H * 64, device="cuda")
-        K.attention_split(qkv, out, H, 64, 0.125, ns)
+    units = B * H * ((T + 31) // 32) ** 2
+    for waves in (1, 3, 7, 64, 333, 1024, 3072, units + 5):
+        out = torch.full((B, T, H * 64), float("nan"), device="cuda")
+        K.attention_sk(qkv, out, H, 64, 0.125, waves)
         torch.cuda.synchronize()
-        assert (out - ref).abs().max().item() < 2e-5
+        assert (out - ref).abs().max().item() < 2e-5, waves
+    un = K.attention_unsplit(qkv, H, 64, 0.125)
+    assert (un - ref).abs().max().item() < 2e-5
 
 
-def test_attention_concurrent_streams_with_splits(K):
-    # two slices running split launches at once must not share scratch
+def test_attention_concurrent_streams_stream_k(K):
+    # two slices running stream-K launches at once must not share scratch
     torch.manual_seed(2)
     qa = torch.randn(1, 700, 3 * 2 * 64, device="cuda")
     qb = torch.randn(1, 900, 3 * 2 * 64, device="cuda")
@@ -71,9 +76,9 @@ def test_attention_concurrent_streams_with_splits(K):
     torch.cuda.synchronize()
     for _ in range(3):
         with torch.cuda.stream(sa):
-            oa = K.attention_split(qa, torch.empty(1, 700, 128, device="cuda"), 2, 64, 0.125, 3)
+            oa = K.attention_sk(qa, torch.empty(1, 700, 128, device="cuda"), 2, 64, 0.125, 300)
         with torch.cuda.stream(sb):
-            ob = K.attention_split(qb, torch.empty(1, 900, 128, device="cuda"), 2, 64, 0.125, 4)
+            ob = K.attention_sk(qb, torch.empty(1, 900, 128, device="cuda"), 2, 64, 0.125, 512)
         outs.append((oa, ob))
     torch.cuda.synchronize()
     ra, rb = _ref_attention(qa, 2, 64, 0.125), _ref_attention(qb, 2, 64, 0.125)

@@ -1,0 +1,96 @@
+"""Per-slice kernel microbenchmark on the GPU box: the YOLOS-small layer's hot ops timed on
+CU-masked streams of 256/128/64/32 CUs (SPX/DPX/QPX/CPX-sized slices), one slice at a time.
+
+    python tools/kbench.py [--iters N] [--out gpurun_out/kbench.json]
+
+Reports microseconds per call and achieved TFLOP/s for: attention (unsplit one-wave-per-tile
+baseline, stream-K with 2 and 3 resident waves/SIMD, PyTorch SDPA), and the four fp32 GEMMs of a
+layer (hipBLASLt via torch).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from walkai_nos_amd.bench_core import slice_cus  # noqa: E402
+from walkai_nos_amd.ops import kernels as K  # noqa: E402
+from walkai_nos_amd.ops.probe import Stream  # noqa: E402
+
+T, H, HD, D, FF = 3401, 6, 64, 384, 1536
+
+
+def timeit(fn, stream, iters):
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            fn()
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record(stream)
+        for _ in range(iters):
+            fn()
+        en.record(stream)
+    en.synchronize()
+    return st.elapsed_time(en) * 1000.0 / iters
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--out", default="gpurun_out/kbench.json")
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    qkv = torch.randn(1, T, 3 * D, device="cuda")
+    out = torch.empty(1, T, D, device="cuda")
+    x = torch.randn(T, D, device="cuda")
+    h = torch.randn(T, FF, device="cuda")
+    w_qkv, w_o = torch.randn(3 * D, D, device="cuda"), torch.randn(D, D, device="cuda")
+    w_1, w_2 = torch.randn(FF, D, device="cuda"), torch.randn(D, FF, device="cuda")
+    b_ff = torch.randn(FF, device="cuda")
+    attn_flops = 4.0 * T * T * HD * H
+    q, k, v = qkv.view(1, T, 3, H, HD).permute(2, 0, 3, 1, 4)
+    results = []
+    for prof, part, label in (("spx_nps1", 0, "spx"), ("dpx_nps1", 0, "dpx"), ("qpx_nps1", 0, "qpx"),
+                              ("cpx_nps1", 0, "cpx")):
+        cus = slice_cus(prof, part)
+        n = 256 if cus is None else len(cus)
+        with Stream(0, cus) as hs:
+            s = hs.torch_stream()
+            r = {"slice": label, "cus": n}
+            K.set_slice_cus(n)
+            r["attn_unsplit_us"] = timeit(lambda: K.attention_unsplit(qkv, H, HD, 0.125), s, a.iters)
+            for wpe in (2, 3):
+                K.set_attention_variant(wpe)
+                wv = K.attention_waves(n)
+                r[f"attn_sk{wpe}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, a.iters)
+                r[f"attn_sk{wpe}_waves"] = wv
+            r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, a.iters)
+            for kname in ("attn_unsplit_us", "attn_sk2_us", "attn_sk3_us", "attn_sdpa_us"):
+                r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
+            gemms = {"qkv": (lambda: torch.matmul(x, w_qkv.t()), 2.0 * T * D * 3 * D),
+                     "proj": (lambda: torch.matmul(x, w_o.t()), 2.0 * T * D * D),
+                     "fc1": (lambda: K.linear_gelu(x, w_1, b_ff), 2.0 * T * D * FF),
+                     "fc2": (lambda: torch.matmul(h, w_2.t()), 2.0 * T * FF * D)}
+            for gname, (fn, fl) in gemms.items():
+                us = timeit(fn, s, a.iters)
+                r[f"gemm_{gname}_us"] = round(us, 1)
+                r[f"gemm_{gname}_tflops"] = round(fl / us / 1e6, 2)
+            r["layernorm_us"] = round(timeit(lambda: K.layernorm(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
+            for kname in list(r):
+                if isinstance(r[kname], float):
+                    r[kname] = round(r[kname], 2)
+            print(json.dumps(r), flush=True)
+            results.append(r)
+    K.set_attention_variant(3)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(results, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

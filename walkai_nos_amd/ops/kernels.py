@@ -13,8 +13,9 @@ Kernels (``csrc/kernels.hip``):
 * ``linear_residual``  — hipBLASLt GEMM with the residual folded in as the GEMM's C input
   (``torch.addmm`` beta=1), no extra pass;
 * ``attention_qkv``    — flash attention over the packed ``[B, T, 3*D]`` QKV tensor on
-  ``v_mfma_f32_32x32x2_f32`` (exact fp32 MFMA), online softmax, one workgroup per
-  (batch*head, 64-query tile); writes ``[B, T, D]`` directly so no transpose pass is needed.
+  ``v_mfma_f32_32x32x2_f32`` (exact fp32 MFMA), online softmax, stream-K decomposition over
+  (32-query tile x 32-key block) units with a persistent grid sized to the slice's CUs; writes
+  ``[B, T, D]`` directly so no transpose pass is needed.
 """
 from __future__ import annotations
 
@@ -47,14 +48,22 @@ def slice_cus() -> int:
     return getattr(_slice, "cus", None) or 256
 
 
-def attention_splits(B: int, T: int, H: int, cus: int) -> int:
-    """Key splits so that a launch has >= 2 waves per SIMD of the slice (4 SIMDs per CU)."""
-    waves = B * H * ((T + 31) // 32)
-    target = 2 * 4 * cus
-    ns = 1
-    while waves * ns < target and ns < 8 and T // (32 * (ns + 1)) >= 4:
-        ns += 1
-    return ns
+_waves_per_cu: Optional[int] = None
+
+
+def set_attention_variant(waves_per_simd: int) -> None:
+    """Register budget of the stream-K kernel: 3 resident waves/SIMD (168 VGPRs) or 2 (256)."""
+    global _waves_per_cu
+    _check(_L().nos_attention_set_variant(waves_per_simd))
+    _waves_per_cu = None
+
+
+def attention_waves(cus: int) -> int:
+    """Persistent stream-K grid for a slice of ``cus`` CUs: every resident wave slot, once."""
+    global _waves_per_cu
+    if _waves_per_cu is None:
+        _waves_per_cu = int(_L().nos_attention_waves_per_cu())
+    return _waves_per_cu * cus
 
 
 def set_backend(name: str) -> None:
@@ -81,8 +90,8 @@ def _L() -> ctypes.CDLL:
             L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, i32, i32, f32, vp]
             L.nos_bias_gelu_f32.argtypes = [vp, vp, i32, i32, vp]
             L.nos_attention_f32.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
-            L.nos_attention_f32_split.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
-            L.nos_attention_ws_bytes.argtypes = [i32, i32, i32, i32]
+            L.nos_attention_f32_sk.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_ws_bytes.argtypes = [i32]
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             _lib = L
@@ -156,17 +165,26 @@ def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) ->
     qkv = qkv.contiguous()
     B, T, _ = qkv.shape
     out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
-    ns = attention_splits(B, T, heads, slice_cus())
-    return attention_split(qkv, out, heads, head_dim, scale, ns)
+    return attention_sk(qkv, out, heads, head_dim, scale, attention_waves(slice_cus()))
 
 
-def attention_split(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float, ns: int) -> torch.Tensor:
+def attention_sk(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float,
+                 waves: int) -> torch.Tensor:
+    """Stream-K launch with an explicit persistent grid of ``waves`` waves; the partial-segment
+    workspace comes from the caller's stream-ordered allocator."""
     B, T, _ = qkv.shape
     L = _L()
-    nbytes = L.nos_attention_ws_bytes(B, T, heads, ns)
-    ws = torch.empty(max(1, nbytes // 4), dtype=torch.float32, device=qkv.device) if nbytes else None
-    _check(L.nos_attention_f32_split(qkv.data_ptr(), out.data_ptr(), ws.data_ptr() if ws is not None else None,
-                                     B, T, heads, head_dim, scale, ns, _stream()))
+    ws = torch.empty(L.nos_attention_ws_bytes(waves) // 4, dtype=torch.float32, device=qkv.device)
+    _check(L.nos_attention_f32_sk(qkv.data_ptr(), out.data_ptr(), ws.data_ptr(), B, T, heads, head_dim, scale,
+                                  waves, _stream()))
+    return out
+
+
+def attention_unsplit(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
+    """One wave per (query tile, head): no workspace, normalised in-kernel (A/B reference)."""
+    B, T, _ = qkv.shape
+    out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
+    _check(_L().nos_attention_f32(qkv.data_ptr(), out.data_ptr(), B, T, heads, head_dim, scale, _stream()))
     return out
 
 
