@@ -324,6 +324,222 @@ __global__ __launch_bounds__(256) void attn_sk_fixup(const float* __restrict__ p
   }
 }
 
+
+// ---- stream-K attention, LDS-shared K/V (production path) --------------------------------------
+// A 256-thread workgroup = 4 waves = 4 consecutive 32-query tiles (a 128-query "group") of one
+// head. The workgroup streams 32-key blocks of K and V through LDS once for all four waves
+// (coalesced dwordx4 global loads, register-prefetched one block ahead, double-buffered, one
+// barrier per block), so L2->CU traffic and texture-address work drop 4x versus every wave
+// fetching its own fragments (the v1 kernel above is TA-bound at ~640 cache-line lookups per wave
+// per block). LDS images: K row-major with a 68-float stride — the per-lane ds_read_b128 of
+// K[key=j][32*hf + 4*s4] then hits 16 distinct 16-B slots per lane group (17*j mod 16); V
+// row-major (stride 64), read as ds_read_b32 V[key][j] with 32 consecutive banks per half-wave.
+// Stream-K runs over (group x key block) units with a persistent grid of P workgroups, the same
+// first/last-segment workspace scheme and XCD-major order as attn_fwd_sk.
+constexpr int KSTR = 68, VSTR = 64;
+constexpr int KBUF = 32 * KSTR, VBUF = 32 * VSTR;
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restrict__ qkv, float* __restrict__ out,
+                                                          float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                          int B, int T, int H, float scale_log2e, int P) {
+  __shared__ __attribute__((aligned(16))) float lds_k[2 * KBUF];
+  __shared__ __attribute__((aligned(16))) float lds_v[2 * VBUF];
+  const int w = sk_logical(blockIdx.x, P);
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const long long U = (long long)B * H * QG * NK;
+  long long u = sk_begin(w, U, P);
+  const long long u1 = sk_begin(w + 1, U, P);
+  const int D = H * HD, ld = 3 * D;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int j = lane & 31, hf = lane >> 5;
+  // cooperative-load mapping: float4 f = tid + 256*i, i = 0..1 -> key row f/16, dims 4*(f%16)
+  const int lrow = tid >> 4, lc4 = tid & 15;
+  bool first = true;
+  while (u < u1) {
+    const long long grp = u / NK;
+    const int kb0 = int(u - grp * NK);
+    const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
+    const int qg = int(grp % QG);
+    const int head = int((grp / QG) % H);
+    const int b = int(grp / ((long long)QG * H));
+    const float* base = qkv + size_t(b) * T * ld;
+    const int qt = qg * 4 + wv;
+    const bool active = qt < QT;
+    const int q0 = qt * 32;
+
+    float qreg[32];
+    {
+      const int qrow = min(q0 + j, T - 1);
+      const float4* qp = reinterpret_cast<const float4*>(base + size_t(qrow) * ld + head * HD + 32 * hf);
+#pragma unroll
+      for (int s4 = 0; s4 < 8; ++s4) {
+        const float4 v = qp[s4];
+        qreg[4 * s4 + 0] = v.x * scale_log2e;
+        qreg[4 * s4 + 1] = v.y * scale_log2e;
+        qreg[4 * s4 + 2] = v.z * scale_log2e;
+        qreg[4 * s4 + 3] = v.w * scale_log2e;
+      }
+    }
+    const float* kg = base + D + head * HD + 4 * lc4;
+    const float* vg = base + 2 * D + head * HD + 4 * lc4;
+    float4 pk0, pk1, pv0, pv1;
+    auto fetch = [&](int blk) {
+      const int r0 = min(blk * 32 + lrow, T - 1), r1 = min(blk * 32 + 16 + lrow, T - 1);
+      pk0 = *reinterpret_cast<const float4*>(kg + size_t(r0) * ld);
+      pk1 = *reinterpret_cast<const float4*>(kg + size_t(r1) * ld);
+      pv0 = *reinterpret_cast<const float4*>(vg + size_t(r0) * ld);
+      pv1 = *reinterpret_cast<const float4*>(vg + size_t(r1) * ld);
+    };
+    auto stash = [&](int buf) {
+      *reinterpret_cast<float4*>(&lds_k[buf * KBUF + lrow * KSTR + 4 * lc4]) = pk0;
+      *reinterpret_cast<float4*>(&lds_k[buf * KBUF + (16 + lrow) * KSTR + 4 * lc4]) = pk1;
+      *reinterpret_cast<float4*>(&lds_v[buf * VBUF + lrow * VSTR + 4 * lc4]) = pv0;
+      *reinterpret_cast<float4*>(&lds_v[buf * VBUF + (16 + lrow) * VSTR + 4 * lc4]) = pv1;
+    };
+    __syncthreads();  // the previous segment's last block is no longer being read
+    fetch(kb0);
+    stash(0);
+    __syncthreads();
+
+    f32x16 o0 = {0}, o1 = {0};
+    float m = -INFINITY, l = 0.f;
+    for (int blk = kb0; blk < kb1; ++blk) {
+      const int buf = (blk - kb0) & 1;
+      const bool more = blk + 1 < kb1;
+      if (more) fetch(blk + 1);
+      if (active) {
+        const float* ks = &lds_k[buf * KBUF + j * KSTR + 32 * hf];
+        float kreg[32];
+#pragma unroll
+        for (int s4 = 0; s4 < 8; ++s4) {
+          const float4 v = *reinterpret_cast<const float4*>(ks + 4 * s4);
+          kreg[4 * s4 + 0] = v.x;
+          kreg[4 * s4 + 1] = v.y;
+          kreg[4 * s4 + 2] = v.z;
+          kreg[4 * s4 + 3] = v.w;
+        }
+        const float* vs = &lds_v[buf * VBUF + j];
+        float v0[16], v1[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          v0[t] = vs[key_of(t, hf) * VSTR];
+          v1[t] = vs[key_of(t, hf) * VSTR + 32];
+        }
+        f32x16 sacc = {0};
+#pragma unroll
+        for (int st = 0; st < 32; ++st) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(kreg[st], qreg[st], sacc, 0, 0, 0);
+        const int kb = blk * 32;
+        if (kb + 32 > T) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb + key_of(r, hf) >= T) sacc[r] = -INFINITY;
+        }
+        float mx = sacc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - m_new);
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sacc[r] = __builtin_amdgcn_exp2f(sacc[r] - m_new);
+          psum += sacc[r];
+        }
+        psum += __shfl_xor(psum, 32, 64);
+        l = l * alpha + psum;
+        m = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o0[r] *= alpha;
+          o1[r] *= alpha;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v0[t], sacc[t], o0, 0, 0, 0);
+          o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v1[t], sacc[t], o1, 0, 0, 0);
+        }
+      }
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+    }
+
+    if (active) {
+      if (kb0 == 0 && kb1 == NK) {
+        const int q = q0 + j;
+        if (q < T) {
+          const float inv = 1.f / l;
+          float* orow = out + (size_t(b) * T + q) * D + head * HD;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int d = key_of(r, hf);
+            orow[d] = o0[r] * inv;
+            orow[32 + d] = o1[r] * inv;
+          }
+        }
+      } else {
+        // slot layout: part_o[wg][first?0:1][wave][d][32 queries], part_ml[wg][slot][wave][2][32]
+        const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * 4 + wv;
+        float* po = part_o + slot * (HD * 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = key_of(r, hf);
+          po[d * 32 + j] = o0[r];
+          po[(32 + d) * 32 + j] = o1[r];
+        }
+        if (hf == 0) {
+          part_ml[slot * 64 + j] = m;
+          part_ml[slot * 64 + 32 + j] = l;
+        }
+      }
+    }
+    u += kb1 - kb0;
+    first = false;
+  }
+}
+
+// Merge for attn_fwd_sk_lds: one 256-thread block per 32-query tile.
+__global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
+                                                         const float* __restrict__ part_ml, float* __restrict__ out,
+                                                         int B, int T, int H, int P) {
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const long long U = (long long)B * H * QG * NK;
+  const int wv = blockIdx.x & 3;
+  const long long grp = blockIdx.x >> 2;
+  const int qg = int(grp % QG);
+  const int qt = qg * 4 + wv;
+  if (qt >= QT) return;
+  const long long t0 = grp * NK, t1 = t0 + NK;
+  const long long w_lo = ((t0 + 1) * P + U - 1) / U - 1;
+  const long long w_hi = (t1 * P + U - 1) / U - 1;
+  if (w_lo == w_hi) return;
+  const int head = int((grp / QG) % H);
+  const int b = int(grp / ((long long)QG * H));
+  const int D = H * HD;
+  const int d = threadIdx.x & 63;
+  for (int jq = threadIdx.x >> 6; jq < 32; jq += 4) {
+    const int q = qt * 32 + jq;
+    if (q >= T) break;
+    float mmax = -INFINITY;
+    for (long long w = w_lo; w <= w_hi; ++w) {
+      const long long s = w * U / P;
+      if (s == (w + 1) * U / P) continue;
+      const size_t slot = (size_t(w) * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
+      mmax = fmaxf(mmax, part_ml[slot * 64 + jq]);
+    }
+    float num = 0.f, den = 0.f;
+    for (long long w = w_lo; w <= w_hi; ++w) {
+      const long long s = w * U / P;
+      if (s == (w + 1) * U / P) continue;
+      const size_t slot = (size_t(w) * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
+      const float sc = __builtin_amdgcn_exp2f(part_ml[slot * 64 + jq] - mmax);
+      num += part_o[slot * (HD * 32) + d * 32 + jq] * sc;
+      den += part_ml[slot * 64 + 32 + jq] * sc;
+    }
+    out[(size_t(b) * T + q) * D + head * HD + d] = num / den;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -360,27 +576,36 @@ int nos_bias_gelu_f32(float* y, const float* b, int rows, int N, void* stream) {
 
 // Resident attention waves per CU (occupancy of attn_fwd_sk); the persistent grid is this times
 // the slice's CU count.
-// Variant: 2 or 3 resident waves per SIMD (register budget 256 or 168 VGPRs).
-static int g_wpe = 3;
+// Variant: 0 = LDS-shared K/V workgroup kernel (default); 2 / 3 = one-wave kernel with 2 or 3
+// resident waves per SIMD (register budget 256 or 168 VGPRs), kept for A/B measurement.
+static int g_variant = 0;
 
-int nos_attention_set_variant(int wpe) {
-  if (wpe != 2 && wpe != 3) return -1;
-  g_wpe = wpe;
+int nos_attention_set_variant(int v) {
+  if (v != 0 && v != 2 && v != 3) return -1;
+  g_variant = v;
   return 0;
 }
 
+// Persistent grid slots per CU for the selected variant (workgroups, not waves).
 int nos_attention_waves_per_cu() {
   int n = 0;
-  const hipError_t e = g_wpe == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<3>, 64, 0)
-                                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<2>, 64, 0);
-  if (e != hipSuccess || n <= 0) n = 4 * g_wpe;
+  hipError_t e;
+  if (g_variant == 0)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk_lds, 256, 0);
+  else if (g_variant == 3)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<3>, 64, 0);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_sk<2>, 64, 0);
+  if (e != hipSuccess || n <= 0) n = g_variant == 0 ? 2 : 4 * g_variant;
   return n;
 }
 
 // bytes of caller-provided workspace for a stream-K launch of `waves` waves. The workspace comes
 // from the caller's stream-ordered allocator, so concurrent slices never share scratch and a launch
 // inside graph capture never allocates.
-size_t nos_attention_ws_bytes(int waves) { return size_t(waves) * 2 * (HD * 32 + 64) * sizeof(float); }
+size_t nos_attention_ws_bytes(int waves) {
+  return size_t(waves) * 2 * (HD * 32 + 64) * sizeof(float) * (g_variant == 0 ? 4 : 1);
+}
 
 int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, int H, int head_dim, float scale,
                          int waves, void* stream) {
@@ -395,9 +620,19 @@ int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, 
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const float scale_log2e = scale * 1.4426950408889634f;
   const int NK = (T + 31) / 32;
+  if (g_variant == 0) {
+    const int QG = (NK + 3) / 4;
+    float* part_o = ws;
+    float* part_ml = ws + size_t(waves) * 8 * HD * 32;
+    hipLaunchKernelGGL(attn_fwd_sk_lds, dim3(waves), dim3(256), 0, s, qkv, out, part_o, part_ml, B, T, H,
+                       scale_log2e, waves);
+    if (int rc = check_launch("attn_fwd_sk_lds")) return rc;
+    hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves);
+    return check_launch("attn_sk_lds_fixup");
+  }
   float* part_o = ws;
   float* part_ml = ws + size_t(waves) * 2 * HD * 32;
-  if (g_wpe == 3)
+  if (g_variant == 3)
     hipLaunchKernelGGL(attn_fwd_sk<3>, dim3(waves), dim3(64), 0, s, qkv, out, part_o, part_ml, B, T, H, scale_log2e,
                        waves);
   else

@@ -57,11 +57,16 @@ def test_attention_stream_k_any_grid_matches_reference(K, T, H, B):
     qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
     ref = _ref_attention(qkv, H, 64, 0.125)
     units = B * H * ((T + 31) // 32) ** 2
-    for waves in (1, 3, 7, 64, 333, 1024, 3072, units + 5):
-        out = torch.full((B, T, H * 64), float("nan"), device="cuda")
-        K.attention_sk(qkv, out, H, 64, 0.125, waves)
-        torch.cuda.synchronize()
-        assert (out - ref).abs().max().item() < 2e-5, waves
+    try:
+        for variant in (0, 2, 3):
+            K.set_attention_variant(variant)
+            for waves in (1, 3, 7, 64, 333, 1024, 3072, units + 5):
+                out = torch.full((B, T, H * 64), float("nan"), device="cuda")
+                K.attention_sk(qkv, out, H, 64, 0.125, waves)
+                torch.cuda.synchronize()
+                assert (out - ref).abs().max().item() < 2e-5, (variant, waves)
+    finally:
+        K.set_attention_variant(0)
     un = K.attention_unsplit(qkv, H, 64, 0.125)
     assert (un - ref).abs().max().item() < 2e-5
 

@@ -1,0 +1,141 @@
+"""Packaging: kustomize manifests, Helm chart, CRDs, ComponentConfigs, console scripts, demo."""
+import glob
+import importlib
+import os
+import re
+import sys
+
+import pytest
+import yaml
+
+from walkai_nos_amd.api.config import (CapacitySchedulingArgs, GpuAgentConfig, GpuPartitionerConfig, MigAgentConfig,
+                                       load_config)
+from walkai_nos_amd.models.xcp.known_configs import load_known_geometries
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _p(*a):
+    return os.path.join(ROOT, *a)
+
+
+def test_every_plain_yaml_parses():
+    files = [f for pat in ("config/**/*.yaml", "demos/**/*.yaml", "hack/**/*.yaml", ".github/**/*.yml",
+                           "helm-charts/nos/values.yaml", "helm-charts/nos/Chart.yaml", "helm-charts/nos/crds/*.yaml")
+             for f in glob.glob(_p(pat), recursive=True)]
+    assert len(files) > 20
+    for f in files:
+        docs = [d for d in yaml.safe_load_all(open(f)) if d is not None]
+        assert docs, f
+
+
+def test_crds_match_between_kustomize_and_helm():
+    for f in glob.glob(_p("config/crd/bases/*.yaml")):
+        helm = _p("helm-charts/nos/crds", os.path.basename(f))
+        assert open(f).read() == open(helm).read()
+    kinds = {yaml.safe_load(open(f))["spec"]["names"]["kind"] for f in glob.glob(_p("config/crd/bases/*.yaml"))}
+    assert kinds == {"ElasticQuota", "CompositeElasticQuota"}
+
+
+def test_crd_schema_covers_quota_model_fields():
+    eq = yaml.safe_load(open(_p("config/crd/bases/nos.nebuly.com_elasticquotas.yaml")))
+    v = eq["spec"]["versions"][0]
+    props = v["schema"]["openAPIV3Schema"]["properties"]
+    assert set(props["spec"]["properties"]) == {"min", "max"}
+    assert props["spec"]["required"] == ["min"]
+    assert "used" in props["status"]["properties"]
+    assert v["subresources"] == {"status": {}}
+    ceq = yaml.safe_load(open(_p("config/crd/bases/nos.nebuly.com_compositeelasticquotas.yaml")))
+    cprops = ceq["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["spec"]
+    assert set(cprops["required"]) == {"namespaces", "min"}
+
+
+def test_component_configs_in_manifests_load_and_validate():
+    assert isinstance(load_config(open(_p("config/gpupartitioner/gpu_partitioner_config.yaml")).read()),
+                      GpuPartitionerConfig)
+    assert isinstance(load_config(open(_p("config/partitionagent/partition_agent_config.yaml")).read()),
+                      MigAgentConfig)
+    assert isinstance(load_config(open(_p("config/sliceagent/slice_agent_config.yaml")).read()), GpuAgentConfig)
+    args = load_config(open(_p("config/quota/scheduler_config.yaml")).read())
+    assert isinstance(args, CapacitySchedulingArgs) and args.nvidiaGpuResourceMemoryGB == 288
+    specs = load_known_geometries(open(_p("config/gpupartitioner/known_geometries.yaml")).read())
+    assert specs["MI355X"].allowed_geometries
+
+
+def test_helm_known_geometries_value_loads():
+    values = yaml.safe_load(open(_p("helm-charts/nos/values.yaml")))
+    specs = load_known_geometries(yaml.safe_dump(values["gpuPartitioner"]["knownGeometries"]))
+    assert {"MI355X", "MI350X", "MI325X", "MI300X"} <= set(specs)
+    assert values["nvidiaGpuResourceMemoryGB"] == 288
+
+
+def _flatten(d, prefix=""):
+    out = set()
+    for k, v in d.items():
+        key = f"{prefix}.{k}" if prefix else k
+        out.add(key)
+        if isinstance(v, dict):
+            out |= _flatten(v, key)
+    return out
+
+
+def test_helm_templates_only_reference_defined_values():
+    values = _flatten(yaml.safe_load(open(_p("helm-charts/nos/values.yaml"))))
+    missing = []
+    for f in glob.glob(_p("helm-charts/nos/templates/**/*.yaml"), recursive=True) + \
+            glob.glob(_p("helm-charts/nos/templates/*.tpl")):
+        for ref in re.findall(r"\.Values\.([A-Za-z0-9_.]+)", open(f).read()):
+            if ref not in values:
+                missing.append((os.path.relpath(f, ROOT), ref))
+    assert not missing, missing
+
+
+def test_helm_template_blocks_balanced():
+    for f in glob.glob(_p("helm-charts/nos/templates/**/*.yaml"), recursive=True):
+        s = open(f).read()
+        opens = len(re.findall(r"{{-?\s*(if|with|range|define)\b", s))
+        ends = len(re.findall(r"{{-?\s*end\s*-?}}", s))
+        assert opens == ends, f
+
+
+def test_console_scripts_resolve():
+    try:
+        import tomllib
+    except ImportError:  # py3.10
+        import tomli as tomllib
+    proj = tomllib.load(open(_p("pyproject.toml"), "rb"))
+    scripts = proj["project"]["scripts"]
+    assert len(scripts) >= 8
+    for name, target in scripts.items():
+        mod, fn = target.split(":")
+        assert callable(getattr(importlib.import_module(mod), fn)), name
+
+
+def test_manifests_reference_existing_entry_points():
+    try:
+        import tomllib
+    except ImportError:
+        import tomli as tomllib
+    scripts = set(tomllib.load(open(_p("pyproject.toml"), "rb"))["project"]["scripts"])
+    used = set()
+    for f in glob.glob(_p("config/**/*.yaml"), recursive=True) + \
+            glob.glob(_p("helm-charts/nos/templates/**/*.yaml"), recursive=True):
+        used |= set(re.findall(r"command: \[(nos-[a-z]+)\]", open(f).read()))
+    assert used and used <= scripts, used - scripts
+
+
+def test_demo_client_uses_safe_loaders_only():
+    src = open(_p("demos/gpu-sharing-comparison/client/main.py")).read()
+    assert "allow_pickle=False" in src and "safetensors" in src
+    assert "pickle.load" not in src and "weights_only=False" not in src
+    compile(src, "main.py", "exec")
+
+
+@pytest.mark.parametrize("overlay,resource", [("xcp", "amd.com/cpx_nps1"), ("cumask", "amd.com/gpu-32cu.36gb"),
+                                              ("time-slicing", "amd.com/gpu")])
+def test_demo_overlays_request_valid_resources(overlay, resource):
+    from walkai_nos_amd import constant
+    k = yaml.safe_load(open(_p("demos/gpu-sharing-comparison/manifests/overlays", overlay, "kustomization.yaml")))
+    assert resource in k["patches"][0]["patch"]
+    assert (resource == constant.RESOURCE_AMD_GPU or constant.RESOURCE_XCP_REGEX.match(resource)
+            or constant.RESOURCE_SLICE_REGEX.match(resource))

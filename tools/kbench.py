@@ -4,7 +4,8 @@ CU-masked streams of 256/128/64/32 CUs (SPX/DPX/QPX/CPX-sized slices), one slice
     python tools/kbench.py [--iters N] [--out gpurun_out/kbench.json]
 
 Reports microseconds per call and achieved TFLOP/s for: attention (unsplit one-wave-per-tile
-baseline, stream-K with 2 and 3 resident waves/SIMD, PyTorch SDPA), and the four fp32 GEMMs of a
+baseline, stream-K LDS-shared workgroup kernel, stream-K one-wave kernel with 2 and 3
+resident waves/SIMD, PyTorch SDPA), and the four fp32 GEMMs of a
 layer (hipBLASLt via torch).
 """
 from __future__ import annotations
@@ -63,13 +64,13 @@ def main() -> int:
             r = {"slice": label, "cus": n}
             K.set_slice_cus(n)
             r["attn_unsplit_us"] = timeit(lambda: K.attention_unsplit(qkv, H, HD, 0.125), s, a.iters)
-            for wpe in (2, 3):
-                K.set_attention_variant(wpe)
+            for var in (0, 2, 3):
+                K.set_attention_variant(var)
                 wv = K.attention_waves(n)
-                r[f"attn_sk{wpe}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, a.iters)
-                r[f"attn_sk{wpe}_waves"] = wv
+                r[f"attn_sk{var}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, a.iters)
+                r[f"attn_sk{var}_grid"] = wv
             r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, a.iters)
-            for kname in ("attn_unsplit_us", "attn_sk2_us", "attn_sk3_us", "attn_sdpa_us"):
+            for kname in ("attn_unsplit_us", "attn_sk0_us", "attn_sk2_us", "attn_sk3_us", "attn_sdpa_us"):
                 r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
             gemms = {"qkv": (lambda: torch.matmul(x, w_qkv.t()), 2.0 * T * D * 3 * D),
                      "proj": (lambda: torch.matmul(x, w_o.t()), 2.0 * T * D * D),
@@ -85,7 +86,7 @@ def main() -> int:
                     r[kname] = round(r[kname], 2)
             print(json.dumps(r), flush=True)
             results.append(r)
-    K.set_attention_variant(3)
+    K.set_attention_variant(0)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(results, f, indent=1)

@@ -7,6 +7,7 @@ not a DaemonSet (every node POSTed the same cluster-wide snapshot).
 from __future__ import annotations
 
 import argparse
+import os
 import logging
 import sys
 import threading
@@ -31,7 +32,7 @@ def main(argv=None) -> int:
     ap.add_argument("--endpoint", required=True)
     ap.add_argument("--interval", default="1m")
     ap.add_argument("--http-timeout", default="10s")
-    ap.add_argument("--api-token", default="")
+    ap.add_argument("--api-token", default=os.environ.get("NOS_API_TOKEN", ""))
     ap.add_argument("--kubeconfig", default="")
     ap.add_argument("--log-level", default="info")
     args = ap.parse_args(argv)

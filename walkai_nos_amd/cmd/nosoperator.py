@@ -1,6 +1,7 @@
 """nos-operator: (Composite)ElasticQuota status and pod capacity labels."""
 from __future__ import annotations
 
+import os
 import sys
 
 from ..api.config import CapacitySchedulingArgs, GpuPartitionerConfig, load_config_file
@@ -13,6 +14,9 @@ def main(argv=None) -> int:
     args = base_parser("nos operator").parse_args(argv)
     setup_logging(args.log_level)
     sargs = load_config_file(args.config, "CapacitySchedulingArgs") if args.config else CapacitySchedulingArgs()
+    if not args.config and os.environ.get("NOS_GPU_MEMORY_GB"):
+        sargs.nvidiaGpuResourceMemoryGB = int(os.environ["NOS_GPU_MEMORY_GB"])
+        sargs.validate()
     client = make_client(args.kubeconfig)
     mcfg = GpuPartitionerConfig()
     mcfg.leaderElection.leaderElect = True

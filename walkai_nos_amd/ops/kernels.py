@@ -51,15 +51,16 @@ def slice_cus() -> int:
 _waves_per_cu: Optional[int] = None
 
 
-def set_attention_variant(waves_per_simd: int) -> None:
-    """Register budget of the stream-K kernel: 3 resident waves/SIMD (168 VGPRs) or 2 (256)."""
+def set_attention_variant(variant: int) -> None:
+    """0 = LDS-shared K/V workgroup kernel (default); 2 / 3 = one-wave-per-tile stream-K kernel
+    with 2 or 3 resident waves per SIMD (A/B reference)."""
     global _waves_per_cu
-    _check(_L().nos_attention_set_variant(waves_per_simd))
+    _check(_L().nos_attention_set_variant(variant))
     _waves_per_cu = None
 
 
 def attention_waves(cus: int) -> int:
-    """Persistent stream-K grid for a slice of ``cus`` CUs: every resident wave slot, once."""
+    """Persistent stream-K grid for a slice of ``cus`` CUs: every resident workgroup slot, once."""
     global _waves_per_cu
     if _waves_per_cu is None:
         _waves_per_cu = int(_L().nos_attention_waves_per_cu())
