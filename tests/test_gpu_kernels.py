@@ -125,6 +125,41 @@ def test_linear_residual(K):
     assert (out - ref).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("M,N,Kd", [(3401, 384, 384), (3401, 1152, 384), (3401, 1536, 384), (3401, 384, 1536),
+                                    (100, 128, 64), (1, 128, 32)])
+def test_mfma_gemm_every_tile_and_epilogue(K, M, N, Kd):
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(0)
+    x = torch.randn(M, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda")
+    h = x.double() @ w.double().t()
+    refs = {"plain": (h, {}), "bias": (h + b.double(), {"bias": b}),
+            "gelu": (None, {"bias": b, "gelu": True}), "res": (h + b.double() + r.double(), {"bias": b, "residual": r})}
+    hb = h + b.double()
+    refs["gelu"] = (0.5 * hb * (1 + torch.erf(hb / math.sqrt(2))), refs["gelu"][1])
+    for cfg in G.eligible(M, N, Kd):
+        for name, (ref, kw) in refs.items():
+            out = G.gemm(x, w, tile=cfg, **kw)
+            torch.cuda.synchronize()
+            err = (out.double() - ref).abs().max().item()
+            assert err < 2e-3 * max(1.0, Kd / 384), (cfg, name, err)
+
+
+def test_gemm_autotune_picks_and_caches(K):
+    from walkai_nos_amd.ops import gemm as G
+    x = torch.randn(3401, 384, device="cuda")
+    w = torch.randn(1536, 384, device="cuda") * 0.05
+    b = torch.randn(1536, device="cuda")
+    out = K.linear_gelu(x, w, b)
+    hb = x.double() @ w.double().t() + b.double()
+    ref = 0.5 * hb * (1 + torch.erf(hb / math.sqrt(2)))
+    assert (out.double() - ref).abs().max().item() < 2e-3
+    assert G.choose(3401, 1536, 384, G.EPI_BIAS | G.EPI_GELU, K.slice_cus()) is not None
+    assert G.tuning_table()
+
+
 def test_yolos_hip_matches_torch_backend(K):
     from walkai_nos_amd.models.workload.yolos import YolosSmall, demo_input
     m = YolosSmall().cuda().eval()

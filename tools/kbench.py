@@ -20,6 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from walkai_nos_amd.bench_core import slice_cus  # noqa: E402
+from walkai_nos_amd.ops import gemm as G  # noqa: E402
 from walkai_nos_amd.ops import kernels as K  # noqa: E402
 from walkai_nos_amd.ops.probe import Stream  # noqa: E402
 
@@ -52,6 +53,7 @@ def main() -> int:
     w_qkv, w_o = torch.randn(3 * D, D, device="cuda"), torch.randn(D, D, device="cuda")
     w_1, w_2 = torch.randn(FF, D, device="cuda"), torch.randn(D, FF, device="cuda")
     b_ff = torch.randn(FF, device="cuda")
+    b_qkv, b_d = torch.randn(3 * D, device="cuda"), torch.randn(D, device="cuda")
     attn_flops = 4.0 * T * T * HD * H
     q, k, v = qkv.view(1, T, 3, H, HD).permute(2, 0, 3, 1, 4)
     results = []
@@ -74,12 +76,24 @@ def main() -> int:
                 r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
             gemms = {"qkv": (lambda: torch.matmul(x, w_qkv.t()), 2.0 * T * D * 3 * D),
                      "proj": (lambda: torch.matmul(x, w_o.t()), 2.0 * T * D * D),
-                     "fc1": (lambda: K.linear_gelu(x, w_1, b_ff), 2.0 * T * D * FF),
+                     "fc1": (lambda: G._library(x, w_1, b_ff, None, torch.empty(T, FF, device="cuda"),
+                                                G.EPI_BIAS | G.EPI_GELU), 2.0 * T * D * FF),
                      "fc2": (lambda: torch.matmul(h, w_2.t()), 2.0 * T * FF * D)}
             for gname, (fn, fl) in gemms.items():
                 us = timeit(fn, s, a.iters)
                 r[f"gemm_{gname}_us"] = round(us, 1)
                 r[f"gemm_{gname}_tflops"] = round(fl / us / 1e6, 2)
+            # hand-written MFMA GEMM, every tile, with the model's fused epilogues
+            mfma = {"qkv": (x, w_qkv, {"bias": b_qkv}, 2.0 * T * D * 3 * D),
+                    "proj": (x, w_o, {"bias": b_d, "residual": x}, 2.0 * T * D * D),
+                    "fc1": (x, w_1, {"bias": b_ff, "gelu": True}, 2.0 * T * D * FF),
+                    "fc2": (h, w_2, {"bias": b_d, "residual": x}, 2.0 * T * FF * D)}
+            for gname, (xa, wa, kw, fl) in mfma.items():
+                for cfg in G.eligible(xa.shape[0], wa.shape[0], xa.shape[1]):
+                    us = timeit(lambda: G.gemm(xa, wa, tile=cfg, **kw), s, a.iters)
+                    tag = "x".join(map(str, G.TILES[cfg]))
+                    r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
+                    r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
             r["layernorm_us"] = round(timeit(lambda: K.layernorm(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
             for kname in list(r):
                 if isinstance(r[kname], float):

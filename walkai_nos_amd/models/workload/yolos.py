@@ -73,7 +73,7 @@ class _Block(nn.Module):
         B, T, D = x.shape
         H, Dh = self.c.num_heads, self.c.head_dim
         h = K.layernorm(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
-        qkv = F.linear(h, self.qkv.weight, self.qkv.bias)                  # [B, T, 3D]
+        qkv = K.linear(h, self.qkv.weight, self.qkv.bias)                  # [B, T, 3D]
         o = K.attention_qkv(qkv, H, Dh, 1.0 / math.sqrt(Dh))               # [B, T, D]
         x = K.linear_residual(o, self.proj.weight, self.proj.bias, x)      # x + o @ Wp^T + bp
         h = K.layernorm(x, self.ln2.weight, self.ln2.bias, self.c.layer_norm_eps)

@@ -9,9 +9,9 @@ Kernels (``csrc/kernels.hip``):
 
 * ``layernorm``        — one wave per row, fp32, vectorised float4 loads, two-pass mean/var in
   registers (rows of 384 floats = 6 floats per lane);
-* ``linear_gelu``      — hipBLASLt GEMM (``F.linear``) + fused bias+erf-GELU epilogue kernel;
-* ``linear_residual``  — hipBLASLt GEMM with the residual folded in as the GEMM's C input
-  (``torch.addmm`` beta=1), no extra pass;
+* ``linear`` / ``linear_gelu`` / ``linear_residual`` — fp32 MFMA GEMM (``csrc/gemm.hip``) with bias,
+  exact-erf GELU or the residual add fused into the store; tile shape autotuned per (shape, slice)
+  against hipBLASLt, which stays the choice where it is faster (``ops/gemm.py``);
 * ``attention_qkv``    — flash attention over the packed ``[B, T, 3*D]`` QKV tensor on
   ``v_mfma_f32_32x32x2_f32`` (exact fp32 MFMA), online softmax, stream-K decomposition over
   (32-query tile x 32-key block) units with a persistent grid sized to the slice's CUs; writes
@@ -131,26 +131,43 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> 
     return out
 
 
-def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    if not _use_hip(x) or x.dtype != torch.float32:
-        return F.gelu(F.linear(x, w, b))
-    y = torch.matmul(x, w.t())  # bias + GELU fused in the epilogue kernel below
+def bias_gelu_(y: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """In place ``y = GELU(y + b)`` (exact erf) with the HIP epilogue kernel."""
     N = y.shape[-1]
-    rows = y.numel() // N
     if N % 4 != 0:
-        return F.gelu(y + b)
-    _check(_L().nos_bias_gelu_f32(y.data_ptr(), b.data_ptr(), rows, N, _stream()))
+        y.copy_(F.gelu(y + b))
+        return y
+    _check(_L().nos_bias_gelu_f32(y.data_ptr(), b.data_ptr(), y.numel() // N, N, _stream()))
     return y
 
 
+def gelu_epilogue(y: torch.Tensor) -> torch.Tensor:
+    y.copy_(F.gelu(y))
+    return y
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """``x @ w^T + b`` on the MFMA GEMM (or hipBLASLt where the tuner found it faster)."""
+    if not _use_hip(x) or x.dtype != torch.float32:
+        return F.linear(x, w, b)
+    from .gemm import gemm
+    return gemm(x, w, b)
+
+
+def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``GELU(x @ w^T + b)`` with bias and exact GELU fused into the GEMM's store."""
+    if not _use_hip(x) or x.dtype != torch.float32:
+        return F.gelu(F.linear(x, w, b))
+    from .gemm import gemm
+    return gemm(x, w, b, gelu=True)
+
+
 def linear_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
-    """``res + x @ w^T + b`` with the residual and bias folded into one GEMM call."""
-    if not x.is_cuda or get_backend() == "torch":
+    """``res + x @ w^T + b`` with bias and residual fused into the GEMM's store."""
+    if not _use_hip(x) or x.dtype != torch.float32:
         return res + F.linear(x, w, b)
-    shp = res.shape
-    c = (res + b).reshape(-1, shp[-1])  # one fused elementwise pass; GEMM accumulates onto it
-    out = torch.addmm(c, x.reshape(-1, x.shape[-1]), w.t())
-    return out.view(shp)
+    from .gemm import gemm
+    return gemm(x, w, b, residual=res)
 
 
 def attention_ref(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
