@@ -223,3 +223,49 @@ def test_shared_state_token_semantics():
     s.on_report_done()
     s.on_apply_done()
     assert not s.at_least_one_report_since_last_apply()
+
+
+def test_probe_on_commit_publishes_status_probe_annotation():
+    import json
+
+    from walkai_nos_amd.controllers.agent.probe import ProbeRunner
+    e = Env()
+    calls = []
+
+    def fake_probe(dev, cus, label):
+        calls.append(label)
+        n = 32 if e.smi.get_compute_partition(0) == "CPX" else 256
+        return {"n_cus": n, "bf16_tflops": 5.0 * n, "fp32_tflops": 0.5 * n, "hbm_gbps": 600.0}
+
+    runner = ProbeRunner(e.shared, "node-a", probe_fn=fake_probe,
+                         targets=lambda: [(i, None, f"dev{i}") for i in range(2)], asynchronous=False)
+    e.reporter.extra = runner.annotations
+    e.reporter.reconcile(Request("node-a"))
+    doc = json.loads(e.annotations()[api.ANNOTATION_PROBE_RESULT])  # startup baseline of the current layout
+    assert doc["commit"] == 0 and doc["slices"]["dev0"]["fp32_tflops"] == 128.0
+    e.spec({"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", api.ANNOTATION_PARTITIONING_PLAN: "1"})
+    e.actuator.reconcile(Request("node-a"))
+    e.reporter.reconcile(Request("node-a"))
+    doc = json.loads(e.annotations()[api.ANNOTATION_PROBE_RESULT])
+    assert doc["commit"] == 1 and set(doc["slices"]) == {"dev0", "dev1"}
+    assert doc["slices"]["dev0"]["fp32_tflops"] == 16.0
+    e.reporter.reconcile(Request("node-a"))
+    assert calls == ["dev0", "dev1"] * 2  # one probe round per commit, not per report
+
+
+def test_probe_runner_survives_a_failing_slice():
+    from walkai_nos_amd.controllers.agent.probe import ProbeRunner
+    s = SharedState()
+
+    def probe(dev, cus, label):
+        if dev == 1:
+            raise RuntimeError("device lost")
+        return {"n_cus": 64, "bf16_tflops": 300.0}
+
+    r = ProbeRunner(s, "n", probe_fn=probe, targets=lambda: [(0, None, "a"), (1, None, "b")], asynchronous=False)
+    s.record_commit(True)
+    r.poll()
+    assert r.results["slices"]["a"]["bf16_tflops"] == 300.0 and "error" in r.results["slices"]["b"]
+    s.record_commit(False)  # a vetoed commit does not trigger a new round
+    r.poll()
+    assert r.results["commit"] == 1

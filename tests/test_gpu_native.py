@@ -105,3 +105,16 @@ def test_rccl_node_barrier_all_local_devices(gpu):
         assert b.vote_all([False] + [True] * (torch.cuda.device_count() - 1)) is False
     finally:
         b.close()
+
+
+def test_probe_on_commit_with_real_kernels(gpu):
+    from walkai_nos_amd.controllers.agent.probe import ProbeRunner, hip_probe
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    s = SharedState()
+    r = ProbeRunner(s, "box", probe_fn=hip_probe, targets=lambda: [(0, None, "whole"), (0, list(range(32)), "cpx0")],
+                    asynchronous=False)
+    r.poll()
+    whole, cpx = r.results["slices"]["whole"], r.results["slices"]["cpx0"]
+    assert whole["n_cus"] >= 256 and cpx["n_cus"] == 32
+    assert 300 < whole["bf16_tflops"] < 2600 and whole["hbm_gbps"] > 1000
+    assert 3 < whole["bf16_tflops"] / cpx["bf16_tflops"] < 12

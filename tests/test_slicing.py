@@ -112,3 +112,14 @@ def test_slicing_node_greedy():
     assert n.update_geometry_for({"32cu.36gb": 10})
     assert n.gpus[0].geometry() == {"32cu.36gb": 8} and n.gpus[1].geometry() == {"32cu.36gb": 2}
     assert n.allocatable["amd.com/gpu-32cu.36gb"] == 10
+
+
+def test_slice_probe_targets_cover_each_live_slice_cu_set():
+    from walkai_nos_amd.controllers.sliceagent.agent import slice_probe_targets
+    from walkai_nos_amd.device.slicing_client import MemorySliceStore
+    store = MemorySliceStore()
+    store.save({0: place([], [("g::s0", "32cu.36gb"), ("g::s1", "64cu.72gb")], 256), 1: [Slice("h::s0", "10gb")]})
+    t = {label: (gpu, cus) for gpu, cus, label in slice_probe_targets(store)()}
+    assert set(t) == {"g::s0", "g::s1", "h::s0"}
+    assert len(t["g::s0"][1]) == 32 and len(t["g::s1"][1]) == 64 and t["g::s1"][0] == 0
+    assert t["h::s0"][0] == 1 and len(t["h::s0"][1]) == 256  # memory-only slice runs on the shared pool

@@ -49,8 +49,12 @@ def main(argv=None) -> int:
     dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
     mgr = make_manager(client, cfg, "partitionagent")
     bf = node_barrier_factory(smi) if cfg.commitBarrier == "rccl" else None
+    probe = None
+    if cfg.probeOnCommit:
+        from ..controllers.agent.probe import ProbeRunner
+        probe = lambda shared: ProbeRunner(shared, node).annotations  # noqa: E731
     setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
-                          refresh_interval=cfg.reportConfigIntervalSeconds)
+                          refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe)
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr)
 

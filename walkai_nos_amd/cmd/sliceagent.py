@@ -48,8 +48,14 @@ def main(argv=None) -> int:
         def restart(self, node_name, timeout=60):
             plugins.sync()
 
+    cu_count = gpus[0].cu_count or 256
+    probe = None
+    if cfg.probeOnCommit:
+        from ..controllers.agent.probe import ProbeRunner
+        from ..controllers.sliceagent.agent import slice_probe_targets
+        probe = lambda shared: ProbeRunner(shared, node, targets=slice_probe_targets(store, cu_count)).annotations  # noqa: E731
     setup_slice_agent(mgr, node, sc, store, device_plugin=Notify(), refresh_interval=cfg.reportConfigIntervalSeconds,
-                      cu_count=gpus[0].cu_count or 256, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288)
+                      cu_count=cu_count, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288, probe=probe)
     stop = threading.Event()
     threading.Thread(target=run_forever, args=(plugins, 2.0, stop), daemon=True).start()
     serve_endpoints(mgr, cfg)

@@ -150,7 +150,7 @@ class Actuator:
             self._reregister()
         REGISTRY.phase_seconds.labels(phase="agent_apply_total").observe(time.perf_counter() - t0)
         self.applied_plans += 1
-        self.shared.last_commit = "ok" if ok else "failed"
+        self.shared.record_commit(ok)
         if plan.blocked:
             for g, reason in plan.blocked:
                 log.info("GPU %d not changed: %s", g, reason)

@@ -14,8 +14,18 @@ from .shared import SharedState
 def setup_partition_agent(mgr: Manager, node_name: str, partition_client: Any, device_plugin: Any = None,
                           barrier_factory: Optional[BarrierFactory] = None, refresh_interval: float = 10.0,
                           verify: Optional[Callable[[int, str], bool]] = None,
-                          extra_annotations: Optional[Callable[[], dict]] = None):
+                          extra_annotations: Optional[Callable[[], dict]] = None,
+                          probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None):
+    """``probe``: factory taking the agent's SharedState and returning an extra-annotation hook
+    (e.g. ``lambda sh: ProbeRunner(sh, node).annotations``) that measures each commit."""
     shared = SharedState()
+    if probe is not None:
+        hook = probe(shared)
+        if extra_annotations is None:
+            extra_annotations = hook
+        else:
+            user = extra_annotations
+            extra_annotations = lambda: {**user(), **hook()}  # noqa: E731
     reporter = Reporter(mgr.client, partition_client, shared, refresh_interval, extra_annotations=extra_annotations)
     actuator = Actuator(mgr.client, partition_client, shared, node_name, device_plugin, barrier_factory, verify,
                         clock=mgr.clock)

@@ -21,8 +21,15 @@ class SharedState:
         self.lock = threading.RLock()
         self.last_parsed_plan_id: str = ""
         self.last_commit: Optional[str] = None
+        self.commit_seq = 0  # bumped on every successful commit (probe-on-commit trigger)
         self._token = False
         self._token_lock = threading.Lock()
+
+    def record_commit(self, ok: bool) -> None:
+        with self.lock:
+            self.last_commit = "ok" if ok else "failed"
+            if ok:
+                self.commit_seq += 1
 
     def on_report_done(self) -> None:
         with self._token_lock:

@@ -139,7 +139,7 @@ class SliceActuator:
             if self.device_plugin is not None:
                 self.device_plugin.restart(self.node_name)
             REGISTRY.phase_seconds.labels(phase="agent_apply_total").observe(time.perf_counter() - t0)
-            self.shared.last_commit = "ok" if ok else "failed"
+            self.shared.record_commit(ok)
             self.shared.on_apply_done()
             if not ok:
                 raise GpuError("commit barrier vetoed the slice plan")
@@ -158,10 +158,13 @@ class SliceActuator:
 
 def setup_slice_agent(mgr: Manager, node_name: str, slicing_client: Any, store: Any, device_plugin: Any = None,
                       barrier_factory: Optional[Callable[[int], Any]] = None, refresh_interval: float = 10.0,
-                      cu_count: int = 256, memory_gb: int = 288):
+                      cu_count: int = 256, memory_gb: int = 288,
+                      probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None):
     from ...models.slicing.profile import extract_profile_name
     shared = SharedState()
-    reporter = Reporter(mgr.client, slicing_client, shared, refresh_interval, profile_extractor=extract_profile_name)
+    extra = probe(shared) if probe is not None else None
+    reporter = Reporter(mgr.client, slicing_client, shared, refresh_interval, profile_extractor=extract_profile_name,
+                        extra_annotations=extra)
     actuator = SliceActuator(mgr.client, slicing_client, store, shared, node_name, device_plugin, barrier_factory,
                              cu_count, memory_gb)
     mgr.new_controller(constant.SLICE_AGENT_REPORTER_CONTROLLER, reporter.reconcile,
@@ -170,3 +173,17 @@ def setup_slice_agent(mgr: Manager, node_name: str, slicing_client: Any, store: 
                        [Watch("Node", [ExcludeDelete(), MatchingName(node_name), AnnotationsChanged()])])
     return shared, reporter, actuator
 
+
+
+def slice_probe_targets(store: Any, cu_count: int = 256) -> Callable[[], list]:
+    """Probe targets for :class:`~walkai_nos_amd.controllers.agent.probe.ProbeRunner`: every live
+    slice's CU set on its physical GPU (a CU-masked stream), labelled by the slice id."""
+    from ...models.slicing.cumask import cus_of
+
+    def targets() -> list:
+        out = []
+        for gpu, slices in sorted(store.load().items()):
+            for sl in slices:
+                out.append((gpu, cus_of(sl, slices, cu_count), sl.id))
+        return out
+    return targets
