@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -41,11 +42,15 @@ __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast
 
 template <int DTYPE>
 __global__ __launch_bounds__(kThreads) void mfma_probe(const uint4* __restrict__ src, uint32_t src_len,
-                                                      float* __restrict__ out, int iters) {
+                                                      float* __restrict__ out, int iters,
+                                                      unsigned long long* __restrict__ clk) {
   __shared__ uint4 lds[kLdsVec];
   const int t = threadIdx.x;
   for (int i = t; i < kLdsVec; i += kThreads) lds[i] = src[(blockIdx.x * 131u + i) % src_len];
   __syncthreads();
+  // shader-clock cycles (s_memtime) vs the constant-rate wall clock (s_memrealtime) over the loop:
+  // their ratio is the core clock the matrix pipes actually ran at under this load (DVFS).
+  const unsigned long long c0 = clock64(), w0 = wall_clock64();
 
   float result = 0.f;
   if constexpr (DTYPE == 0) {  // bf16 32x32x16
@@ -105,6 +110,10 @@ __global__ __launch_bounds__(kThreads) void mfma_probe(const uint4* __restrict__
     for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
   }
   out[blockIdx.x * kThreads + t] = result;
+  if (clk != nullptr && t == 0) {
+    clk[2 * blockIdx.x] = clock64() - c0;
+    clk[2 * blockIdx.x + 1] = wall_clock64() - w0;
+  }
 }
 
 // FLOP per loop iteration per wave for each dtype variant
@@ -150,6 +159,8 @@ struct Scratch {
   uint32_t src_len = 0;
   float* out = nullptr;
   size_t out_len = 0;
+  unsigned long long* clk = nullptr;
+  size_t clk_len = 0;
 };
 thread_local Scratch g_s;
 
@@ -171,6 +182,11 @@ int ensure_scratch(int device, int n_wg) {
     if (int rc = check(hipMalloc(&g_s.out, need * sizeof(float)), "hipMalloc out")) return rc;
     g_s.out_len = need;
   }
+  if (g_s.clk_len < size_t(n_wg) * 2) {
+    if (g_s.clk) hipFree(g_s.clk);
+    if (int rc = check(hipMalloc(&g_s.clk, size_t(n_wg) * 2 * sizeof(unsigned long long)), "hipMalloc clk")) return rc;
+    g_s.clk_len = size_t(n_wg) * 2;
+  }
   return 0;
 }
 
@@ -183,6 +199,7 @@ struct nos_probe_result {
   double flops;    // FLOP (or bytes moved for the HBM probe) per launch
   double rate;     // TFLOP/s (or GB/s)
   int32_t n_wg;
+  double mhz;      // mean shader clock over the MFMA loop (0 for the HBM probe)
 };
 
 const char* nos_probe_last_error() { return g_err.c_str(); }
@@ -231,10 +248,10 @@ int nos_probe_mfma(int device, void* stream, int dtype, int n_wg, int iters, int
   hipEventCreate(&e1);
   auto launch = [&]() {
     switch (dtype) {
-      case 0: hipLaunchKernelGGL(mfma_probe<0>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
-      case 1: hipLaunchKernelGGL(mfma_probe<1>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
-      case 2: hipLaunchKernelGGL(mfma_probe<2>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
-      default: hipLaunchKernelGGL(mfma_probe<3>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters); break;
+      case 0: hipLaunchKernelGGL(mfma_probe<0>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters, g_s.clk); break;
+      case 1: hipLaunchKernelGGL(mfma_probe<1>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters, g_s.clk); break;
+      case 2: hipLaunchKernelGGL(mfma_probe<2>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters, g_s.clk); break;
+      default: hipLaunchKernelGGL(mfma_probe<3>, dim3(n_wg), dim3(kThreads), 0, s, g_s.src, g_s.src_len, g_s.out, iters, g_s.clk); break;
     }
   };
   launch();  // warm-up (code object load, clocks)
@@ -255,6 +272,20 @@ int nos_probe_mfma(int device, void* stream, int dtype, int n_wg, int iters, int
   res->flops = kFlopPerIterWave[dtype] * double(iters) * double(n_wg) * (kThreads / 64);
   res->rate = res->flops / (best * 1e-3) / 1e12;
   res->n_wg = n_wg;
+  // clock of the last rep: sum of shader cycles / sum of wall ticks x wall-clock rate
+  res->mhz = 0;
+  int wall_khz = 0;
+  if (hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && wall_khz > 0) {
+    std::vector<unsigned long long> h(size_t(n_wg) * 2);
+    if (hipMemcpy(h.data(), g_s.clk, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+      double cyc = 0, wall = 0;
+      for (int i = 0; i < n_wg; ++i) {
+        cyc += double(h[2 * i]);
+        wall += double(h[2 * i + 1]);
+      }
+      if (wall > 0) res->mhz = cyc / wall * (wall_khz / 1000.0);
+    }
+  }
   return 0;
 }
 
@@ -290,6 +321,7 @@ int nos_probe_hbm(int device, void* stream, size_t bytes, int n_wg, int reps, no
   res->flops = 2.0 * double(n) * sizeof(uint4);
   res->rate = res->flops / (best * 1e-3) / 1e9;
   res->n_wg = n_wg;
+  res->mhz = 0;
   return 0;
 }
 

@@ -12,22 +12,11 @@ from walkai_nos_amd.models.partitioned import PartitionedGPU, PartitionedNode
 from walkai_nos_amd.models.xcp import known_configs as kc
 from walkai_nos_amd.models.xcp.profile import XcpProfile, extract_profile_name, parse_profile, smaller_than
 
-A100_80 = [
-    {"1g.10gb": 7},
-    {"1g.10gb": 5, "2g.20gb": 1},
-    {"1g.10gb": 3, "2g.20gb": 2},
-    {"1g.10gb": 1, "2g.20gb": 3},
-    {"1g.10gb": 2, "2g.20gb": 1, "3g.40gb": 1},
-    {"2g.20gb": 2, "3g.40gb": 1},
-    {"1g.10gb": 3, "3g.40gb": 1},
-    {"1g.10gb": 1, "2g.20gb": 1, "3g.40gb": 1},
-    {"3g.40gb": 2},
-    {"1g.10gb": 3, "4g.40gb": 1},
-    {"1g.10gb": 1, "2g.20gb": 1, "4g.40gb": 1},
-    {"7g.79gb": 1},
-]
-A100_40 = [{"7g.40gb": 1}, {"4g.20gb": 1, "2g.10gb": 1, "1g.5gb": 1}, {"3g.20gb": 2}, {"1g.5gb": 7}]
-A30 = [{"4g.24gb": 1}, {"2g.12gb": 2}, {"2g.12gb": 1, "1g.6gb": 2}, {"1g.6gb": 4}]
+from walkai_nos_amd.models import mig  # noqa: E402
+
+A100_80 = mig.KNOWN_GEOMETRIES[mig.A100_PCIE_80GB]
+A100_40 = mig.KNOWN_GEOMETRIES[mig.A100_SXM4_40GB]
+A30 = mig.KNOWN_GEOMETRIES[mig.A30]
 
 
 def g(table, used=None, free=None, model="m"):
@@ -161,3 +150,11 @@ def test_profiles_total_order_and_resources():
     assert extract_profile_name("amd.com/gpu") is None
     with pytest.raises(ValueError):
         parse_profile("cpx-nps1")
+
+
+def test_mig_parity_tables_and_helpers():
+    assert mig.parse_profile("1g.10gb") == (1, 10) and mig.parse_profile("x") is None
+    assert mig.extract_profile_name("nvidia.com/mig-3g.40gb") == "3g.40gb"
+    assert mig.memory_gb("7g.79gb") == 79
+    gpu = mig.new_gpu(mig.A100_PCIE_80GB, used={"1g.10gb": 1})
+    assert gpu.update_geometry_for({"3g.40gb": 2}) and gpu.free.get("3g.40gb") == 1

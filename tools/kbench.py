@@ -44,6 +44,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="gpurun_out/kbench.json")
+    ap.add_argument("--only", choices=("all", "attn", "gemm"), default="all")
+    ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     a = ap.parse_args()
     torch.manual_seed(0)
     qkv = torch.randn(1, T, 3 * D, device="cuda")
@@ -59,41 +61,18 @@ def main() -> int:
     results = []
     for prof, part, label in (("spx_nps1", 0, "spx"), ("dpx_nps1", 0, "dpx"), ("qpx_nps1", 0, "qpx"),
                               ("cpx_nps1", 0, "cpx")):
+        if label not in a.slices.split(","):
+            continue
         cus = slice_cus(prof, part)
         n = 256 if cus is None else len(cus)
         with Stream(0, cus) as hs:
             s = hs.torch_stream()
             r = {"slice": label, "cus": n}
             K.set_slice_cus(n)
-            r["attn_unsplit_us"] = timeit(lambda: K.attention_unsplit(qkv, H, HD, 0.125), s, a.iters)
-            for var in (0, 2, 3):
-                K.set_attention_variant(var)
-                wv = K.attention_waves(n)
-                r[f"attn_sk{var}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, a.iters)
-                r[f"attn_sk{var}_grid"] = wv
-            r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, a.iters)
-            for kname in ("attn_unsplit_us", "attn_sk0_us", "attn_sk2_us", "attn_sk3_us", "attn_sdpa_us"):
-                r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
-            gemms = {"qkv": (lambda: torch.matmul(x, w_qkv.t()), 2.0 * T * D * 3 * D),
-                     "proj": (lambda: torch.matmul(x, w_o.t()), 2.0 * T * D * D),
-                     "fc1": (lambda: G._library(x, w_1, b_ff, None, torch.empty(T, FF, device="cuda"),
-                                                G.EPI_BIAS | G.EPI_GELU), 2.0 * T * D * FF),
-                     "fc2": (lambda: torch.matmul(h, w_2.t()), 2.0 * T * FF * D)}
-            for gname, (fn, fl) in gemms.items():
-                us = timeit(fn, s, a.iters)
-                r[f"gemm_{gname}_us"] = round(us, 1)
-                r[f"gemm_{gname}_tflops"] = round(fl / us / 1e6, 2)
-            # hand-written MFMA GEMM, every tile, with the model's fused epilogues
-            mfma = {"qkv": (x, w_qkv, {"bias": b_qkv}, 2.0 * T * D * 3 * D),
-                    "proj": (x, w_o, {"bias": b_d, "residual": x}, 2.0 * T * D * D),
-                    "fc1": (x, w_1, {"bias": b_ff, "gelu": True}, 2.0 * T * D * FF),
-                    "fc2": (h, w_2, {"bias": b_d, "residual": x}, 2.0 * T * FF * D)}
-            for gname, (xa, wa, kw, fl) in mfma.items():
-                for cfg in G.eligible(xa.shape[0], wa.shape[0], xa.shape[1]):
-                    us = timeit(lambda: G.gemm(xa, wa, tile=cfg, **kw), s, a.iters)
-                    tag = "x".join(map(str, G.TILES[cfg]))
-                    r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
-                    r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
+            if a.only in ("all", "attn"):
+                attn_bench(r, qkv, out, q, k, v, n, s, a.iters, attn_flops)
+            if a.only in ("all", "gemm"):
+                gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, a.iters)
             r["layernorm_us"] = round(timeit(lambda: K.layernorm(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
             for kname in list(r):
                 if isinstance(r[kname], float):
@@ -105,6 +84,38 @@ def main() -> int:
     with open(a.out, "w") as f:
         json.dump(results, f, indent=1)
     return 0
+
+
+def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)):
+    r["attn_unsplit_us"] = timeit(lambda: K.attention_unsplit(qkv, H, HD, 0.125), s, iters)
+    for var in variants:
+        K.set_attention_variant(var)
+        wv = K.attention_waves(n)
+        r[f"attn_sk{var}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, iters)
+        r[f"attn_sk{var}_grid"] = wv
+    K.set_attention_variant(0)
+    r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, iters)
+    for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")]:
+        r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
+
+
+def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
+    lib = {"qkv": (x, w_qkv, b_qkv, None, 0, 2.0 * T * D * 3 * D),
+           "proj": (x, w_o, b_d, x, G.EPI_RES, 2.0 * T * D * D),
+           "fc1": (x, w_1, b_ff, None, G.EPI_GELU, 2.0 * T * D * FF),
+           "fc2": (h, w_2, b_d, x, G.EPI_RES, 2.0 * T * FF * D)}
+    for gname, (xa, wa, ba, ra, epi, fl) in lib.items():
+        o = torch.empty(xa.shape[0], wa.shape[0], device="cuda")
+        us = timeit(lambda: G._library(xa, wa, ba, ra, o, G.EPI_BIAS | epi), s, iters)
+        r[f"gemm_{gname}_us"] = round(us, 1)
+        r[f"gemm_{gname}_tflops"] = round(fl / us / 1e6, 2)
+        # hand-written MFMA GEMM, every tile, same fused epilogue
+        kw = {"bias": ba, "gelu": bool(epi & G.EPI_GELU), "residual": ra}
+        for cfg in G.eligible(xa.shape[0], wa.shape[0], xa.shape[1]):
+            us = timeit(lambda: G.gemm(xa, wa, tile=cfg, **kw), s, iters)
+            tag = "x".join(map(str, G.TILES[cfg]))
+            r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
+            r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
 
 
 if __name__ == "__main__":

@@ -20,7 +20,7 @@ DTYPES = {"bf16": 0, "bf16_16x16": 1, "fp32": 2, "fp8": 3}
 
 class ProbeResult(ctypes.Structure):
     _fields_ = [("ms", ctypes.c_double), ("flops", ctypes.c_double), ("rate", ctypes.c_double),
-                ("n_wg", ctypes.c_int32)]
+                ("n_wg", ctypes.c_int32), ("mhz", ctypes.c_double)]
 
 
 _configured = False
@@ -118,6 +118,16 @@ class SliceProbe:
     tflops: float
     tflops_per_cu: float
     n_wg: int
+    mhz: float = 0.0  # mean shader clock over the loop (s_memtime / s_memrealtime)
+
+    @property
+    def pct_of_clock_peak(self) -> float:
+        """Achieved rate over the matrix-pipe peak at the measured clock (0 if unknown)."""
+        # matrix-pipe FLOP per clock per CU
+        per_clk = {"bf16": 4096, "bf16_16x16": 4096, "fp32": 256, "fp8": 8192}.get(self.dtype, 0)
+        if not self.mhz or not per_clk:
+            return 0.0
+        return 100.0 * self.tflops * 1e12 / (per_clk * self.n_cus * self.mhz * 1e6)
 
 
 def probe_mfma(dtype: str = "bf16", device: int = 0, stream: Optional[Stream] = None, n_cus: Optional[int] = None,
@@ -127,7 +137,7 @@ def probe_mfma(dtype: str = "bf16", device: int = 0, stream: Optional[Stream] = 
     r = ProbeResult()
     _check(_lib().nos_probe_mfma(device, stream.handle if stream else None, DTYPES[dtype], n_wg, iters, reps,
                                  ctypes.byref(r)))
-    return SliceProbe(dtype, n_cus, r.ms, r.rate, r.rate / n_cus, n_wg)
+    return SliceProbe(dtype, n_cus, r.ms, r.rate, r.rate / n_cus, n_wg, r.mhz)
 
 
 def probe_hbm(device: int = 0, stream: Optional[Stream] = None, nbytes: int = 1 << 30, n_wg: Optional[int] = None,
