@@ -43,14 +43,14 @@ def test_validation_and_cu_budget():
     with pytest.raises(ValueError):
         sg(40, {"30gb": 2})
     with pytest.raises(ValueError):
-        SlicingGPU("MI355X", 0, 288, 256, {"12cu.10gb": 1}).validate()  # not a multiple of 8 CUs
+        SlicingGPU("MI355X", 0, 288, 256, {"48cu.10gb": 1}).validate()  # not a multiple of 32 CUs
     g = SlicingGPU.full("MI355X", 0, 288, 256)
     assert g.update_geometry_for({"128cu.100gb": 3})
     assert g.geometry() == {"128cu.100gb": 2}  # 256 dedicated CUs max
     g2 = SlicingGPU.full("MI355X", 0, 288, 256)
-    g2.create_slices("10gb", 1)  # a shared slice reserves 8 CUs for the shared pool
+    g2.create_slices("10gb", 1)  # a shared slice reserves one 32-CU row group for the shared pool
     assert not g2.create_slices("256cu.10gb", 1)
-    assert g2.create_slices("248cu.10gb", 1)
+    assert g2.create_slices("224cu.10gb", 1)
 
 
 def test_profiles():
@@ -112,6 +112,19 @@ def test_slicing_node_greedy():
     assert n.update_geometry_for({"32cu.36gb": 10})
     assert n.gpus[0].geometry() == {"32cu.36gb": 8} and n.gpus[1].geometry() == {"32cu.36gb": 2}
     assert n.allocatable["amd.com/gpu-32cu.36gb"] == 10
+
+
+def test_row_groups_keep_slices_shader_engine_balanced():
+    from walkai_nos_amd.models.slicing.cumask import GROUP_ROWS, allocate_rows
+    placed = place([], [("g::a", "32cu.36gb"), ("g::b", "96cu.108gb"), ("g::c", "64cu.72gb")], 256)
+    for s_ in placed:
+        # every slice owns each shader engine (row mod 4) of every XCD equally often
+        per_se = [sum(1 for r in s_.rows if r % GROUP_ROWS == se) for se in range(GROUP_ROWS)]
+        assert len(set(per_se)) == 1, (s_.profile, s_.rows)
+    # a stale unaligned slice blocks its whole group, never splits a new slice over SEs unevenly
+    rows = allocate_rows(4, [5], 32)
+    assert rows == [0, 1, 2, 3]
+    assert allocate_rows(8, [5], 32) == [8, 9, 10, 11, 12, 13, 14, 15]
 
 
 def test_slice_probe_targets_cover_each_live_slice_cu_set():

@@ -6,19 +6,25 @@ Measured on the box (``profiles/gpu_report_r1_first.json``, census of CU-masked 
 * an XCD whose mask bits are all zero is **not** disabled: a mask of bits {0, 8, 16, ...} (all on
   XCD 0) still ran on all 256 CUs.
 
-So a slice must own CUs on every XCD.  The unit of allocation is a **row**: 8 consecutive mask bits
-``[8r, 8r+8)`` = one CU on each of the 8 XCDs; a 256-CU MI355X has 32 rows.  A ``<c>cu`` slice
-owns ``c/8`` rows (contiguous when possible).  Memory-only (shared) slices run on the rows no
-dedicated slice owns.  Rows of slices in use are never moved.
+* mask row ``r`` (bits ``[8r, 8r+8)``, one CU on each XCD) sits on shader engine ``r mod 4`` of
+  every XCD (``profiles/census_map_r1.json``), and each XCD hands workgroups to its 4 SEs
+  round-robin, so a slice must also own the same number of CUs on every SE.
+
+So the unit of allocation is a **row group**: 4 consecutive rows ``[4g, 4g+4)`` = 32 mask bits = one
+CU on every SE of every XCD; a 256-CU MI355X has 8 groups.  A ``<c>cu`` slice owns ``c/32`` groups
+(contiguous when possible).  Memory-only (shared) slices run on the rows no dedicated slice owns.
+Rows of slices in use are never moved.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass, field
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
-from .profile import CU_GRANULARITY, parse_profile
+from .profile import parse_profile
 
 XCDS = 8
+ROW_CUS = 8          # mask bits per row (one CU per XCD)
+GROUP_ROWS = 4       # rows per allocation group (one CU per SE per XCD)
 
 
 @dataclass
@@ -42,23 +48,29 @@ class Slice:
 
 
 def rows_total(cu_count: int) -> int:
-    return cu_count // CU_GRANULARITY
+    return cu_count // ROW_CUS
 
 
 def allocate_rows(n_rows: int, taken: Iterable[int], total_rows: int) -> Optional[List[int]]:
-    """First-fit contiguous run of ``n_rows`` free rows; falls back to any free rows; None if short."""
+    """Whole free row groups for ``n_rows`` rows (a multiple of :data:`GROUP_ROWS`): a contiguous
+    run of groups first-fit, else any free groups; None if there are not enough free groups."""
     taken_set = set(taken)
-    free = [r for r in range(total_rows) if r not in taken_set]
-    if len(free) < n_rows:
+    n_groups = -(-n_rows // GROUP_ROWS)
+    free = [g for g in range(total_rows // GROUP_ROWS)
+            if not any(GROUP_ROWS * g + i in taken_set for i in range(GROUP_ROWS))]
+    if len(free) < n_groups:
         return None
+    pick: Optional[List[int]] = None
     run: List[int] = []
-    for r in free:
-        if run and r != run[-1] + 1:
+    for g in free:
+        if run and g != run[-1] + 1:
             run = []
-        run.append(r)
-        if len(run) == n_rows:
-            return run
-    return free[:n_rows]
+        run.append(g)
+        if len(run) == n_groups:
+            pick = run
+            break
+    pick = pick or free[:n_groups]
+    return [GROUP_ROWS * g + i for g in pick for i in range(GROUP_ROWS)][:n_rows]
 
 
 def place(existing: Sequence[Slice], wanted: Sequence[Tuple[str, str]], cu_count: int) -> List[Slice]:
@@ -70,7 +82,7 @@ def place(existing: Sequence[Slice], wanted: Sequence[Tuple[str, str]], cu_count
     # largest first limits fragmentation
     for sid, prof in sorted(wanted, key=lambda w: -parse_profile(w[1]).cus):
         p = parse_profile(prof)
-        need = p.cus // CU_GRANULARITY
+        need = p.cus // ROW_CUS
         rows: List[int] = []
         if need:
             got = allocate_rows(need, taken, total)

@@ -9,7 +9,7 @@ A slice here has two dimensions:
 * ``<m>gb``          — an HBM budget of *m* GB, compute shared with the other shared slices
   (exactly the reference's MPS semantics: "compute shared equally");
 * ``<c>cu.<m>gb``    — *c* dedicated CUs (a disjoint CU mask, multiple of :data:`CU_GRANULARITY`,
-  placed XCD-aligned where possible) plus *m* GB of HBM.
+  placed as whole XCD- and SE-balanced row groups) plus *m* GB of HBM.
 
 Resource names are ``amd.com/gpu-<profile>``; profiles contain no ``-``.
 """
@@ -23,10 +23,14 @@ from typing import Optional
 from ... import constant
 
 MIN_SLICE_MEMORY_GB = 1
-#: CU-mask granularity: one shader engine of gfx950 (256 CUs / 32 SEs)
-CU_GRANULARITY = 8
+#: CU-mask granularity: one CU on every shader engine of every XCD (8 XCDs x 4 SEs = 32 CUs).
+#: Measured on the box (``profiles/census_map_r1.json``): mask row r (bits 8r..8r+7, one CU per
+#: XCD) sits on shader engine r mod 4, and workgroups are handed to the SEs of an XCD round-robin
+#: whatever their number of enabled CUs, so a slice whose rows cover the SEs unevenly runs at the
+#: pace of its thinnest SE (a 48-CU slice = 2/2/1/1 CUs per SE ran like a 32-CU one).
+CU_GRANULARITY = 32
 #: CUs always left to the shared pool when memory-only slices exist
-MIN_SHARED_CUS = 8
+MIN_SHARED_CUS = 32
 REPLICA_SEPARATOR = "::"
 
 _PROFILE_RE = re.compile(r"^(?:(\d+)cu\.)?(\d+)gb$")
