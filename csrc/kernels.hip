@@ -498,10 +498,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
   }
 }
 
-// Merge for attn_fwd_sk_lds: one 256-thread block per 32-query tile.
+// Merge for attn_fwd_sk_lds: one 256-thread block per 32-query tile. Partials are [d][32 q]
+// images, so thread t reads elements e = t + 256*i (q = t % 32, d = e / 32): every contributor's
+// 8 KB image is read with fully coalesced 1 KB wave loads, scaled by exp2(m_w[q] - m_max[q]) and
+// accumulated in registers; the normalised tile is transposed through LDS so the [q][d] output rows
+// are written as 256-B runs.
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
                                                          int B, int T, int H, int P) {
+  __shared__ float s_mmax[32], s_inv[32];
+  __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
   const long long U = (long long)B * H * QG * NK;
   const int wv = blockIdx.x & 3;
@@ -516,27 +522,50 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   const int head = int((grp / QG) % H);
   const int b = int(grp / ((long long)QG * H));
   const int D = H * HD;
-  const int d = threadIdx.x & 63;
-  for (int jq = threadIdx.x >> 6; jq < 32; jq += 4) {
-    const int q = qt * 32 + jq;
-    if (q >= T) break;
+  const int tid = threadIdx.x;
+  auto slot_of = [&](long long w) -> long long {
+    const long long s = w * U / P;
+    if (s == (w + 1) * U / P) return -1;  // empty range
+    return (w * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
+  };
+  if (tid < 32) {
     float mmax = -INFINITY;
     for (long long w = w_lo; w <= w_hi; ++w) {
-      const long long s = w * U / P;
-      if (s == (w + 1) * U / P) continue;
-      const size_t slot = (size_t(w) * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
-      mmax = fmaxf(mmax, part_ml[slot * 64 + jq]);
+      const long long sl = slot_of(w);
+      if (sl >= 0) mmax = fmaxf(mmax, part_ml[sl * 64 + tid]);
     }
-    float num = 0.f, den = 0.f;
+    float den = 0.f;
     for (long long w = w_lo; w <= w_hi; ++w) {
-      const long long s = w * U / P;
-      if (s == (w + 1) * U / P) continue;
-      const size_t slot = (size_t(w) * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
-      const float sc = __builtin_amdgcn_exp2f(part_ml[slot * 64 + jq] - mmax);
-      num += part_o[slot * (HD * 32) + d * 32 + jq] * sc;
-      den += part_ml[slot * 64 + 32 + jq] * sc;
+      const long long sl = slot_of(w);
+      if (sl >= 0) den += part_ml[sl * 64 + 32 + tid] * __builtin_amdgcn_exp2f(part_ml[sl * 64 + tid] - mmax);
     }
-    out[(size_t(b) * T + q) * D + head * HD + d] = num / den;
+    s_mmax[tid] = mmax;
+    s_inv[tid] = 1.f / den;
+  }
+  __syncthreads();
+  const int q = tid & 31;
+  const float mq = s_mmax[q];
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (long long w = w_lo; w <= w_hi; ++w) {
+    const long long sl = slot_of(w);
+    if (sl < 0) continue;
+    const float sc = __builtin_amdgcn_exp2f(part_ml[sl * 64 + q] - mq);
+    const float* po = part_o + sl * (HD * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += po[tid + 256 * i] * sc;
+  }
+  const float inv = s_inv[q];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s_tile[(tid + 256 * i) >> 5][q] = acc[i] * inv;
+  __syncthreads();
+  // transposed store: thread -> (query row, 64 dims), 4 rows per pass
+  const int d = tid & 63;
+  for (int jq = tid >> 6; jq < 32; jq += 4) {
+    const int qq = qt * 32 + jq;
+    if (qq >= T) break;
+    out[(size_t(b) * T + qq) * D + head * HD + d] = s_tile[d][jq];
   }
 }
 

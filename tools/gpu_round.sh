@@ -32,6 +32,9 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench_hip 600 python bench.py --steps 10 --warmup 2 --out "$OUT/bench_hip.json"
   step bench_torch 600 python bench.py --steps 10 --warmup 2 --backend torch --out "$OUT/bench_torch.json"
 fi
+if [ "$MODE" = all ] || [ "$MODE" = curve ]; then
+  step sharing_curve 500 python tools/sharing_curve.py --seconds 4 --out "$OUT/sharing_curve.json"
+fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
   step rocprof_bench 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- \

@@ -94,6 +94,8 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
         r[f"attn_sk{var}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, wv), s, iters)
         r[f"attn_sk{var}_grid"] = wv
     K.set_attention_variant(0)
+    for mult in (1, 2):  # LDS kernel with fewer persistent workgroups per CU than resident slots
+        r[f"attn_sk0g{mult}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, mult * n), s, iters)
     r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, iters)
     for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")]:
         r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)

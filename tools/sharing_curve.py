@@ -5,8 +5,9 @@
 * ``shared``  — every pod on its own HIP stream with no CU mask: the hardware scheduler runs all
   pods' kernels concurrently over all 256 CUs (what AMD GPUs do for co-resident processes; the
   analogue of the reference's time-slicing and MPS rows);
-* ``cumask``  — each pod gets a disjoint XCD-symmetric CU set of floor(32/N) rows (8 CUs per row,
-  one per XCD), i.e. the nos CU-mask slice an ``amd.com/gpu-<c>cu.<m>gb`` request receives;
+* ``cumask``  — the GPU's 8 SE-balanced 32-CU row groups are dealt out to the N pods as evenly as
+  possible (N=3: 96/96/64 CUs), each pod on its own disjoint CU mask — the nos CU-mask slices
+  ``amd.com/gpu-<c>cu.<m>gb`` requests receive;
 * ``cpx``     — each pod gets one CPX-sized partition (32 CUs, 1/8 of the GPU) regardless of N:
   the MIG-1g analogue (fixed-size hardware slice).
 
@@ -45,8 +46,12 @@ def cu_sets(mode: str, n: int):
         return [None] * n
     if mode == "cpx":
         return [list(range(32 * i, 32 * (i + 1))) for i in range(n)]
-    rows = 32 // n
-    return [list(range(8 * rows * i, 8 * rows * (i + 1))) for i in range(n)]
+    groups = [8 // n + (1 if i < 8 % n else 0) for i in range(n)]
+    out, g0 = [], 0
+    for g in groups:
+        out.append(list(range(32 * g0, 32 * (g0 + g))))
+        g0 += g
+    return out
 
 
 class Pod:
@@ -109,7 +114,7 @@ def run(mode: str, n: int, seconds: float, template: YolosSmall) -> dict:
         p.close()
     torch.cuda.synchronize()
     agg = total / window
-    row = {"mode": mode, "pods": n, "cus_per_pod": pods[0].n_cus, "aggregate_inf_per_s": round(agg, 2),
+    row = {"mode": mode, "pods": n, "cus_per_pod": [p.n_cus for p in pods], "aggregate_inf_per_s": round(agg, 2),
            "mean_latency_s": round(sum(lats) / max(1, len(lats)), 4), "inferences": total}
     for ref, curve in REFERENCE.items():
         if n in curve:

@@ -49,22 +49,33 @@ def slice_cus() -> int:
 
 
 _waves_per_cu: Optional[int] = None
+_variant = 0
 
 
 def set_attention_variant(variant: int) -> None:
     """0 = LDS-shared K/V workgroup kernel (default); 2 / 3 = one-wave-per-tile stream-K kernel
     with 2 or 3 resident waves per SIMD (A/B reference)."""
-    global _waves_per_cu
+    global _waves_per_cu, _variant
     _check(_L().nos_attention_set_variant(variant))
     _waves_per_cu = None
+    _variant = variant
 
 
-def attention_waves(cus: int) -> int:
-    """Persistent stream-K grid for a slice of ``cus`` CUs: every resident workgroup slot, once."""
+def attention_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
+    """Persistent stream-K grid for a slice of ``cus`` CUs: every resident workgroup slot, once —
+    except when that leaves fewer than ~30 (128-query x 32-key) units per workgroup (the whole
+    256-CU GPU at T = 3401): then one slot per CU stays empty, so fewer tiles are split across
+    workgroups and the partial/fixup traffic drops (measured: 164 vs 179 us on SPX)."""
     global _waves_per_cu
     if _waves_per_cu is None:
         _waves_per_cu = int(_L().nos_attention_waves_per_cu())
-    return _waves_per_cu * cus
+    per_cu = _waves_per_cu
+    if T and _variant == 0:
+        nk = (T + 31) // 32
+        units = B * H * ((nk + 3) // 4) * nk
+        while per_cu > 1 and units / (per_cu * cus) < 30:
+            per_cu -= 1
+    return per_cu * cus
 
 
 def set_backend(name: str) -> None:
@@ -183,7 +194,7 @@ def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) ->
     qkv = qkv.contiguous()
     B, T, _ = qkv.shape
     out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
-    return attention_sk(qkv, out, heads, head_dim, scale, attention_waves(slice_cus()))
+    return attention_sk(qkv, out, heads, head_dim, scale, attention_waves(slice_cus(), B, T, heads))
 
 
 def attention_sk(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float,
