@@ -6,12 +6,12 @@
 // (bias + exact GELU, bias + residual) cost a second pass over a 21 MB activation. This kernel:
 //
 //  * runs on the exact-fp32 matrix cores (v_mfma_f32_32x32x2_f32); four waves in a 2x2 grid, each
-//    owning a WM x WN sub-tile (1-4 32x32 accumulators), BK = 32 per stage;
-//  * permutes the K index inside a stage (k = 16*half + step) so every lane's operand fragment is
-//    16 contiguous floats: 4 ds_read_b128 per 32-row fragment instead of 16 scalar reads;
-//  * stages A and W tiles through LDS with a 36-float row stride: a 16-lane ds_read_b128 group
-//    reads rows i..i+15 at slot (9*i + c) mod 16, a bijection, so reads are conflict-free; stores
-//    are 8-lane 128-B runs (conflict-free for ds_write_b128);
+//    owning a WM x WN sub-tile (1-4 32x32 accumulators), BK = 32 or 64 per stage;
+//  * permutes the K index inside a stage (k = BK/2*half + step) so every lane's operand fragment is
+//    BK/2 contiguous floats: ds_read_b128 runs instead of scalar reads;
+//  * stages A and W tiles through LDS with a BK+4-float row stride: a 16-lane ds_read_b128 group
+//    reads rows i..i+15 at slot ((BK+4)/4*i + c) mod 16, a bijection, so reads are conflict-free;
+//    stores are 8-lane 128-B runs (conflict-free for ds_write_b128);
 //  * double-buffers LDS with the next stage's global loads held in registers across the MFMAs, one
 //    barrier per stage;
 //  * maps workgroups to tiles XCD-major (hardware round-robins workgroups over the 8 XCDs), so each
@@ -31,8 +31,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 namespace {
 thread_local std::string g_err;
 
-constexpr int BK = 32;
-constexpr int LSTR = 36;  // LDS row stride (floats)
+constexpr int KALIGN = 32;  // K must be a multiple of this (the smallest stage depth)
 
 enum : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RES = 4 };
 
@@ -42,39 +41,49 @@ __device__ __forceinline__ int xcd_major(int phys, int n) {
   return (n % 8 == 0) ? (phys % 8) * (n / 8) + phys / 8 : phys;
 }
 
-template <int AV, int BV>
+// stage of BK k-values: a row segment is BK/4 float4; LDS row stride BK+4 floats keeps the
+// (row * stride / 4) mod 16 slot map a bijection over 16 consecutive rows (stride/4 odd)
+template <int BK>
+struct Stage {
+  static constexpr int C4 = BK / 4;        // float4 per row segment
+  static constexpr int LSTR = BK + 4;      // LDS row stride (floats)
+};
+
+template <int BK, int AV, int BV>
 __device__ __forceinline__ void stage_fetch(float4 (&pa)[AV], float4 (&pb)[BV], const float* __restrict__ A,
                                             const float* __restrict__ W, int m0, int n0, int M, int K, int k0,
                                             int tid) {
+  constexpr int C4 = Stage<BK>::C4;
 #pragma unroll
   for (int v = 0; v < AV; ++v) {
-    const int f = tid + 256 * v, row = f >> 3, c4 = f & 7;
+    const int f = tid + 256 * v, row = f / C4, c4 = f % C4;
     const int gr = min(m0 + row, M - 1);
     pa[v] = *reinterpret_cast<const float4*>(A + size_t(gr) * K + k0 + 4 * c4);
   }
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
-    const int f = tid + 256 * v, row = f >> 3, c4 = f & 7;
+    const int f = tid + 256 * v, row = f / C4, c4 = f % C4;
     pb[v] = *reinterpret_cast<const float4*>(W + size_t(n0 + row) * K + k0 + 4 * c4);
   }
 }
 
-template <int AV, int BV>
+template <int BK, int AV, int BV>
 __device__ __forceinline__ void stage_stash(const float4 (&pa)[AV], const float4 (&pb)[BV], float* as, float* bs,
                                             int tid) {
+  constexpr int C4 = Stage<BK>::C4, LSTR = Stage<BK>::LSTR;
 #pragma unroll
   for (int v = 0; v < AV; ++v) {
-    const int f = tid + 256 * v, row = f >> 3, c4 = f & 7;
+    const int f = tid + 256 * v, row = f / C4, c4 = f % C4;
     *reinterpret_cast<float4*>(&as[row * LSTR + 4 * c4]) = pa[v];
   }
 #pragma unroll
   for (int v = 0; v < BV; ++v) {
-    const int f = tid + 256 * v, row = f >> 3, c4 = f & 7;
+    const int f = tid + 256 * v, row = f / C4, c4 = f % C4;
     *reinterpret_cast<float4*>(&bs[row * LSTR + 4 * c4]) = pb[v];
   }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int BK>
 __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, const float* __restrict__ W,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
                                                   float* __restrict__ C, int M, int N, int K, int epi) {
@@ -82,6 +91,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
   constexpr int TM = WM / 32, TN = WN / 32;          // 32x32 accumulators per wave
   constexpr int AV = BM * BK / 4 / 256;               // float4 per thread per stage (A)
   constexpr int BV = BN * BK / 4 / 256;               // (W)
+  constexpr int LSTR = Stage<BK>::LSTR;
+  constexpr int KS = BK / 2;                          // MFMA k-steps per stage
   __shared__ __attribute__((aligned(16))) float As[2][BM * LSTR];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LSTR];
 
@@ -105,20 +116,20 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
 
   const int nk = K / BK;
-  stage_fetch<AV, BV>(pa, pb, A, W, m0, n0, M, K, 0, tid);
-  stage_stash<AV, BV>(pa, pb, As[0], Bs[0], tid);
+  stage_fetch<BK, AV, BV>(pa, pb, A, W, m0, n0, M, K, 0, tid);
+  stage_stash<BK, AV, BV>(pa, pb, As[0], Bs[0], tid);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
     // unconditional prefetch (the last stage re-reads itself) keeps pa/pb in registers: a
     // conditional update makes the compiler demote them to scratch
-    stage_fetch<AV, BV>(pa, pb, A, W, m0, n0, M, K, min(ks + 1, nk - 1) * BK, tid);
-    float af[TM][16], bf[TN][16];
+    stage_fetch<BK, AV, BV>(pa, pb, A, W, m0, n0, M, K, min(ks + 1, nk - 1) * BK, tid);
+    float af[TM][KS], bf[TN][KS];
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
-      const float* p = &As[buf][(wm * WM + 32 * a + j) * LSTR + 16 * hf];
+      const float* p = &As[buf][(wm * WM + 32 * a + j) * LSTR + KS * hf];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < KS / 4; ++q) {
         const float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
         af[a][4 * q + 0] = v.x;
         af[a][4 * q + 1] = v.y;
@@ -128,9 +139,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
     }
 #pragma unroll
     for (int b = 0; b < TN; ++b) {
-      const float* p = &Bs[buf][(wn * WN + 32 * b + j) * LSTR + 16 * hf];
+      const float* p = &Bs[buf][(wn * WN + 32 * b + j) * LSTR + KS * hf];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < KS / 4; ++q) {
         const float4 v = *reinterpret_cast<const float4*>(p + 4 * q);
         bf[b][4 * q + 0] = v.x;
         bf[b][4 * q + 1] = v.y;
@@ -139,13 +150,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
       }
     }
 #pragma unroll
-    for (int s = 0; s < 16; ++s)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-    stage_stash<AV, BV>(pa, pb, As[buf ^ 1], Bs[buf ^ 1], tid);
+    stage_stash<BK, AV, BV>(pa, pb, As[buf ^ 1], Bs[buf ^ 1], tid);
     __syncthreads();
   }
 
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
   }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int BK>
 int launch(const float* A, const float* W, const float* bias, const float* R, float* C, int M, int N, int K, int epi,
            hipStream_t s) {
   constexpr int BM = 2 * WM, BN = 2 * WN;
@@ -179,7 +190,11 @@ int launch(const float* A, const float* W, const float* bias, const float* R, fl
     return -1;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_f32<WM, WN>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, C, M, N, K, epi);
+  if (K % BK) {
+    g_err = "gemm: K must be a multiple of the stage depth " + std::to_string(BK);
+    return -1;
+  }
+  hipLaunchKernelGGL((gemm_f32<WM, WN, BK>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, C, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("gemm_f32: ") + hipGetErrorString(e);
@@ -193,14 +208,18 @@ extern "C" {
 
 const char* nos_gemm_last_error() { return g_err.c_str(); }
 
-// Tile configurations: 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128 (BM x BN).
-int nos_gemm_num_configs() { return 4; }
+// Tile configurations (BM x BN, stage depth BK): 0 = 64x64/32, 1 = 128x64/32, 2 = 64x128/32,
+// 3 = 128x128/32, 4 = 64x64/64, 5 = 128x64/64, 6 = 64x128/64.
+static const int kCfg[7][3] = {{64, 64, 32}, {128, 64, 32}, {64, 128, 32}, {128, 128, 32},
+                               {64, 64, 64}, {128, 64, 64}, {64, 128, 64}};
 
-int nos_gemm_tile(int cfg, int* bm, int* bn) {
-  static const int t[4][2] = {{64, 64}, {128, 64}, {64, 128}, {128, 128}};
-  if (cfg < 0 || cfg > 3) return -1;
-  *bm = t[cfg][0];
-  *bn = t[cfg][1];
+int nos_gemm_num_configs() { return 7; }
+
+int nos_gemm_tile(int cfg, int* bm, int* bn, int* bk) {
+  if (cfg < 0 || cfg > 6) return -1;
+  *bm = kCfg[cfg][0];
+  *bn = kCfg[cfg][1];
+  *bk = kCfg[cfg][2];
   return 0;
 }
 
@@ -208,7 +227,7 @@ int nos_gemm_tile(int cfg, int* bm, int* bn) {
 // 4 = + R[M,N] (after GELU). K % 32 == 0, N % BN == 0; row-major contiguous operands.
 int nos_gemm_f32(const float* A, const float* W, const float* bias, const float* R, float* C, int M, int N, int K,
                  int epi, int cfg, void* stream) {
-  if (K % BK) {
+  if (K % KALIGN) {
     g_err = "gemm: K must be a multiple of 32";
     return -1;
   }
@@ -218,10 +237,13 @@ int nos_gemm_f32(const float* A, const float* W, const float* bias, const float*
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (cfg) {
-    case 0: return launch<32, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 1: return launch<64, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 2: return launch<32, 64>(A, W, bias, R, C, M, N, K, epi, s);
-    case 3: return launch<64, 64>(A, W, bias, R, C, M, N, K, epi, s);
+    case 0: return launch<32, 32, 32>(A, W, bias, R, C, M, N, K, epi, s);
+    case 1: return launch<64, 32, 32>(A, W, bias, R, C, M, N, K, epi, s);
+    case 2: return launch<32, 64, 32>(A, W, bias, R, C, M, N, K, epi, s);
+    case 3: return launch<64, 64, 32>(A, W, bias, R, C, M, N, K, epi, s);
+    case 4: return launch<32, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
+    case 5: return launch<64, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
+    case 6: return launch<32, 64, 64>(A, W, bias, R, C, M, N, K, epi, s);
     default:
       g_err = "gemm: unknown tile config";
       return -1;

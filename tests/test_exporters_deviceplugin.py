@@ -129,3 +129,22 @@ def test_device_plugin_list_and_watch_allocate_and_register():
         finally:
             mgr.stop()
             reg.stop()
+
+
+def test_amdsmi_metrics_poller_publishes_activity_vram_and_mode():
+    from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+    from walkai_nos_amd.exporters.gpu_metrics import GpuMetricsPoller
+    from walkai_nos_amd.utils.metrics import REGISTRY
+    smi = FakeAmdSmi(n_gpus=2)
+    smi.set_processes(1, 3)
+    p = GpuMetricsPoller(smi, "node-m")
+    p.poll()
+    text = REGISTRY.render().decode()
+    assert 'nos_amdsmi_gfx_activity_percent{gpu="1",node="node-m"} 100.0' in text
+    assert 'nos_amdsmi_partition_info{compute="SPX",gpu="0",memory="NPS1",node="node-m"} 1.0' in text
+    smi.set_processes(0, 0)
+    smi.set_compute_partition(0, "CPX")
+    p.poll()
+    text = REGISTRY.render().decode()
+    assert 'nos_amdsmi_partition_info{compute="CPX",gpu="0",memory="NPS1",node="node-m"} 8.0' in text
+    assert 'compute="SPX",gpu="0",memory="NPS1",node="node-m"' not in text  # stale mode series removed

@@ -115,7 +115,7 @@ def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
         kw = {"bias": ba, "gelu": bool(epi & G.EPI_GELU), "residual": ra}
         for cfg in G.eligible(xa.shape[0], wa.shape[0], xa.shape[1]):
             us = timeit(lambda: G.gemm(xa, wa, tile=cfg, **kw), s, iters)
-            tag = "x".join(map(str, G.TILES[cfg]))
+            tag = "x".join(map(str, G.TILES[cfg][:2])) + f"k{G.TILES[cfg][2]}"
             r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
             r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
 

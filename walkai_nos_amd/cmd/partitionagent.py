@@ -55,6 +55,8 @@ def main(argv=None) -> int:
         probe = lambda shared: ProbeRunner(shared, node).annotations  # noqa: E731
     setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
                           refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe)
+    from ..exporters.gpu_metrics import GpuMetricsPoller
+    GpuMetricsPoller(smi, node).register(mgr)
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr)
 

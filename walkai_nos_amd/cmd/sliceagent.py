@@ -58,6 +58,8 @@ def main(argv=None) -> int:
                       cu_count=cu_count, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288, probe=probe)
     stop = threading.Event()
     threading.Thread(target=run_forever, args=(plugins, 2.0, stop), daemon=True).start()
+    from ..exporters.gpu_metrics import GpuMetricsPoller
+    GpuMetricsPoller(smi, node).register(mgr)
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr, stop)
 

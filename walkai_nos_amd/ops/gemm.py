@@ -1,7 +1,7 @@
 """fp32 GEMM with fused epilogues on the hand-written MFMA kernel (``csrc/gemm.hip``).
 
 ``gemm(x, w, bias=None, gelu=False, residual=None)`` computes ``x @ w^T (+ bias) (GELU) (+ residual)``
-in one kernel. The tile shape (64x64, 128x64, 64x128 or 128x128) is chosen per
+in one kernel. The tile shape (64x64, 128x64, 64x128 or 128x128; stage depth 32 or 64) is chosen per
 ``(M, N, K, epilogue, slice CUs)``: the first call of a new key outside HIP-graph capture times every
 eligible tile on the caller's stream (3 reps each, CUDA events) and caches the fastest together with
 hipBLASLt (``torch.addmm``) as a candidate, so the kernel is only used where it actually wins on
@@ -19,9 +19,11 @@ import torch
 from . import kernels as K
 
 EPI_BIAS, EPI_GELU, EPI_RES = 1, 2, 4
-TILES = {0: (64, 64), 1: (128, 64), 2: (64, 128), 3: (128, 128)}
-#: resident workgroups per CU for each tile (LDS-limited: 37 / 55 / 55 / 74 KB of 160 KB)
-SLOTS_PER_CU = {0: 4, 1: 2, 2: 2, 3: 2}
+#: config -> (BM, BN, BK): workgroup tile and stage depth
+TILES = {0: (64, 64, 32), 1: (128, 64, 32), 2: (64, 128, 32), 3: (128, 128, 32),
+         4: (64, 64, 64), 5: (128, 64, 64), 6: (64, 128, 64)}
+#: resident workgroups per CU for each config (LDS-limited: 37/55/55/74/70/104/104 KB of 160 KB)
+SLOTS_PER_CU = {0: 4, 1: 2, 2: 2, 3: 2, 4: 2, 5: 1, 6: 1}
 LIBRARY = -1  # "use hipBLASLt" choice in the tuning cache
 
 _lock = threading.Lock()
@@ -43,14 +45,14 @@ def _lib() -> ctypes.CDLL:
 def eligible(M: int, N: int, Kd: int) -> list:
     if Kd % 32 or M < 1:
         return []
-    return [c for c, (bm, bn) in TILES.items() if N % bn == 0]
+    return [c for c, (bm, bn, bk) in TILES.items() if N % bn == 0 and Kd % bk == 0]
 
 
 def heuristic(M: int, N: int, cus: int, cands: list) -> int:
     """Fewest 'rounds' of tiles over the slice's workgroup slots, then the larger tile."""
     best, best_key = cands[0], None
     for c in cands:
-        bm, bn = TILES[c]
+        bm, bn, _ = TILES[c]
         tiles = -(-M // bm) * (N // bn)
         slots = SLOTS_PER_CU[c] * cus
         rounds = -(-tiles // slots)
@@ -149,5 +151,6 @@ def gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
 
 def tuning_table() -> Dict[str, str]:
     with _lock:
-        return {f"M{m}_N{n}_K{k}_epi{e}_cus{c}": ("hipblaslt" if v == LIBRARY else "x".join(map(str, TILES[v])))
+        return {f"M{m}_N{n}_K{k}_epi{e}_cus{c}": ("hipblaslt" if v == LIBRARY else "x".join(map(str, TILES[v][:2]))
+                                                  + f"/k{TILES[v][2]}")
                 for (m, n, k, e, c), v in sorted(_cache.items())}
