@@ -83,7 +83,7 @@ __device__ __forceinline__ void stage_stash(const float4 (&pa)[AV], const float4
   }
 }
 
-template <int WM, int WN, int BK>
+template <int WM, int WN, int BK, int NBUF>
 __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, const float* __restrict__ W,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
                                                   float* __restrict__ C, int M, int N, int K, int epi) {
@@ -93,8 +93,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
   constexpr int BV = BN * BK / 4 / 256;               // (W)
   constexpr int LSTR = Stage<BK>::LSTR;
   constexpr int KS = BK / 2;                          // MFMA k-steps per stage
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LSTR];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LSTR];
+  // NBUF = 2: double-buffered stages, one barrier per stage; NBUF = 1: half the LDS (twice the
+  // resident workgroups per CU) for a second barrier per stage
+  __shared__ __attribute__((aligned(16))) float As[NBUF][BM * LSTR];
+  __shared__ __attribute__((aligned(16))) float Bs[NBUF][BN * LSTR];
 
   const int tiles_n = N / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
   stage_stash<BK, AV, BV>(pa, pb, As[0], Bs[0], tid);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
-    const int buf = ks & 1;
+    const int buf = NBUF == 2 ? (ks & 1) : 0;
     // unconditional prefetch (the last stage re-reads itself) keeps pa/pb in registers: a
     // conditional update makes the compiler demote them to scratch
     stage_fetch<BK, AV, BV>(pa, pb, A, W, m0, n0, M, K, min(ks + 1, nk - 1) * BK, tid);
@@ -156,7 +158,13 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
 #pragma unroll
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][s], bf[b][s], acc[a][b], 0, 0, 0);
-    stage_stash<BK, AV, BV>(pa, pb, As[buf ^ 1], Bs[buf ^ 1], tid);
+    if constexpr (NBUF == 1) {
+      // every wave has its fragments (own LDS reads drained) before anyone overwrites the buffer;
+      // a raw barrier: __syncthreads()'s fences here make the compiler demote pa/pb to scratch
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
+    }
+    stage_stash<BK, AV, BV>(pa, pb, As[NBUF == 2 ? (buf ^ 1) : 0], Bs[NBUF == 2 ? (buf ^ 1) : 0], tid);
     __syncthreads();
   }
 
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
   }
 }
 
-template <int WM, int WN, int BK>
+template <int WM, int WN, int BK, int NBUF = 2>
 int launch(const float* A, const float* W, const float* bias, const float* R, float* C, int M, int N, int K, int epi,
            hipStream_t s) {
   constexpr int BM = 2 * WM, BN = 2 * WN;
@@ -194,7 +202,7 @@ int launch(const float* A, const float* W, const float* bias, const float* R, fl
     g_err = "gemm: K must be a multiple of the stage depth " + std::to_string(BK);
     return -1;
   }
-  hipLaunchKernelGGL((gemm_f32<WM, WN, BK>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, C, M, N, K, epi);
+  hipLaunchKernelGGL((gemm_f32<WM, WN, BK, NBUF>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, C, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("gemm_f32: ") + hipGetErrorString(e);
@@ -209,14 +217,15 @@ extern "C" {
 const char* nos_gemm_last_error() { return g_err.c_str(); }
 
 // Tile configurations (BM x BN, stage depth BK): 0 = 64x64/32, 1 = 128x64/32, 2 = 64x128/32,
-// 3 = 128x128/32, 4 = 64x64/64, 5 = 128x64/64, 6 = 64x128/64.
-static const int kCfg[7][3] = {{64, 64, 32}, {128, 64, 32}, {64, 128, 32}, {128, 128, 32},
-                               {64, 64, 64}, {128, 64, 64}, {64, 128, 64}};
+// 3 = 128x128/32, 4 = 64x64/64, 5 = 128x64/64, 6 = 64x128/64; single-buffered LDS:
+// 7 = 64x64/32, 8 = 128x64/32, 9 = 64x128/32.
+static const int kCfg[10][3] = {{64, 64, 32}, {128, 64, 32}, {64, 128, 32}, {128, 128, 32}, {64, 64, 64},
+                                {128, 64, 64}, {64, 128, 64}, {64, 64, 32}, {128, 64, 32}, {64, 128, 32}};
 
-int nos_gemm_num_configs() { return 7; }
+int nos_gemm_num_configs() { return 10; }
 
 int nos_gemm_tile(int cfg, int* bm, int* bn, int* bk) {
-  if (cfg < 0 || cfg > 6) return -1;
+  if (cfg < 0 || cfg > 9) return -1;
   *bm = kCfg[cfg][0];
   *bn = kCfg[cfg][1];
   *bk = kCfg[cfg][2];
@@ -244,6 +253,9 @@ int nos_gemm_f32(const float* A, const float* W, const float* bias, const float*
     case 4: return launch<32, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
     case 5: return launch<64, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
     case 6: return launch<32, 64, 64>(A, W, bias, R, C, M, N, K, epi, s);
+    case 7: return launch<32, 32, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
+    case 8: return launch<64, 32, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
+    case 9: return launch<32, 64, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
     default:
       g_err = "gemm: unknown tile config";
       return -1;

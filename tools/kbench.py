@@ -28,13 +28,21 @@ T, H, HD, D, FF = 3401, 6, 64, 384, 1536
 
 
 def timeit(fn, stream, iters):
+    """GPU time per call: ``iters`` calls captured in one HIP graph on the slice's stream and
+    replayed, so host-side launch overhead (ctypes, allocation) is not measured."""
     with torch.cuda.stream(stream):
         for _ in range(3):
             fn()
+        stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(iters):
+                fn()
+        g.replay()
+        stream.synchronize()
         st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         st.record(stream)
-        for _ in range(iters):
-            fn()
+        g.replay()
         en.record(stream)
     en.synchronize()
     return st.elapsed_time(en) * 1000.0 / iters
@@ -115,7 +123,7 @@ def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
         kw = {"bias": ba, "gelu": bool(epi & G.EPI_GELU), "residual": ra}
         for cfg in G.eligible(xa.shape[0], wa.shape[0], xa.shape[1]):
             us = timeit(lambda: G.gemm(xa, wa, tile=cfg, **kw), s, iters)
-            tag = "x".join(map(str, G.TILES[cfg][:2])) + f"k{G.TILES[cfg][2]}"
+            tag = "x".join(map(str, G.TILES[cfg][:2])) + f"k{G.TILES[cfg][2]}" + ("sb" if cfg >= 7 else "")
             r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
             r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
 

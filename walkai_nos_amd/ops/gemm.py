@@ -3,7 +3,8 @@
 ``gemm(x, w, bias=None, gelu=False, residual=None)`` computes ``x @ w^T (+ bias) (GELU) (+ residual)``
 in one kernel. The tile shape (64x64, 128x64, 64x128 or 128x128; stage depth 32 or 64) is chosen per
 ``(M, N, K, epilogue, slice CUs)``: the first call of a new key outside HIP-graph capture times every
-eligible tile on the caller's stream (3 reps each, CUDA events) and caches the fastest together with
+eligible tile on the caller's stream (3 reps each, replayed from a HIP graph so host launch overhead
+is excluded) and caches the fastest together with
 hipBLASLt (``torch.addmm``) as a candidate, so the kernel is only used where it actually wins on
 the slice it runs on. During graph capture an untuned key falls back to a static heuristic (the tile
 count that best fills the slice's workgroup slots).
@@ -21,9 +22,10 @@ from . import kernels as K
 EPI_BIAS, EPI_GELU, EPI_RES = 1, 2, 4
 #: config -> (BM, BN, BK): workgroup tile and stage depth
 TILES = {0: (64, 64, 32), 1: (128, 64, 32), 2: (64, 128, 32), 3: (128, 128, 32),
-         4: (64, 64, 64), 5: (128, 64, 64), 6: (64, 128, 64)}
-#: resident workgroups per CU for each config (LDS-limited: 37/55/55/74/70/104/104 KB of 160 KB)
-SLOTS_PER_CU = {0: 4, 1: 2, 2: 2, 3: 2, 4: 2, 5: 1, 6: 1}
+         4: (64, 64, 64), 5: (128, 64, 64), 6: (64, 128, 64),
+         7: (64, 64, 32), 8: (128, 64, 32), 9: (64, 128, 32)}  # 7-9: single-buffered LDS
+#: resident workgroups per CU for each config (LDS- or VGPR-limited)
+SLOTS_PER_CU = {0: 4, 1: 2, 2: 2, 3: 2, 4: 2, 5: 1, 6: 1, 7: 8, 8: 5, 9: 5}
 LIBRARY = -1  # "use hipBLASLt" choice in the tuning cache
 
 _lock = threading.Lock()
@@ -93,20 +95,39 @@ def _library(x2, w, bias, res2, out, epi) -> None:
         K.gelu_epilogue(out)
 
 
+def _gpu_time(fn, stream, reps: int = 3) -> float:
+    """GPU milliseconds of ``reps`` calls. On a side stream (the slice's CU-masked stream in the
+    bench) the calls are captured into a HIP graph and replayed, so host launch overhead is not
+    timed; on the legacy default stream (no capture allowed) plain event timing is the fallback."""
+    fn()
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if stream.cuda_stream != 0:
+        stream.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        st.record(stream)
+        g.replay()
+        en.record(stream)
+        en.synchronize()
+        return st.elapsed_time(en)
+    st.record(stream)
+    for _ in range(reps):
+        fn()
+    en.record(stream)
+    en.synchronize()
+    return st.elapsed_time(en)
+
+
 def _tune(key, cands, x2, w, bias, res2, out, epi) -> int:
     stream = torch.cuda.current_stream()
     timings = {}
     for c in cands + [LIBRARY]:
         fn = (lambda c=c: _library(x2, w, bias, res2, out, epi)) if c == LIBRARY else \
             (lambda c=c: _launch(c, x2, w, bias, res2, out, epi))
-        fn()
-        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        st.record(stream)
-        for _ in range(3):
-            fn()
-        en.record(stream)
-        en.synchronize()
-        timings[c] = st.elapsed_time(en)
+        timings[c] = _gpu_time(fn, stream)
     best = min(timings, key=timings.get)
     with _lock:
         _cache[key] = best
@@ -152,5 +173,5 @@ def gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
 def tuning_table() -> Dict[str, str]:
     with _lock:
         return {f"M{m}_N{n}_K{k}_epi{e}_cus{c}": ("hipblaslt" if v == LIBRARY else "x".join(map(str, TILES[v][:2]))
-                                                  + f"/k{TILES[v][2]}")
+                                                  + f"/k{TILES[v][2]}" + ("/sb" if v >= 7 else ""))
                 for (m, n, k, e, c), v in sorted(_cache.items())}
