@@ -150,6 +150,13 @@ class Slot:
             self.stream.synchronize()
             self.graph = g
 
+    def mark(self) -> Any:
+        """Event at the current tail of this slot's stream."""
+        import torch
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
     def close(self) -> None:
         self.graph = None
         self.model = None
@@ -191,6 +198,7 @@ class NodeBench:
         self.pods_samples: List[int] = []
         self.pending_samples: List[int] = []
         self.slots: Dict[Tuple[str, int], Slot] = {}
+        self._inflight: List[Any] = []
         self.gpu = gpu_data_plane
         if self.gpu:
             import torch
@@ -250,10 +258,20 @@ class NodeBench:
         return out
 
     def data_step(self) -> int:
+        """Enqueue this epoch's inferences. The previous epoch's GPU work must be complete first
+        (the control plane of this epoch ran on the CPU meanwhile): at most one epoch is in
+        flight, so the slots running concurrently always belong to one partition layout and a GPU
+        never executes the backlog of an old mode alongside its new one."""
+        if self.gpu:
+            for ev in self._inflight:
+                ev.synchronize()
+            self._inflight = []
         n = 0
         for prof, part, work in self.my_pods():
             if self.gpu:
-                self.slots[(prof, part)].run(work)
+                slot = self.slots[(prof, part)]
+                slot.run(work)
+                self._inflight.append(slot.mark())
             n += work
         self.inferences += n
         return n
