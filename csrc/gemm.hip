@@ -33,7 +33,7 @@ thread_local std::string g_err;
 
 constexpr int KALIGN = 32;  // K must be a multiple of this (the smallest stage depth)
 
-enum : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RES = 4 };
+enum : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RES = 4, EPI_RES2 = 8 };
 
 __device__ __forceinline__ int acc_row(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
@@ -86,7 +86,8 @@ __device__ __forceinline__ void stage_stash(const float4 (&pa)[AV], const float4
 template <int WM, int WN, int BK, int NBUF>
 __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, const float* __restrict__ W,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
-                                                  float* __restrict__ C, int M, int N, int K, int epi) {
+                                                  const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
+                                                  int M, int N, int K, int epi) {
   constexpr int BM = 2 * WM, BN = 2 * WN;
   constexpr int TM = WM / 32, TN = WN / 32;          // 32x32 accumulators per wave
   constexpr int AV = BM * BK / 4 / 256;               // float4 per thread per stage (A)
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
         if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
         const size_t idx = size_t(row) * N + col;
         if (epi & EPI_RES) v += R[idx];
+        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];  // broadcast over batch
         C[idx] = v;
       }
     }
@@ -190,8 +192,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32(const float* __restrict__ A, 
 }
 
 template <int WM, int WN, int BK, int NBUF = 2>
-int launch(const float* A, const float* W, const float* bias, const float* R, float* C, int M, int N, int K, int epi,
-           hipStream_t s) {
+int launch(const float* A, const float* W, const float* bias, const float* R, const float* R2, int r2_rows, float* C,
+           int M, int N, int K, int epi, hipStream_t s) {
   constexpr int BM = 2 * WM, BN = 2 * WN;
   if (N % BN) {
     g_err = "gemm: N must be a multiple of the tile width " + std::to_string(BN);
@@ -202,7 +204,7 @@ int launch(const float* A, const float* W, const float* bias, const float* R, fl
     g_err = "gemm: K must be a multiple of the stage depth " + std::to_string(BK);
     return -1;
   }
-  hipLaunchKernelGGL((gemm_f32<WM, WN, BK, NBUF>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, C, M, N, K, epi);
+  hipLaunchKernelGGL((gemm_f32<WM, WN, BK, NBUF>), dim3(tiles), dim3(256), 0, s, A, W, bias, R, R2, r2_rows, C, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("gemm_f32: ") + hipGetErrorString(e);
@@ -233,29 +235,31 @@ int nos_gemm_tile(int cfg, int* bm, int* bn, int* bk) {
 }
 
 // C[M,N] = A[M,K] · W[N,K]^T, epilogue flags: 1 = + bias[N], 2 = exact GELU (after bias),
-// 4 = + R[M,N] (after GELU). K % 32 == 0, N % BN == 0; row-major contiguous operands.
-int nos_gemm_f32(const float* A, const float* W, const float* bias, const float* R, float* C, int M, int N, int K,
-                 int epi, int cfg, void* stream) {
+// 4 = + R[M,N] (after GELU), 8 = + R2[row % r2_rows, N] (a second residual broadcast over the
+// batch, e.g. YOLOS's per-layer mid position embeddings). K % 32 == 0, N % BN == 0; row-major
+// contiguous operands.
+int nos_gemm_f32(const float* A, const float* W, const float* bias, const float* R, const float* R2, int r2_rows,
+                 float* C, int M, int N, int K, int epi, int cfg, void* stream) {
   if (K % KALIGN) {
     g_err = "gemm: K must be a multiple of 32";
     return -1;
   }
-  if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R)) {
+  if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R) || ((epi & EPI_RES2) && (!R2 || r2_rows <= 0))) {
     g_err = "gemm: epilogue operand missing";
     return -1;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (cfg) {
-    case 0: return launch<32, 32, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 1: return launch<64, 32, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 2: return launch<32, 64, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 3: return launch<64, 64, 32>(A, W, bias, R, C, M, N, K, epi, s);
-    case 4: return launch<32, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
-    case 5: return launch<64, 32, 64>(A, W, bias, R, C, M, N, K, epi, s);
-    case 6: return launch<32, 64, 64>(A, W, bias, R, C, M, N, K, epi, s);
-    case 7: return launch<32, 32, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
-    case 8: return launch<64, 32, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
-    case 9: return launch<32, 64, 32, 1>(A, W, bias, R, C, M, N, K, epi, s);
+    case 0: return launch<32, 32, 32>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 1: return launch<64, 32, 32>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 2: return launch<32, 64, 32>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 3: return launch<64, 64, 32>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 4: return launch<32, 32, 64>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 5: return launch<64, 32, 64>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 6: return launch<32, 64, 64>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 7: return launch<32, 32, 32, 1>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 8: return launch<64, 32, 32, 1>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
+    case 9: return launch<32, 64, 32, 1>(A, W, bias, R, R2, r2_rows, C, M, N, K, epi, s);
     default:
       g_err = "gemm: unknown tile config";
       return -1;

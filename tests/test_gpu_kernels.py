@@ -172,3 +172,35 @@ def test_yolos_hip_matches_torch_backend(K):
     torch.cuda.synchronize()
     assert (l - ref_l).abs().max().item() < 1e-3
     assert (bx - ref_b).abs().max().item() < 1e-4
+
+
+def test_gemm_second_residual_broadcast_and_out_view(K):
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(3)
+    T, N, Kd = 300, 128, 64
+    x = torch.randn(2 * T, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.1
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(2 * T, N, device="cuda")
+    r2 = torch.randn(1, T, N, device="cuda")
+    ref = x.double() @ w.double().t() + b.double() + r.double() + r2.double().repeat(2, 1, 1).reshape(2 * T, N)
+    for cfg in G.eligible(2 * T, N, Kd):
+        buf = torch.zeros(2 * T + 7, N, device="cuda")
+        out = G.gemm(x, w, b, residual=r, residual2=r2, tile=cfg, out=buf[3:3 + 2 * T])
+        torch.cuda.synchronize()
+        assert (out.double() - ref).abs().max().item() < 1e-3, cfg
+        assert buf[:3].abs().max().item() == 0 and buf[-4:].abs().max().item() == 0  # no stray writes
+
+
+def test_patch_embed_matches_conv(K):
+    torch.manual_seed(4)
+    px = torch.randn(1, 3, 800, 1066, device="cuda")
+    w = torch.randn(384, 3, 16, 16, device="cuda") * 0.02
+    b = torch.randn(384, device="cuda")
+    pos = torch.randn(50 * 66, 384, device="cuda")
+    out = K.patch_embed(px, w, b, 16, pos)
+    ref = torch.nn.functional.conv2d(px.double(), w.double(), b.double(), stride=16).flatten(2).transpose(1, 2) \
+        + pos.double()
+    torch.cuda.synchronize()
+    assert out.shape == (1, 3300, 384)
+    assert (out.double() - ref).abs().max().item() < 1e-3

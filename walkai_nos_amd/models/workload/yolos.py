@@ -69,7 +69,7 @@ class _Block(nn.Module):
         self.fc1 = nn.Linear(d, f)
         self.fc2 = nn.Linear(f, d)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, mid: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, T, D = x.shape
         H, Dh = self.c.num_heads, self.c.head_dim
         h = K.layernorm(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
@@ -78,7 +78,7 @@ class _Block(nn.Module):
         x = K.linear_residual(o, self.proj.weight, self.proj.bias, x)      # x + o @ Wp^T + bp
         h = K.layernorm(x, self.ln2.weight, self.ln2.bias, self.c.layer_norm_eps)
         h = K.linear_gelu(h, self.fc1.weight, self.fc1.bias)               # gelu(h @ W1^T + b1)
-        return K.linear_residual(h, self.fc2.weight, self.fc2.bias, x)
+        return K.linear_residual(h, self.fc2.weight, self.fc2.bias, x, mid)   # (+ mid pos-embed, fused)
 
 
 class _MLPHead(nn.Module):
@@ -156,13 +156,21 @@ class YolosSmall(nn.Module):
     # -- forward -------------------------------------------------------------------------
     def forward(self, pixels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         B, _, Hh, Ww = pixels.shape
-        x = self.patch(pixels).flatten(2).transpose(1, 2)                   # [B, P, D]
         pe, mid = self.position_embeddings((Hh, Ww))
-        x = torch.cat((self.cls_token.expand(B, -1, -1), x, self.det_tokens.expand(B, -1, -1)), dim=1) + pe
+        nd = self.c.num_detection_tokens
+        if B == 1 and pixels.is_cuda and K.get_backend() == "hip":
+            # patch rows written straight into the token buffer by the GEMM (bias + pos fused)
+            P = (Hh // self.c.patch_size) * (Ww // self.c.patch_size)
+            x = torch.empty(1, 1 + P + nd, self.c.hidden_size, device=pixels.device, dtype=pixels.dtype)
+            K.patch_embed(pixels, self.patch.weight, self.patch.bias, self.c.patch_size, pe[0, 1:1 + P],
+                          out=x[0, 1:1 + P])
+            x[:, :1] = self.cls_token + pe[:, :1]
+            x[:, 1 + P:] = self.det_tokens + pe[:, 1 + P:]
+        else:
+            xp = K.patch_embed(pixels, self.patch.weight, self.patch.bias, self.c.patch_size)   # [B, P, D]
+            x = torch.cat((self.cls_token.expand(B, -1, -1), xp, self.det_tokens.expand(B, -1, -1)), dim=1) + pe
         for i, blk in enumerate(self.blocks):
-            x = blk(x)
-            if mid is not None and i < self.c.num_layers - 1:
-                x = x + mid[i]
+            x = blk(x, mid[i] if mid is not None and i < self.c.num_layers - 1 else None)
         det = x[:, -self.c.num_detection_tokens:, :]
         det = K.layernorm(det.contiguous(), self.ln_f.weight, self.ln_f.bias, self.c.layer_norm_eps)
         return self.cls_head(det), torch.sigmoid(self.box_head(det))

@@ -19,7 +19,7 @@ import torch
 
 from . import kernels as K
 
-EPI_BIAS, EPI_GELU, EPI_RES = 1, 2, 4
+EPI_BIAS, EPI_GELU, EPI_RES, EPI_RES2 = 1, 2, 4, 8
 #: config -> (BM, BN, BK): workgroup tile and stage depth
 TILES = {0: (64, 64, 32), 1: (128, 64, 32), 2: (64, 128, 32), 3: (128, 128, 32),
          4: (64, 64, 64), 5: (128, 64, 64), 6: (64, 128, 64),
@@ -38,7 +38,7 @@ def _lib() -> ctypes.CDLL:
     L = K._L()
     if not _bound:
         vp, i32 = ctypes.c_void_p, ctypes.c_int
-        L.nos_gemm_f32.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]
+        L.nos_gemm_f32.argtypes = [vp, vp, vp, vp, vp, i32, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_last_error.restype = ctypes.c_char_p
         _bound = True
     return L
@@ -67,17 +67,23 @@ def heuristic(M: int, N: int, cus: int, cands: list) -> int:
 
 
 def _launch(cfg: int, x2: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], res2: Optional[torch.Tensor],
-            out: torch.Tensor, epi: int) -> None:
+            out: torch.Tensor, epi: int, r2: Optional[torch.Tensor] = None) -> None:
     M, Kd = x2.shape
     N = w.shape[0]
     rc = _lib().nos_gemm_f32(x2.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
-                             res2.data_ptr() if res2 is not None else None, out.data_ptr(), M, N, Kd, epi, cfg,
-                             torch.cuda.current_stream().cuda_stream)
+                             res2.data_ptr() if res2 is not None else None,
+                             r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+                             out.data_ptr(), M, N, Kd, epi, cfg, torch.cuda.current_stream().cuda_stream)
     if rc != 0:
         raise RuntimeError(f"nos gemm failed: {_lib().nos_gemm_last_error().decode()} (rc={rc})")
 
 
-def _library(x2, w, bias, res2, out, epi) -> None:
+def _library(x2, w, bias, res2, out, epi, r2=None) -> None:
+    if epi & EPI_RES2:
+        _library(x2, w, bias, res2, out, epi & ~EPI_RES2)
+        M = out.shape[0]
+        out.view(-1, r2.shape[0], out.shape[1]).add_(r2) if M % r2.shape[0] == 0 else out.add_(r2[:M])
+        return
     if epi & EPI_RES:
         c = res2 + bias if bias is not None else res2
         torch.addmm(c, x2, w.t(), out=out)
@@ -121,12 +127,12 @@ def _gpu_time(fn, stream, reps: int = 3) -> float:
     return st.elapsed_time(en)
 
 
-def _tune(key, cands, x2, w, bias, res2, out, epi) -> int:
+def _tune(key, cands, x2, w, bias, res2, out, epi, r2=None) -> int:
     stream = torch.cuda.current_stream()
     timings = {}
     for c in cands + [LIBRARY]:
-        fn = (lambda c=c: _library(x2, w, bias, res2, out, epi)) if c == LIBRARY else \
-            (lambda c=c: _launch(c, x2, w, bias, res2, out, epi))
+        fn = (lambda c=c: _library(x2, w, bias, res2, out, epi, r2)) if c == LIBRARY else \
+            (lambda c=c: _launch(c, x2, w, bias, res2, out, epi, r2))
         timings[c] = _gpu_time(fn, stream)
     best = min(timings, key=timings.get)
     with _lock:
@@ -140,19 +146,32 @@ def choose(M: int, N: int, Kd: int, epi: int, cus: int) -> Optional[int]:
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
-         residual: Optional[torch.Tensor] = None, tile: Optional[int] = None) -> torch.Tensor:
-    """``x @ w^T (+bias) (GELU) (+residual)`` for fp32 CUDA tensors; ``tile`` forces a config."""
+         residual: Optional[torch.Tensor] = None, tile: Optional[int] = None,
+         residual2: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x @ w^T (+bias) (GELU) (+residual) (+residual2)`` for fp32 CUDA tensors.
+
+    ``residual2`` is ``[R, N]`` (or ``[1, R, N]``) broadcast over the batch by row index modulo R;
+    ``out`` (contiguous ``[..., N]`` with ``M`` rows) receives the result in place; ``tile`` forces
+    a config."""
     shp = x.shape
     x2 = x.reshape(-1, shp[-1]).contiguous()
     M, Kd = x2.shape
     N = w.shape[0]
-    out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if out is None:
+        out2 = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    else:
+        if not out.is_contiguous() or out.numel() != M * N:
+            raise ValueError("gemm: out must be contiguous with M x N elements")
+        out2 = out.view(M, N)
     res2 = residual.reshape(M, N).contiguous() if residual is not None else None
-    epi = (EPI_BIAS if bias is not None else 0) | (EPI_GELU if gelu else 0) | (EPI_RES if residual is not None else 0)
+    r2 = residual2.reshape(-1, N).contiguous() if residual2 is not None else None
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_GELU if gelu else 0) | (EPI_RES if residual is not None else 0) \
+        | (EPI_RES2 if residual2 is not None else 0)
     cands = eligible(M, N, Kd)
+    result = out2.view(*shp[:-1], N) if out is None else out
     if tile is not None:
-        _launch(tile, x2, w.contiguous(), bias, res2, out, epi)
-        return out.view(*shp[:-1], N)
+        _launch(tile, x2, w.contiguous(), bias, res2, out2, epi, r2)
+        return result
     cus = K.slice_cus()
     key = (M, N, Kd, epi, cus)
     cfg = choose(*key)
@@ -162,12 +181,12 @@ def gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, 
         elif torch.cuda.is_current_stream_capturing():
             cfg = heuristic(M, N, cus, cands)
         else:
-            cfg = _tune(key, cands, x2, w.contiguous(), bias, res2, out, epi)
+            cfg = _tune(key, cands, x2, w.contiguous(), bias, res2, out2, epi, r2)
     if cfg == LIBRARY:
-        _library(x2, w, bias, res2, out, epi)
+        _library(x2, w, bias, res2, out2, epi, r2)
     else:
-        _launch(cfg, x2, w.contiguous(), bias, res2, out, epi)
-    return out.view(*shp[:-1], N)
+        _launch(cfg, x2, w.contiguous(), bias, res2, out2, epi, r2)
+    return result
 
 
 def tuning_table() -> Dict[str, str]:

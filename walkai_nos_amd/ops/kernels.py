@@ -173,12 +173,32 @@ def linear_gelu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tens
     return gemm(x, w, b, gelu=True)
 
 
-def linear_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
-    """``res + x @ w^T + b`` with bias and residual fused into the GEMM's store."""
+def linear_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, res: torch.Tensor,
+                    res2: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``res + x @ w^T + b (+ res2)`` with bias and residual(s) fused into the GEMM's store;
+    ``res2`` ([T, N], broadcast over the batch) is YOLOS's per-layer mid position embedding."""
     if not _use_hip(x) or x.dtype != torch.float32:
-        return res + F.linear(x, w, b)
+        y = res + F.linear(x, w, b)
+        return y + res2 if res2 is not None else y
     from .gemm import gemm
-    return gemm(x, w, b, residual=res)
+    return gemm(x, w, b, residual=res, residual2=res2)
+
+
+def patch_embed(pixels: torch.Tensor, w: torch.Tensor, b: torch.Tensor, patch: int,
+                pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Non-overlapping patch embedding (a stride-``patch`` conv) as one unfold copy + the MFMA GEMM,
+    with the bias and the patch position embeddings (``pos``: [P, D]) fused into the store.
+    Returns [B, P, D]; written into ``out`` ([B*P, D] contiguous) when given."""
+    B, C, Hh, Ww = pixels.shape
+    gh, gw = Hh // patch, Ww // patch
+    if not _use_hip(pixels) or pixels.dtype != torch.float32:
+        y = F.conv2d(pixels, w, b, stride=patch).flatten(2).transpose(1, 2)
+        return y + pos if pos is not None else y
+    cols = pixels[:, :, :gh * patch, :gw * patch].reshape(B, C, gh, patch, gw, patch) \
+        .permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * patch * patch)
+    from .gemm import gemm
+    y = gemm(cols, w.reshape(w.shape[0], -1), b, residual2=pos, out=out)
+    return y.view(B, gh * gw, -1)
 
 
 def attention_ref(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
