@@ -151,3 +151,32 @@ def test_spec_annotations_sum_per_gpu_profile():
     from walkai_nos_amd.partitioning.state import GPUPartitioning, NodePartitioning
     np_ = NodePartitioning([GPUPartitioning(0, {"amd.com/cpx_nps1": 8}), GPUPartitioning(1, {"amd.com/gpu-8cu.4gb": 2})])
     assert spec_annotations(np_) == {"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", "nos.nebuly.com/spec-gpu-1-8cu.4gb": "2"}
+
+
+def test_simulate_policy_picks_the_plan_that_schedules_most_pods():
+    from walkai_nos_amd.controllers.partitioner.pod_controller import (plan_cluster_simulate, planned_state,
+                                                                       simulate_schedule)
+    api_ = InMemoryAPIServer()
+    api_.create(xnode("a", gpus=1, anns={"nos.nebuly.com/status-gpu-0-spx_nps1-free": "1"}))
+    models = {"a": xcp_node.new_node(api_.get("Node", "a"))}
+    pending = [{"spx_nps1": 1}] + [{"cpx_nps1": 1}] * 6
+    # FIFO serves the head-of-line whole-GPU pod (1 pod scheduled) ...
+    fifo = plan_cluster_fifo(models, pending)
+    assert simulate_schedule(planned_state(models, fifo), pending)[0] == 1
+    # ... the simulation planner picks the CPX layout that schedules 6 of them
+    sim = plan_cluster_simulate(models, pending)
+    assert sim["a"].gpus[0].geometry() == {"cpx_nps1": 8}
+    assert simulate_schedule(planned_state(models, sim), pending) == (6, 0.75)
+
+
+def test_simulate_policy_end_to_end_on_the_in_memory_cluster():
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=2, policy="simulate")
+    c.run(30)
+    for i in range(10):
+        c.submit({"amd.com/cpx_nps1": 1}, name=f"c{i}")
+    c.submit({"amd.com/dpx_nps1": 1}, name="d0")
+    c.run(120)
+    # partitions are homogeneous per GPU: 10 x 1/8 + 1 x 1/2 cannot all fit on 2 GPUs; the
+    # simulation keeps the layout that runs the most pods (both GPUs CPX)
+    assert len(c.running_pods()) == 10 and [ko.name(p) for p in c.pending_pods()] == ["d0"]

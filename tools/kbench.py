@@ -52,7 +52,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="gpurun_out/kbench.json")
-    ap.add_argument("--only", choices=("all", "attn", "gemm"), default="all")
+    ap.add_argument("--only", choices=("all", "attn", "gemm", "model"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     a = ap.parse_args()
     torch.manual_seed(0)
@@ -81,6 +81,8 @@ def main() -> int:
                 attn_bench(r, qkv, out, q, k, v, n, s, a.iters, attn_flops)
             if a.only in ("all", "gemm"):
                 gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, a.iters)
+            if a.only in ("all", "model"):
+                model_bench(r, s, max(3, a.iters // 4))
             r["layernorm_us"] = round(timeit(lambda: K.layernorm(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
             for kname in list(r):
                 if isinstance(r[kname], float):
@@ -107,6 +109,19 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
     r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, iters)
     for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")]:
         r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
+
+
+def model_bench(r, s, iters):
+    """One whole YOLOS-small inference (batch 1) on this slice, graph-replayed."""
+    from walkai_nos_amd.models.workload.yolos import DEMO_INPUT_HW, YolosSmall, demo_input
+    with torch.cuda.stream(s):
+        m = YolosSmall().cuda().eval()
+        xin = demo_input(1, DEMO_INPUT_HW, "cuda")
+    with torch.no_grad():
+        us = timeit(lambda: m(xin), s, iters)
+    r["model_ms"] = round(us / 1000.0, 3)
+    r["model_tflops"] = round(m.flops_per_inference() / us / 1e6, 2)
+    r["model_inf_per_s_per_gpu"] = round(1e6 / us * 256 / r["cus"], 1)
 
 
 def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):

@@ -80,8 +80,8 @@ class GpuPartitionerConfig(ManagerConfig):
             raise ValueError("batchWindowIdleSeconds must be greater than 0")
         if self.devicePluginDelaySeconds <= 0:
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
-        if self.planningPolicy not in ("fifo", "batch"):
-            raise ValueError("planningPolicy must be 'fifo' or 'batch'")
+        if self.planningPolicy not in ("fifo", "batch", "simulate"):
+            raise ValueError("planningPolicy must be 'fifo', 'batch' or 'simulate'")
         if self.scoring not in ("fraction", "pods"):
             raise ValueError("scoring must be 'fraction' or 'pods'")
 

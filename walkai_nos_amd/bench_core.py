@@ -59,6 +59,7 @@ class BenchConfig:
     preroll: int = 20                   # control-plane-only epochs before warmup (steady state)
     rank: int = 0
     world: int = 1
+    policy: str = "fifo"                # planner policy (fifo | batch | simulate)
 
 
 class ChurnProcess:
@@ -187,7 +188,7 @@ class NodeBench:
         from .sim.cluster import SimCluster
 
         self.cfg = cfg
-        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0)
+        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
         if barrier_factory is not None:
             for sn in self.cluster.nodes.values():
                 self._set_barrier(sn, barrier_factory)

@@ -142,6 +142,70 @@ def plan_cluster_fifo(models: Mapping[str, NodeModel], pending: List[Dict[str, i
     return changed
 
 
+def simulate_schedule(models: Mapping[str, NodeModel], pending: List[Dict[str, int]]) -> Tuple[int, float]:
+    """Pods (and GPU fraction) a first-fit scheduler would place, in arrival order, on ``models``."""
+    sim = {n: m.clone() for n, m in models.items()}
+    pods, frac = 0, 0.0
+    for req in pending:
+        for name in sorted(sim):
+            try:
+                sim[name].add_pod(req)
+            except ValueError:
+                continue
+            pods += 1
+            w = getattr(sim[name], "weight", None)
+            frac += sum(q * (w(p) if w is not None else 1.0) for p, q in req.items())
+            break
+    return pods, frac
+
+
+def materialize(orig: NodeModel, planned: NodeModel) -> NodeModel:
+    """The planned geometry on the original occupancy (planners leave their own tentative
+    reservations in the models they return; a simulation must start from real usage)."""
+    out = orig.clone()
+    for g_out, g_plan in zip(out.gpus, planned.gpus):
+        geo = g_plan.geometry()
+        g_out.free = {p: q - g_out.used.get(p, 0) for p, q in geo.items() if q - g_out.used.get(p, 0) > 0}
+    return out
+
+
+def planned_state(models: Mapping[str, NodeModel], changed: Mapping[str, NodeModel]) -> Dict[str, NodeModel]:
+    return {n: (materialize(m, changed[n]) if n in changed else m) for n, m in models.items()}
+
+
+def plan_cluster_simulate(models: Mapping[str, NodeModel], pending: List[Dict[str, int]],
+                          incoming: Optional[Mapping[str, int]] = None) -> Dict[str, NodeModel]:
+    """Scheduler-simulation planner (reference docs ``dynamic-gpu-partitioning/configuration.md:6-40``:
+    "choose the partitioning that schedules the highest number of pending pods").
+
+    Candidate plans: FIFO head-of-line, the whole-batch search, and FIFO over the queue re-ordered
+    smallest-first and largest-first. Each candidate's resulting cluster is scheduled by a first-fit
+    simulation of the pending queue; the winner schedules the most pods, then the most GPU fraction,
+    then changes the fewest GPUs."""
+    total: Dict[str, int] = {}
+    for req in pending:
+        for p, q in req.items():
+            total[p] = total.get(p, 0) + q
+
+    def size(req: Dict[str, int]) -> float:
+        m = next(iter(models.values()), None)
+        w = getattr(m, "weight", None) if m is not None else None
+        return sum(q * (w(p) if w is not None else 1.0) for p, q in req.items())
+
+    candidates = [plan_cluster_fifo(models, pending, incoming), plan_cluster(models, total),
+                  plan_cluster_fifo(models, sorted(pending, key=size), incoming),
+                  plan_cluster_fifo(models, sorted(pending, key=size, reverse=True), incoming)]
+    best: Optional[Tuple[Tuple[int, float, int], Dict[str, NodeModel]]] = None
+    for changed in candidates:
+        final = planned_state(models, changed)
+        pods, frac = simulate_schedule(final, pending)
+        churn = sum(_changed_gpus(models[n], c) for n, c in changed.items())
+        key = (-pods, -frac, churn)
+        if best is None or key < best[0]:
+            best = (key, changed)
+    return best[1] if best is not None else {}
+
+
 class PodController:
     def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
                  clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
@@ -149,7 +213,7 @@ class PodController:
         self.client = client
         self.kind = kind
         self.scoring = scoring
-        if policy not in ("fifo", "batch"):
+        if policy not in ("fifo", "batch", "simulate"):
             raise ValueError(f"unknown planning policy {policy!r}")
         self.policy = policy
         self.partitioner = partitioner or Partitioner(client)
@@ -284,12 +348,13 @@ class PodController:
             if flying:
                 return Result(requeue_after=self.retry_after)
             return Result()
-        if self.policy == "fifo":
+        if self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}
             for n in flying:
                 for p, q in self.incoming_free(n).items():
                     incoming[p] = incoming.get(p, 0) + q
-            changed = plan_cluster_fifo(models, self.pending_pods() or [requested], incoming)
+            planner = plan_cluster_fifo if self.policy == "fifo" else plan_cluster_simulate
+            changed = planner(models, self.pending_pods() or [requested], incoming)
             need = requested
         else:
             pending = self.pending_requests() or requested
