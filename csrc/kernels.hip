@@ -569,11 +569,299 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   }
 }
 
+// ---- fp32 as three bf16 planes ("x3") ----------------------------------------------------------
+// gfx950 has no xf32 and runs f32-input MFMA at 1/16 of the bf16 rate. An fp32 value splits
+// exactly into three bf16 terms, x = x0 + x1 + x2 (each residual of a round-to-nearest bf16
+// conversion is exact in f32 and carries the next 8 mantissa bits), so a product a·b of two fp32
+// operands is a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0 up to terms of relative size 2^-24 — the
+// fp32 rounding level. Six bf16 MFMAs (32x32x16, 32 cycles each) replace eight f32 MFMAs
+// (32x32x2, 64 cycles each) per 32x32x16 block: 2.67x fewer matrix-pipe cycles at fp32 accuracy.
+// The small products are accumulated first so the running sum absorbs them at fp32 rounding.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename F, typename H>
+__device__ __forceinline__ void split3(const F& x, H& a, H& b, H& c) {
+  a = __builtin_convertvector(x, H);  // v_cvt_pk_bf16_f32: round to nearest even
+  const F r = x - __builtin_convertvector(a, F);
+  b = __builtin_convertvector(r, H);
+  c = __builtin_convertvector(r - __builtin_convertvector(b, F), H);
+}
+
+// D += A·B with A, B given as three bf16 planes each (6 MFMAs, small terms first)
+__device__ __forceinline__ f32x16 mfma_x3(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
+                                          const bf16x8& b1, const bf16x8& b2, f32x16 d) {
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, d, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, d, 0, 0, 0);
+}
+
+// fp32 [n] -> bf16 planes [3][n] (plane stride n); 4 elements per thread
+__global__ __launch_bounds__(256) void split3_f32(const float* __restrict__ x, __bf16* __restrict__ y, size_t n4) {
+  const size_t stride = size_t(gridDim.x) * 256;
+  for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
+    bf16x4 p0, p1, p2;
+    split3(v, p0, p1, p2);
+    reinterpret_cast<bf16x4*>(y)[i] = p0;
+    reinterpret_cast<bf16x4*>(y)[n4 + i] = p1;
+    reinterpret_cast<bf16x4*>(y)[2 * n4 + i] = p2;
+  }
+}
+
+// Stream-K flash attention on x3 planes of the packed QKV tensor: the same (128-query group x
+// 32-key block) units, persistent grid, XCD-major order and partial-segment workspace as
+// attn_fwd_sk_lds (so attn_sk_lds_fixup merges its partials), with every product on
+// v_mfma_f32_32x32x16_bf16:
+//  * S^T = K·Q^T: lane (j, h) holds Q[q0+j][16s+8h .. +7] per plane (12 x 16-B loads per segment,
+//    kept in registers); K fragments are ds_read_b128 row reads of a [plane][key][72] bf16 image
+//    (144-B rows: 9r mod 16 is a bijection on every ds_read_b128 lane group — conflict-free);
+//  * softmax on the S^T accumulator (one query per lane, keys in registers) as in the f32 kernel,
+//    the log2e/sqrt(d) scale applied inside the exp2's fma;
+//  * P^T is split into planes in registers and used as the B operand of O^T += V^T·P^T straight
+//    from the accumulator (registers 8s..8s+7 = k-step s, key 16s + 8(e>>2) + 4h + (e&3) in
+//    element e); the matching V^T fragments come from a row-major [plane][key][96] V image through
+//    ds_read_b64_tr_b16 (two 4-key transposed reads per fragment; 192-B rows put the four rows of a
+//    read group at bank offsets 0/48/32/16 — conflict-free);
+//  * K and V blocks arrive as coalesced 16-B loads of pre-split planes (the producer splits once;
+//    every query group re-reads them), register-prefetched one block ahead, double-buffered.
+constexpr int XK_STR = 72, XV_STR = 96;
+constexpr int XK_PLANE = 32 * XK_STR, XV_PLANE = 32 * XV_STR;
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__ qkv3, size_t plane,
+                                                      float* __restrict__ out, float* __restrict__ part_o,
+                                                      float* __restrict__ part_ml, int B, int T, int H,
+                                                      float scale_log2e, int P) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
+  __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
+  const int w = sk_logical(blockIdx.x, P);
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const long long U = (long long)B * H * QG * NK;
+  long long u = sk_begin(w, U, P);
+  const long long u1 = sk_begin(w + 1, U, P);
+  const int D = H * HD, ld = 3 * D;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int j = lane & 31, hf = lane >> 5;
+  // loader: 16-B chunk (8 bf16) per plane: key row tid/8, dims 8*(tid%8)
+  const int lrow = tid >> 3, lch = tid & 7;
+  // transposed-read lane address inside a plane image: group g = lane/16 (h = g/2, column block
+  // 16*(g&1)), lane i = lane%16 supplies row 4h + i/4, columns 4*(i%4)
+  const int gi = lane & 15, gg = lane >> 4;
+  const int vtr = (4 * hf + (gi >> 2)) * XV_STR + 16 * (gg & 1) + 4 * (gi & 3);
+  bool first = true;
+  while (u < u1) {
+    const long long grp = u / NK;
+    const int kb0 = int(u - grp * NK);
+    const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
+    const int qg = int(grp % QG);
+    const int head = int((grp / QG) % H);
+    const int b = int(grp / ((long long)QG * H));
+    const __bf16* base = qkv3 + size_t(b) * T * ld;
+    const int qt = qg * 4 + wv;
+    const bool active = qt < QT;
+    const int q0 = qt * 32;
+
+    bf16x8 qf[3][4];
+    {
+      const int qrow = min(q0 + j, T - 1);
+      const __bf16* qp = base + size_t(qrow) * ld + head * HD + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[p][s] = *reinterpret_cast<const bf16x8*>(qp + p * plane + 16 * s);
+    }
+    const __bf16* kg = base + D + head * HD + 8 * lch;
+    const __bf16* vg = base + 2 * D + head * HD + 8 * lch;
+    // one block = 32 key rows x 128 B per plane of K and of V: one 16-B chunk per thread each
+    uint4 pk0, pk1, pk2, pv0, pv1, pv2;
+    auto fetch = [&](int blk) {
+      const size_t r = size_t(min(blk * 32 + lrow, T - 1)) * ld;
+      pk0 = *reinterpret_cast<const uint4*>(kg + r);
+      pk1 = *reinterpret_cast<const uint4*>(kg + plane + r);
+      pk2 = *reinterpret_cast<const uint4*>(kg + 2 * plane + r);
+      pv0 = *reinterpret_cast<const uint4*>(vg + r);
+      pv1 = *reinterpret_cast<const uint4*>(vg + plane + r);
+      pv2 = *reinterpret_cast<const uint4*>(vg + 2 * plane + r);
+    };
+    auto stash = [&](int buf) {
+      __bf16* kd = &lds_k[buf * 3 * XK_PLANE + lrow * XK_STR + 8 * lch];
+      __bf16* vd = &lds_v[buf * 3 * XV_PLANE + lrow * XV_STR + 8 * lch];
+      *reinterpret_cast<uint4*>(kd) = pk0;
+      *reinterpret_cast<uint4*>(kd + XK_PLANE) = pk1;
+      *reinterpret_cast<uint4*>(kd + 2 * XK_PLANE) = pk2;
+      *reinterpret_cast<uint4*>(vd) = pv0;
+      *reinterpret_cast<uint4*>(vd + XV_PLANE) = pv1;
+      *reinterpret_cast<uint4*>(vd + 2 * XV_PLANE) = pv2;
+    };
+    __syncthreads();  // the previous segment's last block is no longer being read
+    fetch(kb0);
+    stash(0);
+    __syncthreads();
+
+    f32x16 o0 = {0}, o1 = {0};
+    float m = -INFINITY, l = 0.f;
+    for (int blk = kb0; blk < kb1; ++blk) {
+      const int buf = (blk - kb0) & 1;
+      const bool more = blk + 1 < kb1;
+      if (more) fetch(blk + 1);
+      if (active) {
+        const __bf16* ks = &lds_k[buf * 3 * XK_PLANE + j * XK_STR + 8 * hf];
+        f32x16 sacc = {0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ks + 16 * s);
+          const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ks + XK_PLANE + 16 * s);
+          const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(ks + 2 * XK_PLANE + 16 * s);
+          sacc = mfma_x3(k0, k1, k2, qf[0][s], qf[1][s], qf[2][s], sacc);
+        }
+        const int kb = blk * 32;
+        if (kb + 32 > T) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kb + key_of(r, hf) >= T) sacc[r] = -INFINITY;
+        }
+        float mx = sacc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float m_new = fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);
+        const float mc = m_new * scale_log2e;
+        float psum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          sacc[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], scale_log2e, -mc));
+          psum += sacc[r];
+        }
+        psum += __shfl_xor(psum, 32, 64);
+        l = l * alpha + psum;
+        m = m_new;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          o0[r] *= alpha;
+          o1[r] *= alpha;
+        }
+        const __bf16* vs = &lds_v[buf * 3 * XV_PLANE + vtr];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const f32x8 pv8 = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
+                             sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
+          bf16x8 p0, p1, p2;
+          split3(pv8, p0, p1, p2);
+#pragma unroll
+          for (int dh = 0; dh < 2; ++dh) {
+            bf16x8 vf[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              const __bf16* a = vs + p * XV_PLANE + 16 * s2 * XV_STR + 32 * dh;
+              const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
+              const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 8 * XV_STR));
+              vf[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+            if (dh == 0)
+              o0 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o0);
+            else
+              o1 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o1);
+          }
+        }
+      }
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+    }
+
+    if (active) {
+      if (kb0 == 0 && kb1 == NK) {
+        const int q = q0 + j;
+        if (q < T) {
+          const float inv = 1.f / l;
+          float* orow = out + (size_t(b) * T + q) * D + head * HD;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int d = key_of(r, hf);
+            orow[d] = o0[r] * inv;
+            orow[32 + d] = o1[r] * inv;
+          }
+        }
+      } else {
+        const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * 4 + wv;
+        float* po = part_o + slot * (HD * 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = key_of(r, hf);
+          po[d * 32 + j] = o0[r];
+          po[(32 + d) * 32 + j] = o1[r];
+        }
+        if (hf == 0) {
+          part_ml[slot * 64 + j] = m * scale_log2e;
+          part_ml[slot * 64 + 32 + j] = l;
+        }
+      }
+    }
+    u += kb1 - kb0;
+    first = false;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* nos_kernels_last_error() { return g_err.c_str(); }
+
+// fp32 [n] -> three bf16 planes [3][n]; n % 4 == 0
+int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
+  if (n % 4) {
+    g_err = "split3: n must be a multiple of 4";
+    return -1;
+  }
+  const size_t n4 = n / 4;
+  const int grid = int(std::min<size_t>((n4 + 255) / 256, 4096));
+  hipLaunchKernelGGL(split3_f32, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x,
+                     reinterpret_cast<__bf16*>(planes), n4);
+  return check_launch("split3_f32");
+}
+
+// workgroups per CU of the x3 attention kernel (persistent grid = this x slice CUs)
+int nos_attention_x3_wg_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3, 256, 0) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
+// Stream-K attention over x3 planes of a packed [B, T, 3*H*64] QKV tensor (plane stride
+// `plane_stride` elements); output fp32 [B, T, H*64]. Workspace: nos_attention_ws_bytes of the
+// LDS variant (variant 0 layout), merged by the same fixup kernel.
+int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, float* ws, int B, int T, int H,
+                        int head_dim, float scale, int waves, void* stream) {
+  if (head_dim != HD) {
+    g_err = "attention x3: head_dim must be 64";
+    return -1;
+  }
+  if (ws == nullptr || waves <= 0) {
+    g_err = "attention x3: needs waves > 0 and a workspace";
+    return -1;
+  }
+  if (plane_stride % 8) {
+    g_err = "attention x3: plane stride must be a multiple of 8 elements (16-B aligned planes)";
+    return -1;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int NK = (T + 31) / 32, QG = (NK + 3) / 4;
+  float* part_o = ws;
+  float* part_ml = ws + size_t(waves) * 8 * HD * 32;
+  hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3), plane_stride,
+                     out, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+  if (int rc = check_launch("attn_fwd_x3")) return rc;
+  hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves);
+  return check_launch("attn_sk_lds_fixup");
+}
 
 int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, int rows, int D, float eps,
                       void* stream) {

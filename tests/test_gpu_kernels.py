@@ -204,3 +204,47 @@ def test_patch_embed_matches_conv(K):
     torch.cuda.synchronize()
     assert out.shape == (1, 3300, 384)
     assert (out.double() - ref).abs().max().item() < 1e-3
+
+
+def test_split3_is_exact(K):
+    torch.manual_seed(5)
+    x = torch.randn(1 << 16, device="cuda") * torch.logspace(-20, 20, 1 << 16, device="cuda")
+    p = K.split3(x)
+    assert p.dtype == torch.bfloat16 and p.shape == (3,) + x.shape
+    recon = p[0].double() + p[1].double() + p[2].double()
+    assert torch.equal(recon, x.double())
+    # the GPU split is the CPU reference split bit for bit
+    assert torch.equal(p.cpu(), K.split3(x.cpu()))
+
+
+@pytest.mark.parametrize("T,H,B", [(1000, 2, 1), (3401, 6, 1), (77, 1, 2)])
+def test_attention_x3_fp32_accurate_any_grid(K, T, H, B):
+    # the x3 path must be as accurate as the f32-input MFMA path (both vs fp64), for every
+    # stream-K partial-segment pattern
+    torch.manual_seed(1)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    planes = K.split3(qkv)
+    units = B * H * (((T + 31) // 32 + 3) // 4) * ((T + 31) // 32)
+    f32 = torch.empty(B, T, H * 64, device="cuda")
+    K.attention_sk(qkv, f32, H, 64, 0.125, 256)
+    torch.cuda.synchronize()
+    err_f32 = (f32 - ref).abs().max().item()
+    for waves in (1, 3, 7, 64, 333, 512, units + 5):
+        out = torch.full((B, T, H * 64), float("nan"), device="cuda")
+        K.attention_x3(planes, out, H, 64, 0.125, waves)
+        torch.cuda.synchronize()
+        err = (out - ref).abs().max().item()
+        assert err < max(2.0 * err_f32, 2e-6), (waves, err, err_f32)
+
+
+def test_attention_x3_asymmetric_values(K):
+    T, H = 96, 1
+    qkv = torch.zeros(1, T, 3 * 64, device="cuda")
+    qkv[0, :, :64] = torch.randn(T, 64, device="cuda") * 4
+    qkv[0, :, 64:128] = torch.randn(T, 64, device="cuda") * 4
+    qkv[0, :, 128:] = torch.arange(T * 64, device="cuda", dtype=torch.float32).view(T, 64) / 1000
+    out = torch.empty(1, T, 64, device="cuda")
+    K.attention_x3(K.split3(qkv), out, H, 64, 0.125, 5)
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    assert (out - ref).abs().max().item() < 1e-4

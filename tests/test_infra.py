@@ -156,3 +156,12 @@ def test_bench_control_plane_and_slice_masks():
         nb.control_step()
         nb.data_step()
     assert nb.inferences > 0 and max(nb.util_samples) > 0
+
+
+def test_split3_cpu_reconstructs_exactly():
+    import torch
+
+    from walkai_nos_amd.ops import kernels as K
+    x = torch.randn(4096, dtype=torch.float32) * torch.logspace(-10, 10, 4096)
+    p = K.split3(x)
+    assert torch.equal(p[0].double() + p[1].double() + p[2].double(), x.double())

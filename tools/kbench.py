@@ -106,8 +106,16 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
     K.set_attention_variant(0)
     for mult in (1, 2):  # LDS kernel with fewer persistent workgroups per CU than resident slots
         r[f"attn_sk0g{mult}_us"] = timeit(lambda: K.attention_sk(qkv, out, H, HD, 0.125, mult * n), s, iters)
+    planes = K.split3(qkv)
+    wx = K.attention_x3_waves(n, 1, T, H)
+    r["attn_x3_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, wx), s, iters)
+    r["attn_x3_grid"] = wx
+    for mult in (1, 2):
+        r[f"attn_x3g{mult}_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, mult * n), s, iters)
+    r["split3_qkv_us"] = timeit(lambda: K.split3(qkv), s, iters)
     r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, iters)
-    for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")]:
+    for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")
+                  and not k_.startswith("split3")]:
         r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
 
 

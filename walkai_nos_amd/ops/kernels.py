@@ -78,6 +78,65 @@ def attention_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
     return per_cu * cus
 
 
+_fp32 = threading.local()
+
+
+def set_fp32_matmul(mode: str) -> None:
+    """How fp32 products run on the matrix cores: ``x3`` (default) splits each fp32 operand
+    exactly into three bf16 planes and sums the six significant cross products on the bf16 MFMA
+    (fp32-accurate: the dropped terms are 2^-24 relative, the fp32 rounding level) at 6/16 of the
+    f32-input MFMA's cycles; ``f32`` uses the f32-input MFMA (v_mfma_f32_32x32x2_f32)."""
+    if mode not in ("x3", "f32"):
+        raise ValueError(mode)
+    _fp32.mode = mode
+
+
+def get_fp32_matmul() -> str:
+    return getattr(_fp32, "mode", "x3")
+
+
+def split3(x: torch.Tensor) -> torch.Tensor:
+    """fp32 tensor -> ``[3, *x.shape]`` bf16 planes with ``x == p0 + p1 + p2`` (exact for normal
+    numbers): round-to-nearest-even bf16 of x, then of each exact f32 residual."""
+    x = x.contiguous()
+    out = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+    if not x.is_cuda:
+        r = x
+        for i in range(3):
+            out[i] = r.to(torch.bfloat16)
+            r = r - out[i].float()
+        return out
+    _check(_L().nos_split3_f32(x.data_ptr(), out.data_ptr(), x.numel(), _stream()))
+    return out
+
+
+_x3_wg: Optional[int] = None
+
+
+def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
+    """Persistent grid of the x3 attention kernel (same sizing rule as the f32 LDS kernel)."""
+    global _x3_wg
+    if _x3_wg is None:
+        _x3_wg = int(_L().nos_attention_x3_wg_per_cu())
+    per_cu = _x3_wg
+    if T:
+        nk = (T + 31) // 32
+        units = B * H * ((nk + 3) // 4) * nk
+        while per_cu > 1 and units / (per_cu * cus) < 30:
+            per_cu -= 1
+    return per_cu * cus
+
+
+def attention_x3(planes: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float,
+                 waves: int) -> torch.Tensor:
+    """Stream-K attention over the x3 planes ``[3, B, T, 3*H*64]`` of a packed QKV tensor."""
+    _, B, T, _ = planes.shape
+    ws = torch.empty(waves * 2 * (64 * 32 + 64) * 4, dtype=torch.float32, device=planes.device)
+    _check(_L().nos_attention_x3_sk(planes.data_ptr(), planes[0].numel(), out.data_ptr(), ws.data_ptr(), B, T,
+                                    heads, head_dim, scale, waves, _stream()))
+    return out
+
+
 def set_backend(name: str) -> None:
     """``hip`` (default) or ``torch`` (reference math, GPU A/B baseline only)."""
     if name not in ("hip", "torch"):
@@ -106,6 +165,8 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_ws_bytes.argtypes = [i32]
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
+            L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
+            L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             _lib = L
         return _lib
 
@@ -214,6 +275,8 @@ def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) ->
     qkv = qkv.contiguous()
     B, T, _ = qkv.shape
     out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
+    if get_fp32_matmul() == "x3":
+        return attention_x3(split3(qkv), out, heads, head_dim, scale, attention_x3_waves(slice_cus(), B, T, heads))
     return attention_sk(qkv, out, heads, head_dim, scale, attention_waves(slice_cus(), B, T, heads))
 
 
