@@ -39,12 +39,22 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// store v as three exact bf16 terms at y[i], y[plane + i], y[2*plane + i] (x3 format, see below)
+__device__ __forceinline__ void store_x3(__bf16* __restrict__ y, size_t plane, size_t i, float v) {
+  const __bf16 h0 = (__bf16)v;
+  const float r1 = v - (float)h0;
+  const __bf16 h1 = (__bf16)r1;
+  y[i] = h0;
+  y[plane + i] = h1;
+  y[2 * plane + i] = (__bf16)(r1 - (float)h1);
+}
+
 // ------------------------------------------------------------------------------------------
-// LayerNorm
+// LayerNorm (output fp32 y, or x3 planes yp with plane stride rows*D when yp != nullptr)
 template <int NPL>
 __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x, const float* __restrict__ w,
-                                                     const float* __restrict__ b, float* __restrict__ y, int rows,
-                                                     float eps) {
+                                                     const float* __restrict__ b, float* __restrict__ y,
+                                                     __bf16* __restrict__ yp, int rows, float eps) {
   constexpr int D = NPL * 64;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
@@ -65,6 +75,15 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
     q += v[i] * v[i];
   }
   const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  if (yp) {
+    const size_t plane = size_t(rows) * D;
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) {
+      const int c = i * 64 + lane;
+      store_x3(yp, plane, size_t(row) * D + c, v[i] * rstd * w[c] + b[c]);
+    }
+    return;
+  }
   float* yr = y + size_t(row) * D;
 #pragma unroll
   for (int i = 0; i < NPL; ++i) {
@@ -505,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
 // are written as 256-B runs.
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
-                                                         int B, int T, int H, int P) {
+                                                         int B, int T, int H, int P, __bf16* __restrict__ outp) {
   __shared__ float s_mmax[32], s_inv[32];
   __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
@@ -562,10 +581,15 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   __syncthreads();
   // transposed store: thread -> (query row, 64 dims), 4 rows per pass
   const int d = tid & 63;
+  const size_t plane = size_t(B) * T * D;
   for (int jq = tid >> 6; jq < 32; jq += 4) {
     const int qq = qt * 32 + jq;
     if (qq >= T) break;
-    out[(size_t(b) * T + qq) * D + head * HD + d] = s_tile[d][jq];
+    const size_t i = (size_t(b) * T + qq) * D + head * HD + d;
+    if (outp)
+      store_x3(outp, plane, i, s_tile[d][jq]);
+    else
+      out[i] = s_tile[d][jq];
   }
 }
 
@@ -636,9 +660,9 @@ constexpr int XK_STR = 72, XV_STR = 96;
 constexpr int XK_PLANE = 32 * XK_STR, XV_PLANE = 32 * XV_STR;
 
 __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__ qkv3, size_t plane,
-                                                      float* __restrict__ out, float* __restrict__ part_o,
-                                                      float* __restrict__ part_ml, int B, int T, int H,
-                                                      float scale_log2e, int P) {
+                                                      float* __restrict__ out, __bf16* __restrict__ outp,
+                                                      float* __restrict__ part_o, float* __restrict__ part_ml, int B,
+                                                      int T, int H, float scale_log2e, int P) {
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
   const int w = sk_logical(blockIdx.x, P);
@@ -781,12 +805,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
         const int q = q0 + j;
         if (q < T) {
           const float inv = 1.f / l;
-          float* orow = out + (size_t(b) * T + q) * D + head * HD;
+          const size_t orow = (size_t(b) * T + q) * D + head * HD;
+          if (outp) {
+            const size_t op = size_t(B) * T * D;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int d = key_of(r, hf);
-            orow[d] = o0[r] * inv;
-            orow[32 + d] = o1[r] * inv;
+            for (int r = 0; r < 16; ++r) {
+              const int d = key_of(r, hf);
+              store_x3(outp, op, orow + d, o0[r] * inv);
+              store_x3(outp, op, orow + 32 + d, o1[r] * inv);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int d = key_of(r, hf);
+              out[orow + d] = o0[r] * inv;
+              out[orow + 32 + d] = o1[r] * inv;
+            }
           }
         }
       } else {
@@ -836,10 +870,15 @@ int nos_attention_x3_wg_per_cu() {
 }
 
 // Stream-K attention over x3 planes of a packed [B, T, 3*H*64] QKV tensor (plane stride
-// `plane_stride` elements); output fp32 [B, T, H*64]. Workspace: nos_attention_ws_bytes of the
-// LDS variant (variant 0 layout), merged by the same fixup kernel.
-int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, float* ws, int B, int T, int H,
-                        int head_dim, float scale, int waves, void* stream) {
+// `plane_stride` elements); output fp32 [B, T, H*64] (out) or its x3 planes [3][B*T*H*64] (outp),
+// exactly one non-null. Workspace: nos_attention_ws_bytes of the LDS variant (variant 0 layout),
+// merged by the same fixup kernel.
+int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B, int T,
+                        int H, int head_dim, float scale, int waves, void* stream) {
+  if ((out == nullptr) == (outp == nullptr)) {
+    g_err = "attention x3: exactly one of out / outp";
+    return -1;
+  }
   if (head_dim != HD) {
     g_err = "attention x3: head_dim must be 64";
     return -1;
@@ -856,23 +895,31 @@ int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, float
   const int NK = (T + 31) / 32, QG = (NK + 3) / 4;
   float* part_o = ws;
   float* part_ml = ws + size_t(waves) * 8 * HD * 32;
+  __bf16* op = reinterpret_cast<__bf16*>(outp);
   hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3), plane_stride,
-                     out, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+                     out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
-  hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves);
+  hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
+                     op);
   return check_launch("attn_sk_lds_fixup");
 }
 
-int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, int rows, int D, float eps,
-                      void* stream) {
+// y (fp32) or yp (x3 planes [3][rows][D]) — exactly one of them non-null
+int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,
+                      float eps, void* stream) {
+  if ((y == nullptr) == (yp == nullptr)) {
+    g_err = "layernorm: exactly one of y / yp";
+    return -1;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const dim3 grid((rows + 3) / 4), block(256);
+  __bf16* p = reinterpret_cast<__bf16*>(yp);
   switch (D) {
-    case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, rows, eps); break;
-    case 768: hipLaunchKernelGGL(layernorm_f32<12>, grid, block, 0, s, x, w, b, y, rows, eps); break;
-    case 1024: hipLaunchKernelGGL(layernorm_f32<16>, grid, block, 0, s, x, w, b, y, rows, eps); break;
-    case 1536: hipLaunchKernelGGL(layernorm_f32<24>, grid, block, 0, s, x, w, b, y, rows, eps); break;
-    case 2048: hipLaunchKernelGGL(layernorm_f32<32>, grid, block, 0, s, x, w, b, y, rows, eps); break;
+    case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
+    case 768: hipLaunchKernelGGL(layernorm_f32<12>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(layernorm_f32<16>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
+    case 1536: hipLaunchKernelGGL(layernorm_f32<24>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
+    case 2048: hipLaunchKernelGGL(layernorm_f32<32>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
     default:
       g_err = "layernorm: unsupported hidden size " + std::to_string(D);
       return -1;
@@ -944,7 +991,8 @@ int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, 
     hipLaunchKernelGGL(attn_fwd_sk_lds, dim3(waves), dim3(256), 0, s, qkv, out, part_o, part_ml, B, T, H,
                        scale_log2e, waves);
     if (int rc = check_launch("attn_fwd_sk_lds")) return rc;
-    hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves);
+    hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
+                       static_cast<__bf16*>(nullptr));
     return check_launch("attn_sk_lds_fixup");
   }
   float* part_o = ws;

@@ -248,3 +248,85 @@ def test_attention_x3_asymmetric_values(K):
     K.attention_x3(K.split3(qkv), out, H, 64, 0.125, 5)
     ref = _ref_attention(qkv, H, 64, 0.125)
     assert (out - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("M,N,Kd", [(3401, 384, 384), (3401, 1152, 384), (3401, 1536, 384), (3401, 384, 1536),
+                                    (3300, 384, 768), (100, 128, 64), (1, 128, 32)])
+def test_gemm_x3_every_tile_epilogue_and_output(K, M, N, Kd):
+    # fp32-accurate: the x3 GEMM's error vs fp64 stays within 2x the f32-input MFMA GEMM's
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(0)
+    x = torch.randn(M, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda")
+    x3 = K.split3(x)
+    hb = x.double() @ w.double().t() + b.double()
+    cases = {"bias": (hb, {"bias": b}),
+             "gelu": (0.5 * hb * (1 + torch.erf(hb / math.sqrt(2))), {"bias": b, "gelu": True}),
+             "res": (hb + r.double(), {"bias": b, "residual": r})}
+    for name, (ref, kw) in cases.items():
+        f32 = G.gemm(x, w, tile=G.eligible(M, N, Kd)[0], **kw)
+        err_f32 = (f32.double() - ref).abs().max().item()
+        for cfg in G.x3_eligible(N, Kd):
+            y, y3 = G.gemm_x3(x3, w, tile=cfg, out_f32=True, out_x3=True, **kw)
+            torch.cuda.synchronize()
+            err = (y.double() - ref).abs().max().item()
+            assert err <= max(2.0 * err_f32, 1e-5), (cfg, name, err, err_f32)
+            assert torch.equal(y3[0].double() + y3[1].double() + y3[2].double(), y.double()), (cfg, name)
+            only3 = G.gemm_x3(x3, w, tile=cfg, out_f32=False, out_x3=True, **kw)
+            assert torch.equal(only3, y3), (cfg, name)
+
+
+def test_gemm_x3_second_residual_and_out_view(K):
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(3)
+    T, N, Kd = 300, 128, 64
+    x = torch.randn(2 * T, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.1
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(2 * T, N, device="cuda")
+    r2 = torch.randn(1, T, N, device="cuda")
+    ref = x.double() @ w.double().t() + b.double() + r.double() + r2.double().repeat(2, 1, 1).reshape(2 * T, N)
+    for cfg in G.x3_eligible(N, Kd):
+        buf = torch.zeros(2 * T + 7, N, device="cuda")
+        out = G.gemm_x3(K.split3(x), w, b, residual=r, residual2=r2, tile=cfg, out=buf[3:3 + 2 * T])
+        torch.cuda.synchronize()
+        assert (out.double() - ref).abs().max().item() < 1e-4, cfg
+        assert buf[:3].abs().max().item() == 0 and buf[-4:].abs().max().item() == 0
+
+
+def test_layernorm_and_attention_x3_outputs(K):
+    torch.manual_seed(6)
+    x = torch.randn(1, 3401, 384, device="cuda")
+    w, b = torch.randn(384, device="cuda"), torch.randn(384, device="cuda")
+    y = K.layernorm(x, w, b, 1e-12)
+    y3 = K.layernorm_x3(x, w, b, 1e-12)
+    assert torch.equal(y3[0].double() + y3[1].double() + y3[2].double(), y.double())
+    qkv = torch.randn(1, 1000, 3 * 2 * 64, device="cuda")
+    o3 = K.attention_qkv_x3(K.split3(qkv), 2, 64, 0.125)
+    ref = _ref_attention(qkv, 2, 64, 0.125)
+    o = (o3[0].double() + o3[1].double() + o3[2].double())
+    assert (o - ref.double()).abs().max().item() < 2e-6
+
+
+def test_yolos_x3_matches_f32_mode(K):
+    from walkai_nos_amd.models.workload.yolos import YolosSmall, demo_input
+    m = YolosSmall().cuda().eval()
+    x = demo_input(1, (800, 1066), "cuda")
+    try:
+        with torch.no_grad():
+            K.set_fp32_matmul("f32")
+            l32, b32 = m(x)
+            K.set_fp32_matmul("x3")
+            l3, b3 = m(x)
+            K.set_backend("torch")
+            lt, bt = m(x)
+    finally:
+        K.set_backend("hip")
+        K.set_fp32_matmul("x3")
+    torch.cuda.synchronize()
+    # both HIP modes sit at fp32 rounding distance from the PyTorch fp32 reference
+    e3, e32 = (l3 - lt).abs().max().item(), (l32 - lt).abs().max().item()
+    assert e3 < 1e-3 and e32 < 1e-3, (e3, e32)
+    assert (b3 - bt).abs().max().item() < 1e-4

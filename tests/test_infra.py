@@ -165,3 +165,19 @@ def test_split3_cpu_reconstructs_exactly():
     x = torch.randn(4096, dtype=torch.float32) * torch.logspace(-10, 10, 4096)
     p = K.split3(x)
     assert torch.equal(p[0].double() + p[1].double() + p[2].double(), x.double())
+
+
+def test_weight_planes_cached_on_tensor_and_invalidated_by_writes():
+    import torch
+
+    from walkai_nos_amd.ops import gemm as G
+    w = torch.nn.Parameter(torch.randn(8, 3, 2, 2))
+    p1 = G.weight_planes(w.reshape(8, -1))
+    assert G.weight_planes(w.reshape(8, -1)) is p1        # views of one weight share the cache
+    with torch.no_grad():
+        w.mul_(2)
+    p2 = G.weight_planes(w.reshape(8, -1))
+    assert p2 is not p1
+    assert torch.equal(p2[0].float() + p2[1].float() + p2[2].float(), w.detach().reshape(8, -1))
+    other = torch.randn(8, 12)                             # a different tensor never hits w's cache
+    assert torch.equal(G.weight_planes(other)[0], other.to(torch.bfloat16))

@@ -125,11 +125,15 @@ def model_bench(r, s, iters):
     with torch.cuda.stream(s):
         m = YolosSmall().cuda().eval()
         xin = demo_input(1, DEMO_INPUT_HW, "cuda")
-    with torch.no_grad():
-        us = timeit(lambda: m(xin), s, iters)
-    r["model_ms"] = round(us / 1000.0, 3)
-    r["model_tflops"] = round(m.flops_per_inference() / us / 1e6, 2)
-    r["model_inf_per_s_per_gpu"] = round(1e6 / us * 256 / r["cus"], 1)
+    for mode in ("x3", "f32"):
+        K.set_fp32_matmul(mode)
+        with torch.no_grad():
+            us = timeit(lambda: m(xin), s, iters)
+        sfx = "" if mode == "x3" else "_f32"
+        r[f"model{sfx}_ms"] = round(us / 1000.0, 3)
+        r[f"model{sfx}_tflops"] = round(m.flops_per_inference() / us / 1e6, 2)
+        r[f"model{sfx}_inf_per_s_per_gpu"] = round(1e6 / us * 256 / r["cus"], 1)
+    K.set_fp32_matmul("x3")
 
 
 def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
@@ -149,6 +153,15 @@ def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
             tag = "x".join(map(str, G.TILES[cfg][:2])) + f"k{G.TILES[cfg][2]}" + ("sb" if cfg >= 7 else "")
             r[f"mfma_{gname}_{tag}_us"] = round(us, 1)
             r[f"mfma_{gname}_{tag}_tflops"] = round(fl / us / 1e6, 2)
+        # x3 GEMM (fp32-accurate on the bf16 matrix cores), every tile; planes out where the model
+        # feeds another x3 consumer (qkv, fc1), fp32 out where it feeds the residual stream
+        xa3 = K.split3(xa)
+        x3_out = gname in ("qkv", "fc1")
+        for cfg in G.x3_eligible(wa.shape[0], wa.shape[1]):
+            us = timeit(lambda: G.gemm_x3(xa3, wa, tile=cfg, out_f32=not x3_out, out_x3=x3_out, **kw), s, iters)
+            bm, bn, nb = G.X3_TILES[cfg]
+            r[f"x3_{gname}_{bm}x{bn}b{nb}_us"] = round(us, 1)
+            r[f"x3_{gname}_{bm}x{bn}b{nb}_tflops"] = round(fl / us / 1e6, 2)
 
 
 if __name__ == "__main__":

@@ -345,6 +345,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     util = sum(nb.util_samples) / max(1, len(nb.util_samples))
     pods = sum(nb.pods_samples) / max(1, len(nb.pods_samples))
     from .models.workload.yolos import YolosSmall
+    from .ops import kernels as K
     flops = YolosSmall().flops_per_inference(cfg.hw)
     return {
         "metric": "aggregate GPU utilization % + schedulable pods/node, mixed fractional-GPU load",
@@ -358,6 +359,9 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "scaling": "weak",
         "vs_baseline": round(value / (BASELINE_INFER_PER_S_PER_GPU * cfg.gpus), 3),
         "dtype": "fp32",
+        "numerics": ("fp32-accurate: every fp32 product as 6 bf16 MFMAs over an exact 3-term bf16 split "
+                     "of both operands (dropped terms 2^-24 relative; tests/test_gpu_kernels.py checks the "
+                     "error vs fp64 against the f32-input MFMA path)") if cfg.backend == "hip" else "fp32",
         "data": "synthetic (seeded pod churn; random-init YOLOS-small weights; synthetic 800x1066 images)",
         "gpu_utilization_pct": round(util, 2),
         "pods_per_node": round(pods, 2),
@@ -369,7 +373,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
                    "parallelism": f"fractional-gpu xcp partitions, {cfg.gpus} GPU node",
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
-                   "backend": cfg.backend, "hip_graphs": cfg.graphs},
+                   "backend": cfg.backend, "hip_graphs": cfg.graphs,
+                   "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
 
 

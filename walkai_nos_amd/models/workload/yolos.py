@@ -6,7 +6,10 @@ Pod runs ``hustvl/yolos-small`` inference at batch 1 on one COCO image in a loop
 independent implementation of that architecture (ViT-S/16 encoder with 100 detection tokens and
 DETR-style MLP heads) built for the MI355X inference path:
 
-* fp32 end to end (the reference demo runs fp32 PyTorch; no precision is given up);
+* fp32 end to end (the reference demo runs fp32 PyTorch; no precision is given up): on the GPU every
+  product runs in the x3 format — fp32 operands split exactly into three bf16 planes, six bf16
+  MFMAs per block, fp32-accurate (``ops/kernels.py: set_fp32_matmul``); ``f32`` mode uses the
+  f32-input MFMA instead;
 * the interpolated position embeddings are computed once per input resolution and cached (the
   upstream implementation re-interpolates on every forward);
 * the hot ops dispatch to hand-written HIP kernels (:mod:`walkai_nos_amd.ops.kernels`) on the GPU:
@@ -72,6 +75,16 @@ class _Block(nn.Module):
     def forward(self, x: torch.Tensor, mid: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, T, D = x.shape
         H, Dh = self.c.num_heads, self.c.head_dim
+        if K.x3_active(x):
+            # every fp32 product on the bf16 matrix cores in x3 form: activations leave their
+            # producer as three exact bf16 planes; the residual stream stays fp32
+            h3 = K.layernorm_x3(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
+            qkv3 = K.linear_x3(h3, self.qkv.weight, self.qkv.bias, out_x3=True)
+            o3 = K.attention_qkv_x3(qkv3, H, Dh, 1.0 / math.sqrt(Dh))
+            x = K.linear_x3(o3, self.proj.weight, self.proj.bias, residual=x)
+            h3 = K.layernorm_x3(x, self.ln2.weight, self.ln2.bias, self.c.layer_norm_eps)
+            f3 = K.linear_x3(h3, self.fc1.weight, self.fc1.bias, gelu=True, out_x3=True)
+            return K.linear_x3(f3, self.fc2.weight, self.fc2.bias, residual=x, residual2=mid)
         h = K.layernorm(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
         qkv = K.linear(h, self.qkv.weight, self.qkv.bias)                  # [B, T, 3D]
         o = K.attention_qkv(qkv, H, Dh, 1.0 / math.sqrt(Dh))               # [B, T, D]

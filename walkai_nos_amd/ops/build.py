@@ -60,7 +60,7 @@ TARGETS: Sequence[Target] = (
     Target("libnos_hbmlimit.so", ["hbm_limit.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"], libs=["dl"]),
     Target("libnos_barrier.so", ["rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
            libs=["rccl", "amdhip64"]),
-    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip"], "hipcc"),
+    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip"], "hipcc"),
 )
 
 

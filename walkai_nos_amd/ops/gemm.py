@@ -194,3 +194,131 @@ def tuning_table() -> Dict[str, str]:
         return {f"M{m}_N{n}_K{k}_epi{e}_cus{c}": ("hipblaslt" if v == LIBRARY else "x".join(map(str, TILES[v][:2]))
                                                   + f"/k{TILES[v][2]}" + ("/sb" if v >= 7 else ""))
                 for (m, n, k, e, c), v in sorted(_cache.items())}
+
+
+# ---- x3: fp32-accurate GEMM on the bf16 matrix cores (csrc/gemm_x3.hip) -------------------------
+#: config -> (BM, BN, LDS buffers)
+X3_TILES = {0: (64, 64, 2), 1: (128, 64, 2), 2: (64, 128, 2), 3: (128, 128, 2),
+            4: (64, 64, 1), 5: (128, 64, 1), 6: (64, 128, 1)}
+#: resident workgroups per CU (LDS-limited: 60/90/120 KB double-buffered, 30/45 KB single)
+X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3}
+_x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
+_x3_bound = False
+
+
+def _lib_x3() -> ctypes.CDLL:
+    global _x3_bound
+    L = K._L()
+    if not _x3_bound:
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        L.nos_gemm_x3.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32, vp]
+        L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
+        _x3_bound = True
+    return L
+
+
+def weight_planes(w: torch.Tensor) -> torch.Tensor:
+    """x3 planes of a weight, split once and cached ON the weight tensor (its view base, for a view
+    such as the patch embedding's reshaped kernel) and re-split when the weight is modified in
+    place (its version counter moves). Keying on the tensor object — not its address — keeps a
+    freed weight's planes from being served to a new tensor that reuses the memory."""
+    owner = w._base if w._base is not None else w
+    key = (w.storage_offset(), tuple(w.shape), tuple(w.stride()))
+    cache = owner.__dict__.setdefault("_nos_x3", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] == w._version:
+        return hit[1]
+    if w.is_cuda and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("weight_planes: weights must be split before graph capture (run one eager forward)")
+    p = K.split3(w.detach().contiguous())
+    cache[key] = (w._version, p)
+    return p
+
+
+def x3_eligible(N: int, Kd: int) -> list:
+    if Kd % 32:
+        return []
+    return [c for c, (bm, bn, _) in X3_TILES.items() if N % bn == 0]
+
+
+def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
+    best, best_key = cands[0], None
+    for c in cands:
+        bm, bn, _ = X3_TILES[c]
+        tiles = -(-M // bm) * (N // bn)
+        rounds = -(-tiles // (X3_SLOTS_PER_CU[c] * cus))
+        key = (rounds * bm * bn / min(X3_SLOTS_PER_CU[c], 2), -bm * bn)
+        if best_key is None or key < best_key:
+            best, best_key = c, key
+    return best
+
+
+def _launch_x3(cfg, a3, w3, bias, res, r2, out, out3, epi) -> None:
+    _, M, Kd = a3.shape
+    N = w3.shape[1]
+    rc = _lib_x3().nos_gemm_x3(a3.data_ptr(), a3[0].numel(), w3.data_ptr(), w3[0].numel(),
+                               bias.data_ptr() if bias is not None else None,
+                               res.data_ptr() if res is not None else None,
+                               r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+                               out.data_ptr() if out is not None else None,
+                               out3.data_ptr() if out3 is not None else None, out3[0].numel() if out3 is not None else 0,
+                               M, N, Kd, epi, cfg, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"nos gemm_x3 failed: {_lib_x3().nos_gemm_x3_last_error().decode()} (rc={rc})")
+
+
+def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
+            residual: Optional[torch.Tensor] = None, residual2: Optional[torch.Tensor] = None,
+            out_f32: bool = True, out_x3: bool = False, out: Optional[torch.Tensor] = None,
+            tile: Optional[int] = None):
+    """fp32-accurate ``a @ w^T (+bias) (GELU) (+residual) (+residual2)`` from x3 planes.
+
+    ``a3``: ``[3, ..., K]`` bf16 planes of the fp32 activation; ``w``: the fp32 weight ``[N, K]``
+    (split once, cached) or its planes ``[3, N, K]``. Returns the fp32 result ``[..., N]`` and/or its
+    x3 planes ``[3, ..., N]`` (a tuple when both are requested)."""
+    lead = a3.shape[1:-1]
+    Kd = a3.shape[-1]
+    a3 = a3.reshape(3, -1, Kd)
+    if not a3.is_contiguous():
+        a3 = a3.contiguous()
+    M = a3.shape[1]
+    w3 = w if w.dim() == 3 else weight_planes(w)
+    N = w3.shape[1]
+    dev = a3.device
+    o = None
+    if out_f32:
+        if out is not None:
+            if not out.is_contiguous() or out.numel() != M * N:
+                raise ValueError("gemm_x3: out must be contiguous with M x N elements")
+            o = out.view(M, N)
+        else:
+            o = torch.empty(M, N, dtype=torch.float32, device=dev)
+    o3 = torch.empty(3, M, N, dtype=torch.bfloat16, device=dev) if out_x3 else None
+    res = residual.reshape(M, N).contiguous() if residual is not None else None
+    r2 = residual2.reshape(-1, N).contiguous() if residual2 is not None else None
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_GELU if gelu else 0) | (EPI_RES if residual is not None else 0) \
+        | (EPI_RES2 if residual2 is not None else 0)
+    if tile is None:
+        cus = K.slice_cus()
+        key = (M, N, Kd, epi, int(out_f32) | 2 * int(out_x3), cus)
+        with _lock:
+            tile = _x3_cache.get(key)
+        if tile is None:
+            cands = x3_eligible(N, Kd)
+            if not cands:
+                raise ValueError(f"gemm_x3: unsupported shape N={N} K={Kd}")
+            if torch.cuda.is_current_stream_capturing():
+                tile = x3_heuristic(M, N, cus, cands)
+            else:
+                stream = torch.cuda.current_stream()
+                times = {c: _gpu_time(lambda c=c: _launch_x3(c, a3, w3, bias, res, r2, o, o3, epi), stream)
+                         for c in cands}
+                tile = min(times, key=times.get)
+                with _lock:
+                    _x3_cache[key] = tile
+    _launch_x3(tile, a3, w3, bias, res, r2, o, o3, epi)
+    rf = None if o is None else (o.view(*lead, N) if out is None else out)
+    r3 = None if o3 is None else o3.view(3, *lead, N)
+    if out_f32 and out_x3:
+        return rf, r3
+    return rf if out_f32 else r3

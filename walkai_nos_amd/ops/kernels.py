@@ -129,12 +129,25 @@ def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
 
 def attention_x3(planes: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float,
                  waves: int) -> torch.Tensor:
-    """Stream-K attention over the x3 planes ``[3, B, T, 3*H*64]`` of a packed QKV tensor."""
+    """Stream-K attention over the x3 planes ``[3, B, T, 3*H*64]`` of a packed QKV tensor. ``out`` is
+    fp32 ``[B, T, H*64]`` or bf16 ``[3, B, T, H*64]`` (the output leaves as x3 planes)."""
     _, B, T, _ = planes.shape
     ws = torch.empty(waves * 2 * (64 * 32 + 64) * 4, dtype=torch.float32, device=planes.device)
-    _check(_L().nos_attention_x3_sk(planes.data_ptr(), planes[0].numel(), out.data_ptr(), ws.data_ptr(), B, T,
-                                    heads, head_dim, scale, waves, _stream()))
+    x3_out = out.dtype == torch.bfloat16
+    _check(_L().nos_attention_x3_sk(planes.data_ptr(), planes[0].numel(), None if x3_out else out.data_ptr(),
+                                    out.data_ptr() if x3_out else None, ws.data_ptr(), B, T, heads, head_dim, scale,
+                                    waves, _stream()))
     return out
+
+
+def attention_qkv_x3(planes: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
+    """x3 planes of packed QKV in, x3 planes ``[3, B, T, H*64]`` of the attention output out."""
+    _, B, T, _ = planes.shape
+    if not _use_hip(planes):
+        qkv = (planes[0].double() + planes[1].double() + planes[2].double()).float()
+        return split3(attention_ref(qkv, heads, head_dim, scale))
+    out = torch.empty(3, B, T, heads * head_dim, dtype=torch.bfloat16, device=planes.device)
+    return attention_x3(planes, out, heads, head_dim, scale, attention_x3_waves(slice_cus(), B, T, heads))
 
 
 def set_backend(name: str) -> None:
@@ -158,7 +171,7 @@ def _L() -> ctypes.CDLL:
         if _lib is None:
             L = load(LIB)
             vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
-            L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, i32, i32, f32, vp]
+            L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, vp, i32, i32, f32, vp]
             L.nos_bias_gelu_f32.argtypes = [vp, vp, i32, i32, vp]
             L.nos_attention_f32.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
             L.nos_attention_f32_sk.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
@@ -166,7 +179,7 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
-            L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             _lib = L
         return _lib
 
@@ -199,7 +212,21 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> 
     if D % 4 != 0 or D > 64 * 4 * 8:
         return F.layer_norm(x, (D,), w, b, eps)
     out = torch.empty_like(x)
-    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), rows, D, eps, _stream()))
+    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), None, rows, D, eps,
+                                  _stream()))
+    return out
+
+
+def layernorm_x3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    """LayerNorm whose output leaves as x3 planes ``[3, *x.shape]`` bf16 (the next GEMM's operand)."""
+    if not _use_hip(x):
+        return split3(F.layer_norm(x, (x.shape[-1],), w, b, eps))
+    x = x.contiguous()
+    D = x.shape[-1]
+    rows = x.numel() // D
+    out = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
+    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, out.data_ptr(), rows, D, eps,
+                                  _stream()))
     return out
 
 
@@ -245,6 +272,31 @@ def linear_residual(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, res: torc
     return gemm(x, w, b, residual=res, residual2=res2)
 
 
+def x3_active(t: torch.Tensor) -> bool:
+    """True when the model's fp32 products on ``t`` run in the x3 format on the HIP kernels."""
+    return t.is_cuda and t.dtype == torch.float32 and get_fp32_matmul() == "x3" and _use_hip(t)
+
+
+def linear_x3(a3: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu: bool = False,
+              residual: Optional[torch.Tensor] = None, residual2: Optional[torch.Tensor] = None,
+              out_x3: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``a @ w^T + b`` (GELU) (+ residuals) from the x3 planes of ``a``; the result is fp32, or its x3
+    planes when ``out_x3`` (for the next x3 consumer)."""
+    if not _use_hip(a3):
+        a = (a3[0].double() + a3[1].double() + a3[2].double()).float()
+        y = F.linear(a, w, b)
+        if gelu:
+            y = F.gelu(y)
+        if residual is not None:
+            y = y + residual
+        if residual2 is not None:
+            y = y + residual2
+        return split3(y) if out_x3 else y
+    from .gemm import gemm_x3
+    return gemm_x3(a3, w, b, gelu=gelu, residual=residual, residual2=residual2, out_f32=not out_x3, out_x3=out_x3,
+                   out=out)
+
+
 def patch_embed(pixels: torch.Tensor, w: torch.Tensor, b: torch.Tensor, patch: int,
                 pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Non-overlapping patch embedding (a stride-``patch`` conv) as one unfold copy + the MFMA GEMM,
@@ -257,6 +309,10 @@ def patch_embed(pixels: torch.Tensor, w: torch.Tensor, b: torch.Tensor, patch: i
         return y + pos if pos is not None else y
     cols = pixels[:, :, :gh * patch, :gw * patch].reshape(B, C, gh, patch, gw, patch) \
         .permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * patch * patch)
+    if x3_active(pixels) and (C * patch * patch) % 32 == 0:
+        from .gemm import gemm_x3
+        y = gemm_x3(split3(cols), w.reshape(w.shape[0], -1), b, residual2=pos, out=out)
+        return y.view(B, gh * gw, -1)
     from .gemm import gemm
     y = gemm(cols, w.reshape(w.shape[0], -1), b, residual2=pos, out=out)
     return y.view(B, gh * gw, -1)
