@@ -76,6 +76,31 @@ __device__ __forceinline__ void stash(const uint4 (&r)[3][Tile<ROWS>::V], __bf16
   }
 }
 
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void compute_stage(f32x16 (&acc)[WM / 32][WN / 32], const __bf16* __restrict__ as,
+                                              const __bf16* __restrict__ bs, int wm, int wn, int j, int hf) {
+  constexpr int TM = WM / 32, TN = WN / 32;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        af[a][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * LSTR + (wm * WM + 32 * a + j) * LSTR + 16 * s + 8 * hf]);
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * LSTR + (wn * WN + 32 * b + j) * LSTR + 16 * s + 8 * hf]);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        acc[a][b] = mfma_x3(af[a][0], af[a][1], af[a][2], bfr[b][0], bfr[b][1], bfr[b][2], acc[a][b]);
+  }
+}
+
 template <int WM, int WN, int NBUF>
 __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, size_t a_plane,
                                                  const __bf16* __restrict__ W, size_t w_plane,
@@ -85,6 +110,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
                                                  int epi) {
   constexpr int BM = 2 * WM, BN = 2 * WN;
   constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int VA = Tile<BM>::V, VB = Tile<BN>::V;
   __shared__ __attribute__((aligned(16))) __bf16 As[NBUF][3 * BM * LSTR];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NBUF][3 * BN * LSTR];
 
@@ -98,7 +124,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
   const int wm = wave >> 1, wn = wave & 1;
   const int j = lane & 31, hf = lane >> 5;
 
-  uint4 pa[3][Tile<BM>::V], pb[3][Tile<BN>::V];
+  uint4 pa0[3][VA], pb0[3][VB];
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
@@ -106,46 +132,39 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
 
   const int nk = K / BK;
-  fetch<BM>(pa, A, a_plane, m0, M - 1, K, 0, tid);
-  fetch<BN>(pb, W, w_plane, n0, N - 1, K, 0, tid);
-  stash<BM>(pa, As[0], tid);
-  stash<BN>(pb, Bs[0], tid);
-  __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    const int buf = NBUF == 2 ? (ks & 1) : 0;
-    // unconditional prefetch (the last stage re-reads itself) keeps pa/pb in registers
-    const int kn = min(ks + 1, nk - 1) * BK;
-    fetch<BM>(pa, A, a_plane, m0, M - 1, K, kn, tid);
-    fetch<BN>(pb, W, w_plane, n0, N - 1, K, kn, tid);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 af[TM][3], bfr[TN][3];
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          af[a][q] = *reinterpret_cast<const bf16x8*>(&As[buf][q * BM * LSTR + (wm * WM + 32 * a + j) * LSTR + 16 * s +
-                                                               8 * hf]);
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          bfr[b][q] = *reinterpret_cast<const bf16x8*>(&Bs[buf][q * BN * LSTR + (wn * WN + 32 * b + j) * LSTR + 16 * s +
-                                                                8 * hf]);
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-          acc[a][b] = mfma_x3(af[a][0], af[a][1], af[a][2], bfr[b][0], bfr[b][1], bfr[b][2], acc[a][b]);
-    }
-    if constexpr (NBUF == 1) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): own fragment reads drained
-      __builtin_amdgcn_s_barrier();
-    }
-    stash<BM>(pa, As[NBUF == 2 ? (buf ^ 1) : 0], tid);
-    stash<BN>(pb, Bs[NBUF == 2 ? (buf ^ 1) : 0], tid);
-    __syncthreads();
+// past the end a load re-reads the last stage: loads stay unconditional, so the prefetch registers
+// are never conditionally live (the compiler would demote them to scratch)
+#define X3_LOAD(RA, RB, STAGE)                                           \
+  {                                                                      \
+    const int k0_ = min((STAGE), nk - 1) * BK;                           \
+    fetch<BM>(RA, A, a_plane, m0, M - 1, K, k0_, tid);                   \
+    fetch<BN>(RB, W, w_plane, n0, N - 1, K, k0_, tid);                   \
   }
+#define X3_PUT(RA, RB, BUF)                                              \
+  {                                                                      \
+    if constexpr (NBUF == 1) {                                           \
+      __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0) */               \
+      __builtin_amdgcn_s_barrier();                                      \
+    }                                                                    \
+    stash<BM>(RA, As[BUF], tid);                                         \
+    stash<BN>(RB, Bs[BUF], tid);                                         \
+    __syncthreads();                                                     \
+  }
+// one stage ks: stage ks+1 is loaded into (NA, NB) across the MFMAs of stage ks, then stashed
+#define X3_STEP(KS, NA, NB)                                              \
+  {                                                                      \
+    const int buf_ = NBUF == 2 ? ((KS) & 1) : 0;                         \
+    X3_LOAD(NA, NB, (KS) + 1)                                            \
+    compute_stage<BM, BN, WM, WN>(acc, As[buf_], Bs[buf_], wm, wn, j, hf); \
+    X3_PUT(NA, NB, NBUF == 2 ? (buf_ ^ 1) : 0)                           \
+  }
+
+  X3_LOAD(pa0, pb0, 0)
+  X3_PUT(pa0, pb0, 0)
+  for (int ks = 0; ks < nk; ++ks) X3_STEP(ks, pa0, pb0)
+#undef X3_STEP
+#undef X3_PUT
+#undef X3_LOAD
 
   // epilogue: acc[a][b] register r is C[m0 + wm*WM + 32a + acc_row(r, hf)][n0 + wn*WN + 32b + j]
 #pragma unroll
@@ -195,21 +214,214 @@ int launch(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* 
   }
   return 0;
 }
+
+// ---- LDS-DMA variant ---------------------------------------------------------------------------
+// Same math and epilogue; the operand tiles go global -> LDS with global_load_lds_dwordx4 (no
+// register staging), S LDS buffers deep, so S-1 stages of loads are in flight behind the MFMAs at
+// the cost of LDS only. The DMA writes a wave's 64 lanes x 16 B lane-linearly, so the image has
+// unpadded 64-B rows [plane][row][4 chunks] and conflict-freedom comes from the lane -> chunk map
+// instead: LDS slot c of row r holds k-chunk c ^ ((r >> 2) & 3); a fragment read of chunk 2s+h
+// then lands, over any ds_read_b128 lane group, on 16 distinct 16-B bank slots (r mod 4 picks the
+// 16-bank quarter, (r >> 2) & 3 the slot inside it). One raw s_barrier per stage: a
+// __syncthreads() fence would wait for every outstanding DMA (vmcnt(0)) and serialise the pipeline;
+// the per-wave "stage ks landed" wait is an explicit vmcnt(loads of the S-2 younger stages).
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// one stage of ROWS x 32 bf16 per plane for this wave: row groups g = wave, wave+4, ... of 16 rows
+template <int ROWS>
+__device__ __forceinline__ void dma_stage(const __bf16* __restrict__ X, size_t plane, int r0, int rmax, int K, int k0,
+                                          __bf16* lds, int wave, int lane) {
+  const int rl = lane >> 2, c = (lane & 3) ^ ((lane >> 4) & 3);
+#pragma unroll
+  for (int i = 0; i < ROWS / 64; ++i) {
+    const int g = wave + 4 * i;
+    const int row = min(r0 + 16 * g + rl, rmax);
+    const __bf16* src = X + size_t(row) * K + k0 + 8 * c;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      __builtin_amdgcn_global_load_lds(src + q * plane, (lds_void*)(lds + q * ROWS * 32 + 16 * g * 32), 16, 0, 0);
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void compute_stage_sw(f32x16 (&acc)[WM / 32][WN / 32], const __bf16* __restrict__ as,
+                                                 const __bf16* __restrict__ bs, int wm, int wn, int j, int hf) {
+  constexpr int TM = WM / 32, TN = WN / 32;
+  const int sw = (j >> 2) & 3;  // rows j and j + 32a share (row >> 2) & 3
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int ch = (2 * s + hf) ^ sw;
+    bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        af[a][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * 32 + (wm * WM + 32 * a + j) * 32 + 8 * ch]);
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * 32 + (wn * WN + 32 * b + j) * 32 + 8 * ch]);
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        acc[a][b] = mfma_x3(af[a][0], af[a][1], af[a][2], bfr[b][0], bfr[b][1], bfr[b][2], acc[a][b]);
+  }
+}
+
+template <int WM, int WN, int S>
+__global__ __launch_bounds__(256, 1) void gemm_x3d(const __bf16* __restrict__ A, size_t a_plane,
+                                                  const __bf16* __restrict__ W, size_t w_plane,
+                                                  const float* __restrict__ bias, const float* __restrict__ R,
+                                                  const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
+                                                  __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int K,
+                                                  int epi) {
+  static_assert(S >= 2 && S <= 4, "2-4 LDS stages");
+  constexpr int BM = 2 * WM, BN = 2 * WN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int NLD = 3 * (BM / 64) + 3 * (BN / 64);  // DMA instructions per wave per stage
+  // one __shared__ object per stage buffer: the compiler's LDS-DMA wait tracking can then tell the
+  // buffer being read from the buffers being filled (one array indexed by stage would make every
+  // fragment read wait for ALL outstanding DMA, vmcnt(0), and serialise the pipeline)
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * 32], A1[3 * BM * 32], A2[S > 2 ? 3 * BM * 32 : 8],
+      A3[S > 3 ? 3 * BM * 32 : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * 32], B1[3 * BN * 32], B2[S > 2 ? 3 * BN * 32 : 8],
+      B3[S > 3 ? 3 * BN * 32 : 8];
+
+  const int tiles_n = N / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int t = xcd_major(blockIdx.x, gridDim.x);
+  if (t >= tiles) return;
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int j = lane & 31, hf = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
+
+  const int nk = K / BK;
+#define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
+#define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
+// past the end a stage re-reads the last one, so every iteration issues NLD loads (static vmcnt)
+#define X3D_ISSUE(STAGE, BUF)                                                      \
+  {                                                                                \
+    const int k0_ = min((STAGE), nk - 1) * BK;                                     \
+    dma_stage<BM>(A, a_plane, m0, M - 1, K, k0_, X3D_A(BUF), wave, lane);          \
+    dma_stage<BN>(W, w_plane, n0, N - 1, K, k0_, X3D_B(BUF), wave, lane);          \
+  }
+#define X3D_ITER(KS, BUF)                                                          \
+  {                                                                                \
+    vm_wait<(S - 2) * NLD>(); /* this wave's DMA of stage KS has landed */         \
+    raw_barrier();            /* everyone's has; stage KS-1's buffer is free */    \
+    X3D_ISSUE((KS) + S - 1, ((BUF) + S - 1) % S)                                   \
+    compute_stage_sw<BM, BN, WM, WN>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf);  \
+  }
+  X3D_ISSUE(0, 0)
+  if constexpr (S > 2) X3D_ISSUE(1, 1)
+  if constexpr (S > 3) X3D_ISSUE(2, 2)
+  int ks = 0;
+  for (; ks + S <= nk; ks += S) {
+    X3D_ITER(ks, 0)
+    X3D_ITER(ks + 1, 1)
+    if constexpr (S > 2) X3D_ITER(ks + 2, 2)
+    if constexpr (S > 3) X3D_ITER(ks + 3, 3)
+  }
+  if (ks < nk) X3D_ITER(ks, 0)
+  if (ks + 1 < nk) X3D_ITER(ks + 1, 1)
+  if constexpr (S > 3)
+    if (ks + 2 < nk) X3D_ITER(ks + 2, 2)
+#undef X3D_ITER
+#undef X3D_ISSUE
+#undef X3D_B
+#undef X3D_A
+  vm_wait<0>();  // no DMA may still target this workgroup's LDS when it retires
+
+  // epilogue: acc[a][b] register r is C[m0 + wm*WM + 32a + acc_row(r, hf)][n0 + wn*WN + 32b + j]
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n0 + wn * WN + 32 * b + j;
+    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * WM + 32 * a + acc_row(r, hf);
+        if (row >= M) continue;
+        float v = acc[a][b][r] + bv;
+        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+        const size_t idx = size_t(row) * N + col;
+        if (epi & EPI_RES) v += R[idx];
+        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];
+        if (C) C[idx] = v;
+        if (Cp) {
+          const __bf16 h0 = (__bf16)v;
+          const float r1 = v - (float)h0;
+          const __bf16 h1 = (__bf16)r1;
+          Cp[idx] = h0;
+          Cp[c_plane + idx] = h1;
+          Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int S>
+int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
+             const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
+             hipStream_t s) {
+  constexpr int BM = 2 * WM, BN = 2 * WN;
+  if (N % BN) {
+    g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
+    return -1;
+  }
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  hipLaunchKernelGGL((gemm_x3d<WM, WN, S>), dim3(tiles), dim3(256), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
+                     cp, M, N, K, epi);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("gemm_x3d: ") + hipGetErrorString(e);
+    return int(e);
+  }
+  return 0;
+}
 }  // namespace
 
 extern "C" {
 
 const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 
-// Tile configurations (BM x BN): 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128 (double-buffered
-// LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered: half the LDS, more resident tiles).
-static const int kCfgX3[7][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
-                                 {64, 64, 1}, {128, 64, 1}, {64, 128, 1}};
+// Tile configurations (BM x BN, LDS buffers, load stages in flight): 0 = 64x64, 1 = 128x64,
+// 2 = 64x128, 3 = 128x128 (double-buffered LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered:
+// half the LDS, more resident tiles); 7-12 = LDS-DMA pipeline with nbuf = S stages (S-1 in
+// flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2.
+static const int kCfgX3[13][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+                                  {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
+                                  {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
+                                  {128, 128, 3}, {64, 64, 2}};
 
-int nos_gemm_x3_num_configs() { return 7; }
+int nos_gemm_x3_num_configs() { return 13; }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 6) return -1;
+  if (cfg < 0 || cfg > 12) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -247,6 +459,12 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 4: return launch<32, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 5: return launch<64, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 6: return launch<32, 64, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 7: return launch_d<32, 32, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 8: return launch_d<32, 32, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 9: return launch_d<64, 32, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 10: return launch_d<32, 64, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 11: return launch_d<64, 64, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 12: return launch_d<32, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

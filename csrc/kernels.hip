@@ -616,6 +616,27 @@ __device__ __forceinline__ void split3(const F& x, H& a, H& b, H& c) {
   c = __builtin_convertvector(r - __builtin_convertvector(b, F), H);
 }
 
+// Exact three-term split of acc[e0 .. e0+7] by truncation: x0 = the high 16 bits of x (its f32
+// value is x & 0xffff0000, so no conversion back is needed), x1 = the high half of x - x0, x2 =
+// the rest (<= 8 significant bits, exact in bf16); pairs are packed with one v_perm_b32 each.
+__device__ __forceinline__ void split3_trunc8(const f32x16& acc, int e0, bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  uint32_t w0[4], w1[4], w2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = acc[e0 + 2 * i], b = acc[e0 + 2 * i + 1];
+    const uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
+    w0[i] = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+    const float ra = a - __uint_as_float(ua & 0xffff0000u), rb = b - __uint_as_float(ub & 0xffff0000u);
+    const uint32_t ura = __float_as_uint(ra), urb = __float_as_uint(rb);
+    w1[i] = __builtin_amdgcn_perm(urb, ura, 0x07060302u);
+    const float sa = ra - __uint_as_float(ura & 0xffff0000u), sb = rb - __uint_as_float(urb & 0xffff0000u);
+    w2[i] = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+  }
+  p0 = __builtin_bit_cast(bf16x8, (uint4){w0[0], w0[1], w0[2], w0[3]});
+  p1 = __builtin_bit_cast(bf16x8, (uint4){w1[0], w1[1], w1[2], w1[3]});
+  p2 = __builtin_bit_cast(bf16x8, (uint4){w2[0], w2[1], w2[2], w2[3]});
+}
+
 // D += A·B with A, B given as three bf16 planes each (6 MFMAs, small terms first)
 __device__ __forceinline__ f32x16 mfma_x3(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
                                           const bf16x8& b1, const bf16x8& b2, f32x16 d) {
@@ -735,50 +756,252 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
       const int buf = (blk - kb0) & 1;
       const bool more = blk + 1 < kb1;
       if (more) fetch(blk + 1);
-      if (active) {
-        const __bf16* ks = &lds_k[buf * 3 * XK_PLANE + j * XK_STR + 8 * hf];
-        f32x16 sacc = {0};
+// One 32-key block of the x3 flash-attention loop. The key mask of the tail block sits behind a
+// real (wave-uniform) branch, so full blocks carry no per-key compares. Lazy rescale: the running max m only moves
+// when some lane's block max exceeds it by more than 2^8 in exp2 units (wave-uniform decision), so
+// the O/l rescale and its exp2 run on a few blocks per segment instead of every block; between
+// moves P may reach 2^8, which fp32 P/l/O absorb without loss.
+#define X3_ATTN_BLOCK(MASKED)                                                                        \
+  {                                                                                                  \
+    const __bf16* ks = &lds_k[buf * 3 * XK_PLANE + j * XK_STR + 8 * hf];                             \
+    f32x16 sacc = {0};                                                                               \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                                  \
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ks + 16 * s);                               \
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ks + XK_PLANE + 16 * s);                     \
+      const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(ks + 2 * XK_PLANE + 16 * s);                 \
+      sacc = mfma_x3(k0, k1, k2, qf[0][s], qf[1][s], qf[2][s], sacc);                                \
+    }                                                                                                \
+    if (MASKED) {                                                                                    \
+      asm volatile("; tail block: mask keys >= T" ::: "memory"); /* keep a real branch */          \
+      _Pragma("unroll") for (int r = 0; r < 16; ++r) if (blk * 32 + key_of(r, hf) >= T) sacc[r] = -INFINITY; \
+    }                                                                                                \
+    float mx = fmaxf(sacc[0], sacc[1]);                                                              \
+    _Pragma("unroll") for (int r = 2; r < 16; ++r) mx = fmaxf(mx, sacc[r]);                          \
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));                                                          \
+    if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {                                 \
+      const float m_new = fmaxf(m, mx);                                                              \
+      const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);                         \
+      l *= alpha;                                                                                    \
+      o0 *= alpha;                                                                                   \
+      o1 *= alpha;                                                                                   \
+      m = m_new;                                                                                     \
+    }                                                                                                \
+    const float mc = m * scale_log2e;                                                                \
+    float psum = 0.f;                                                                                \
+    _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                                 \
+      sacc[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], scale_log2e, -mc));                             \
+      psum += sacc[r];                                                                               \
+    }                                                                                                \
+    psum += __shfl_xor(psum, 32, 64);                                                                \
+    l += psum;                                                                                       \
+    const __bf16* vs = &lds_v[buf * 3 * XV_PLANE + vtr];                                             \
+    _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                                               \
+      bf16x8 p0, p1, p2;                                                                             \
+      split3_trunc8(sacc, 8 * s2, p0, p1, p2);                                                       \
+      _Pragma("unroll") for (int dh = 0; dh < 2; ++dh) {                                             \
+        bf16x8 vf[3];                                                                                \
+        _Pragma("unroll") for (int p = 0; p < 3; ++p) {                                              \
+          const __bf16* a = vs + p * XV_PLANE + 16 * s2 * XV_STR + 32 * dh;                          \
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));              \
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 8 * XV_STR)); \
+          vf[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};                    \
+        }                                                                                            \
+        if (dh == 0)                                                                                 \
+          o0 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o0);                                         \
+        else                                                                                         \
+          o1 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o1);                                         \
+      }                                                                                              \
+    }                                                                                                \
+  }
+      if (active) X3_ATTN_BLOCK(blk * 32 + 32 > T)
+#undef X3_ATTN_BLOCK
+      if (more) stash(buf ^ 1);
+      __syncthreads();
+    }
+
+    if (active) {
+      if (kb0 == 0 && kb1 == NK) {
+        const int q = q0 + j;
+        if (q < T) {
+          const float inv = 1.f / l;
+          const size_t orow = (size_t(b) * T + q) * D + head * HD;
+          if (outp) {
+            const size_t op = size_t(B) * T * D;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ks + 16 * s);
-          const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ks + XK_PLANE + 16 * s);
-          const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(ks + 2 * XK_PLANE + 16 * s);
-          sacc = mfma_x3(k0, k1, k2, qf[0][s], qf[1][s], qf[2][s], sacc);
+            for (int r = 0; r < 16; ++r) {
+              const int d = key_of(r, hf);
+              store_x3(outp, op, orow + d, o0[r] * inv);
+              store_x3(outp, op, orow + 32 + d, o1[r] * inv);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int d = key_of(r, hf);
+              out[orow + d] = o0[r] * inv;
+              out[orow + 32 + d] = o1[r] * inv;
+            }
+          }
         }
-        const int kb = blk * 32;
-        if (kb + 32 > T) {
+      } else {
+        const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * 4 + wv;
+        float* po = part_o + slot * (HD * 32);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = key_of(r, hf);
+          po[d * 32 + j] = o0[r];
+          po[(32 + d) * 32 + j] = o1[r];
+        }
+        if (hf == 0) {
+          part_ml[slot * 64 + j] = m * scale_log2e;
+          part_ml[slot * 64 + 32 + j] = l;
+        }
+      }
+    }
+    u += kb1 - kb0;
+    first = false;
+  }
+}
+
+// Software-pipelined x3 attention: iteration i runs the softmax, P split and P·V of key block i
+// while the S^T = K·Q^T MFMAs of block i+1 are already in flight in the same wave's instruction
+// stream, so the ~190 vector instructions per block issue in the matrix pipe's shadow instead of
+// between its bursts. K and V have their own double-buffered rings (iteration i reads K of block
+// i+1 and V of block i), one barrier per iteration. Same units, partials and fixup as attn_fwd_x3.
+__global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
+                                                       float* __restrict__ out, __bf16* __restrict__ outp,
+                                                       float* __restrict__ part_o, float* __restrict__ part_ml, int B,
+                                                       int T, int H, float scale_log2e, int P) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
+  __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
+  const int w = sk_logical(blockIdx.x, P);
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const long long U = (long long)B * H * QG * NK;
+  long long u = sk_begin(w, U, P);
+  const long long u1 = sk_begin(w + 1, U, P);
+  const int D = H * HD, ld = 3 * D;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int j = lane & 31, hf = lane >> 5;
+  const int lrow = tid >> 3, lch = tid & 7;
+  const int gi = lane & 15, gg = lane >> 4;
+  const int vtr = (4 * hf + (gi >> 2)) * XV_STR + 16 * (gg & 1) + 4 * (gi & 3);
+  bool first = true;
+  while (u < u1) {
+    const long long grp = u / NK;
+    const int kb0 = int(u - grp * NK);
+    const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
+    const int nb = kb1 - kb0;
+    const int qg = int(grp % QG);
+    const int head = int((grp / QG) % H);
+    const int b = int(grp / ((long long)QG * H));
+    const __bf16* base = qkv3 + size_t(b) * T * ld;
+    const int qt = qg * 4 + wv;
+    const bool active = qt < QT;
+    const int q0 = qt * 32;
+
+    bf16x8 qf[3][4];
+    {
+      const int qrow = min(q0 + j, T - 1);
+      const __bf16* qp = base + size_t(qrow) * ld + head * HD + 8 * hf;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[p][s] = *reinterpret_cast<const bf16x8*>(qp + p * plane + 16 * s);
+    }
+    const __bf16* kg = base + D + head * HD + 8 * lch;
+    const __bf16* vg = base + 2 * D + head * HD + 8 * lch;
+    uint4 pk0, pk1, pk2, pv0, pv1, pv2;
+    auto fetch_k = [&](int blk) {
+      const size_t r = size_t(min(blk * 32 + lrow, T - 1)) * ld;
+      pk0 = *reinterpret_cast<const uint4*>(kg + r);
+      pk1 = *reinterpret_cast<const uint4*>(kg + plane + r);
+      pk2 = *reinterpret_cast<const uint4*>(kg + 2 * plane + r);
+    };
+    auto fetch_v = [&](int blk) {
+      const size_t r = size_t(min(blk * 32 + lrow, T - 1)) * ld;
+      pv0 = *reinterpret_cast<const uint4*>(vg + r);
+      pv1 = *reinterpret_cast<const uint4*>(vg + plane + r);
+      pv2 = *reinterpret_cast<const uint4*>(vg + 2 * plane + r);
+    };
+    auto stash_k = [&](int buf) {
+      __bf16* kd = &lds_k[buf * 3 * XK_PLANE + lrow * XK_STR + 8 * lch];
+      *reinterpret_cast<uint4*>(kd) = pk0;
+      *reinterpret_cast<uint4*>(kd + XK_PLANE) = pk1;
+      *reinterpret_cast<uint4*>(kd + 2 * XK_PLANE) = pk2;
+    };
+    auto stash_v = [&](int buf) {
+      __bf16* vd = &lds_v[buf * 3 * XV_PLANE + lrow * XV_STR + 8 * lch];
+      *reinterpret_cast<uint4*>(vd) = pv0;
+      *reinterpret_cast<uint4*>(vd + XV_PLANE) = pv1;
+      *reinterpret_cast<uint4*>(vd + 2 * XV_PLANE) = pv2;
+    };
+#define X3P_QK(SACC, BUF)                                                                        \
+  {                                                                                              \
+    const __bf16* ks_ = &lds_k[(BUF) * 3 * XK_PLANE + j * XK_STR + 8 * hf];                      \
+    SACC = f32x16{0};                                                                            \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                              \
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(ks_ + 16 * s);                           \
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(ks_ + XK_PLANE + 16 * s);                 \
+      const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(ks_ + 2 * XK_PLANE + 16 * s);             \
+      SACC = mfma_x3(k0, k1, k2, qf[0][s], qf[1][s], qf[2][s], SACC);                            \
+    }                                                                                            \
+  }
+    __syncthreads();  // the previous segment's last blocks are no longer being read
+    fetch_k(kb0);
+    fetch_v(kb0);
+    stash_k(0);
+    stash_v(0);
+    if (nb > 1) {
+      fetch_k(kb0 + 1);
+      stash_k(1);
+    }
+    __syncthreads();
+
+    f32x16 o0 = {0}, o1 = {0}, scur = {0};
+    float m = -INFINITY, l = 0.f;
+    if (active) X3P_QK(scur, 0)
+    __syncthreads();  // iteration 0 refills K buffer 0, which the line above reads
+    for (int i = 0; i < nb; ++i) {
+      const int blk = kb0 + i;
+      const bool more_k = i + 2 < nb, more_v = i + 1 < nb;
+      if (more_k) fetch_k(blk + 2);
+      if (more_v) fetch_v(blk + 1);
+      if (active) {
+        if (blk * 32 + 32 > T) {
+          asm volatile("; tail block: mask keys >= T" ::: "memory");
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (kb + key_of(r, hf) >= T) sacc[r] = -INFINITY;
+            if (blk * 32 + key_of(r, hf) >= T) scur[r] = -INFINITY;
         }
-        float mx = sacc[0];
+        float mx = fmaxf(scur[0], scur[1]);
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
+        for (int r = 2; r < 16; ++r) mx = fmaxf(mx, scur[r]);
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float m_new = fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);
-        const float mc = m_new * scale_log2e;
+        if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {
+          const float m_new = fmaxf(m, mx);
+          const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);
+          l *= alpha;
+          o0 *= alpha;
+          o1 *= alpha;
+          m = m_new;
+        }
+        // block i+1's scores (the last iteration computes a throwaway product of the other
+        // K buffer: an unconditional MFMA burst keeps this one basic block for the scheduler)
+        f32x16 snext;
+        X3P_QK(snext, (i + 1) & 1)
+        const float mc = m * scale_log2e;
         float psum = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          sacc[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], scale_log2e, -mc));
-          psum += sacc[r];
+          scur[r] = __builtin_amdgcn_exp2f(fmaf(scur[r], scale_log2e, -mc));
+          psum += scur[r];
         }
         psum += __shfl_xor(psum, 32, 64);
-        l = l * alpha + psum;
-        m = m_new;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          o0[r] *= alpha;
-          o1[r] *= alpha;
-        }
-        const __bf16* vs = &lds_v[buf * 3 * XV_PLANE + vtr];
+        l += psum;
+        const __bf16* vs = &lds_v[(i & 1) * 3 * XV_PLANE + vtr];
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const f32x8 pv8 = {sacc[8 * s2 + 0], sacc[8 * s2 + 1], sacc[8 * s2 + 2], sacc[8 * s2 + 3],
-                             sacc[8 * s2 + 4], sacc[8 * s2 + 5], sacc[8 * s2 + 6], sacc[8 * s2 + 7]};
           bf16x8 p0, p1, p2;
-          split3(pv8, p0, p1, p2);
+          split3_trunc8(scur, 8 * s2, p0, p1, p2);
 #pragma unroll
           for (int dh = 0; dh < 2; ++dh) {
             bf16x8 vf[3];
@@ -795,10 +1018,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
               o1 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o1);
           }
         }
+        scur = snext;
       }
-      if (more) stash(buf ^ 1);
+      if (more_k) stash_k(i & 1);
+      if (more_v) stash_v((i + 1) & 1);
       __syncthreads();
     }
+#undef X3P_QK
 
     if (active) {
       if (kb0 == 0 && kb1 == NK) {
@@ -862,10 +1088,20 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
   return check_launch("split3_f32");
 }
 
+static int g_x3_pipelined = 1;
+
+// 1 = software-pipelined x3 kernel (default), 0 = the block-at-a-time x3 kernel (A/B reference)
+int nos_attention_x3_set_pipelined(int on) {
+  g_x3_pipelined = on ? 1 : 0;
+  return 0;
+}
+
 // workgroups per CU of the x3 attention kernel (persistent grid = this x slice CUs)
 int nos_attention_x3_wg_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3, 256, 0) != hipSuccess || n <= 0) n = 1;
+  const hipError_t e = g_x3_pipelined ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3p, 256, 0)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3, 256, 0);
+  if (e != hipSuccess || n <= 0) n = 1;
   return n;
 }
 
@@ -896,8 +1132,12 @@ int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void*
   float* part_o = ws;
   float* part_ml = ws + size_t(waves) * 8 * HD * 32;
   __bf16* op = reinterpret_cast<__bf16*>(outp);
-  hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3), plane_stride,
-                     out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+  if (g_x3_pipelined)
+    hipLaunchKernelGGL(attn_fwd_x3p, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3),
+                       plane_stride, out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+  else
+    hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3),
+                       plane_stride, out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
                      op);

@@ -230,12 +230,17 @@ def test_attention_x3_fp32_accurate_any_grid(K, T, H, B):
     K.attention_sk(qkv, f32, H, 64, 0.125, 256)
     torch.cuda.synchronize()
     err_f32 = (f32 - ref).abs().max().item()
-    for waves in (1, 3, 7, 64, 333, 512, units + 5):
-        out = torch.full((B, T, H * 64), float("nan"), device="cuda")
-        K.attention_x3(planes, out, H, 64, 0.125, waves)
-        torch.cuda.synchronize()
-        err = (out - ref).abs().max().item()
-        assert err < max(2.0 * err_f32, 2e-6), (waves, err, err_f32)
+    try:
+        for pipelined in (True, False):
+            K.set_attention_x3_pipelined(pipelined)
+            for waves in (1, 3, 7, 64, 333, 512, units + 5):
+                out = torch.full((B, T, H * 64), float("nan"), device="cuda")
+                K.attention_x3(planes, out, H, 64, 0.125, waves)
+                torch.cuda.synchronize()
+                err = (out - ref).abs().max().item()
+                assert err < max(2.0 * err_f32, 2e-6), (pipelined, waves, err, err_f32)
+    finally:
+        K.set_attention_x3_pipelined(True)
 
 
 def test_attention_x3_asymmetric_values(K):

@@ -112,6 +112,10 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
     r["attn_x3_grid"] = wx
     for mult in (1, 2):
         r[f"attn_x3g{mult}_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, mult * n), s, iters)
+    K.set_attention_x3_pipelined(False)
+    wnp = K.attention_x3_waves(n, 1, T, H)
+    r["attn_x3np_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, wnp), s, iters)
+    K.set_attention_x3_pipelined(True)
     r["split3_qkv_us"] = timeit(lambda: K.split3(qkv), s, iters)
     r["attn_sdpa_us"] = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), s, iters)
     for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")
@@ -159,9 +163,9 @@ def gemm_bench(r, x, h, w_qkv, w_o, w_1, w_2, b_ff, b_qkv, b_d, s, iters):
         x3_out = gname in ("qkv", "fc1")
         for cfg in G.x3_eligible(wa.shape[0], wa.shape[1]):
             us = timeit(lambda: G.gemm_x3(xa3, wa, tile=cfg, out_f32=not x3_out, out_x3=x3_out, **kw), s, iters)
-            bm, bn, nb = G.X3_TILES[cfg]
-            r[f"x3_{gname}_{bm}x{bn}b{nb}_us"] = round(us, 1)
-            r[f"x3_{gname}_{bm}x{bn}b{nb}_tflops"] = round(fl / us / 1e6, 2)
+            bm, bn, nb, kind = G.X3_TILES[cfg]
+            r[f"x3_{gname}_{bm}x{bn}{kind}b{nb}_us"] = round(us, 1)
+            r[f"x3_{gname}_{bm}x{bn}{kind}b{nb}_tflops"] = round(fl / us / 1e6, 2)
 
 
 if __name__ == "__main__":

@@ -197,11 +197,14 @@ def tuning_table() -> Dict[str, str]:
 
 
 # ---- x3: fp32-accurate GEMM on the bf16 matrix cores (csrc/gemm_x3.hip) -------------------------
-#: config -> (BM, BN, LDS buffers)
-X3_TILES = {0: (64, 64, 2), 1: (128, 64, 2), 2: (64, 128, 2), 3: (128, 128, 2),
-            4: (64, 64, 1), 5: (128, 64, 1), 6: (64, 128, 1)}
-#: resident workgroups per CU (LDS-limited: 60/90/120 KB double-buffered, 30/45 KB single)
-X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3}
+#: config -> (BM, BN, LDS buffers, pipeline): "r" = register-staged loads one stage ahead,
+#: "d" = LDS-DMA (global_load_lds) with nbuf-1 stages in flight
+X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: (128, 128, 2, "r"),
+            4: (64, 64, 1, "r"), 5: (128, 64, 1, "r"), 6: (64, 128, 1, "r"),
+            7: (64, 64, 3, "d"), 8: (64, 64, 4, "d"), 9: (128, 64, 3, "d"), 10: (64, 128, 3, "d"),
+            11: (128, 128, 3, "d"), 12: (64, 64, 2, "d")}
+#: resident workgroups per CU (LDS- or VGPR-limited)
+X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
@@ -238,13 +241,13 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
 def x3_eligible(N: int, Kd: int) -> list:
     if Kd % 32:
         return []
-    return [c for c, (bm, bn, _) in X3_TILES.items() if N % bn == 0]
+    return [c for c, (bm, bn, _, _) in X3_TILES.items() if N % bn == 0]
 
 
 def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
     best, best_key = cands[0], None
     for c in cands:
-        bm, bn, _ = X3_TILES[c]
+        bm, bn, _, _ = X3_TILES[c]
         tiles = -(-M // bm) * (N // bn)
         rounds = -(-tiles // (X3_SLOTS_PER_CU[c] * cus))
         key = (rounds * bm * bn / min(X3_SLOTS_PER_CU[c], 2), -bm * bn)

@@ -113,6 +113,13 @@ def split3(x: torch.Tensor) -> torch.Tensor:
 _x3_wg: Optional[int] = None
 
 
+def set_attention_x3_pipelined(on: bool) -> None:
+    """True (default): the software-pipelined x3 attention kernel; False: block-at-a-time (A/B)."""
+    global _x3_wg
+    _check(_L().nos_attention_x3_set_pipelined(1 if on else 0))
+    _x3_wg = None
+
+
 def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
     """Persistent grid of the x3 attention kernel (same sizing rule as the f32 LDS kernel)."""
     global _x3_wg
@@ -179,6 +186,7 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
+            L.nos_attention_x3_set_pipelined.argtypes = [i32]
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             _lib = L
         return _lib
