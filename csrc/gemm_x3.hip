@@ -18,6 +18,7 @@
 //    as fp32 and/or as three bf16 planes (split in registers) for the next x3 consumer.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -215,6 +216,43 @@ int launch(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* 
   return 0;
 }
 
+// Fused epilogue of a wave's TM x TN accumulators at rows r0.., columns c0..: register r of
+// acc[a][b] is C[r0 + 32a + acc_row(r, hf)][c0 + 32b + j]; bias, exact GELU, residuals; fp32 and/or
+// x3 planes out.
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][TN], int r0, int c0, int j, int hf,
+                                           const float* __restrict__ bias, const float* __restrict__ R,
+                                           const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
+                                           __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int epi) {
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = c0 + 32 * b + j;
+    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = r0 + 32 * a + acc_row(r, hf);
+        if (row >= M) continue;
+        float v = acc[a][b][r] + bv;
+        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+        const size_t idx = size_t(row) * N + col;
+        if (epi & EPI_RES) v += R[idx];
+        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];
+        if (C) C[idx] = v;
+        if (Cp) {
+          const __bf16 h0 = (__bf16)v;
+          const float r1 = v - (float)h0;
+          const __bf16 h1 = (__bf16)r1;
+          Cp[idx] = h0;
+          Cp[c_plane + idx] = h1;
+          Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
+        }
+      }
+    }
+  }
+}
+
 // ---- LDS-DMA variant ---------------------------------------------------------------------------
 // Same math and epilogue; the operand tiles go global -> LDS with global_load_lds_dwordx4 (no
 // register staging), S LDS buffers deep, so S-1 stages of loads are in flight behind the MFMAs at
@@ -239,19 +277,33 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// one stage of ROWS x 32 bf16 per plane for this wave: row groups g = wave, wave+4, ... of 16 rows
-template <int ROWS>
-__device__ __forceinline__ void dma_stage(const __bf16* __restrict__ X, size_t plane, int r0, int rmax, int K, int k0,
-                                          __bf16* lds, int wave, int lane) {
+// Per-lane byte offsets of this wave's DMA rows inside one plane (fixed for the whole K loop):
+// row groups g = wave + 4i of 16 rows; lane -> row 16g + lane/4, k-chunk (lane%4) ^ ((lane/16)%4).
+template <int ROWS, int NW>
+__device__ __forceinline__ void dma_offsets(uint32_t (&voff)[ROWS / 16 / NW], int r0, int rmax, int K, int wave,
+                                            int lane) {
   const int rl = lane >> 2, c = (lane & 3) ^ ((lane >> 4) & 3);
 #pragma unroll
-  for (int i = 0; i < ROWS / 64; ++i) {
-    const int g = wave + 4 * i;
-    const int row = min(r0 + 16 * g + rl, rmax);
-    const __bf16* src = X + size_t(row) * K + k0 + 8 * c;
+  for (int i = 0; i < ROWS / 16 / NW; ++i) {
+    const int row = min(r0 + 16 * (wave + NW * i) + rl, rmax);
+    voff[i] = uint32_t(row) * uint32_t(K) * 2u + 16u * uint32_t(c);
+  }
+}
+
+// one stage of ROWS x 32 bf16 per plane for this wave (NW waves share the row groups): a wave-uniform base (plane, k0) plus the
+// lane's fixed 32-bit offset, so the loads take the SGPR-base + VGPR-offset form and a stage costs
+// no per-lane address arithmetic
+template <int ROWS, int NW>
+__device__ __forceinline__ void dma_stage(const __bf16* __restrict__ X, size_t plane,
+                                          const uint32_t (&voff)[ROWS / 16 / NW], int k0, __bf16* lds, int wave) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      __builtin_amdgcn_global_load_lds(src + q * plane, (lds_void*)(lds + q * ROWS * 32 + 16 * g * 32), 16, 0, 0);
+  for (int i = 0; i < ROWS / 16 / NW; ++i) {
+    const int g = wave + NW * i;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const char* src = reinterpret_cast<const char*>(X + q * plane + k0) + voff[i];
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(lds + q * ROWS * 32 + 16 * g * 32), 16, 0, 0);
+    }
   }
 }
 
@@ -282,17 +334,21 @@ __device__ __forceinline__ void compute_stage_sw(f32x16 (&acc)[WM / 32][WN / 32]
   }
 }
 
-template <int WM, int WN, int S>
-__global__ __launch_bounds__(256, 1) void gemm_x3d(const __bf16* __restrict__ A, size_t a_plane,
+// BM x BN tile on a WGM x WGN grid of waves (4 or 8 waves: 8 gives each SIMD two waves of one
+// workgroup, so a 128x128 tile — half the bytes per MFMA of 64x64 — still hides its load latency)
+template <int BM, int BN, int WGM, int WGN, int S>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __restrict__ A, size_t a_plane,
                                                   const __bf16* __restrict__ W, size_t w_plane,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
                                                   const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
                                                   __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int K,
                                                   int epi) {
   static_assert(S >= 2 && S <= 4, "2-4 LDS stages");
-  constexpr int BM = 2 * WM, BN = 2 * WN;
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int NLD = 3 * (BM / 64) + 3 * (BN / 64);  // DMA instructions per wave per stage
+  static_assert(BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "row groups must divide over the waves");
+  constexpr int NLD = 3 * (BM / 16 / NW) + 3 * (BN / 16 / NW);  // DMA instructions per wave per stage
   // one __shared__ object per stage buffer: the compiler's LDS-DMA wait tracking can then tell the
   // buffer being read from the buffers being filled (one array indexed by stage would make every
   // fragment read wait for ALL outstanding DMA, vmcnt(0), and serialise the pipeline)
@@ -307,8 +363,9 @@ __global__ __launch_bounds__(256, 1) void gemm_x3d(const __bf16* __restrict__ A,
   if (t >= tiles) return;
   const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
+  const int wm = wave / WGN, wn = wave % WGN;
   const int j = lane & 31, hf = lane >> 5;
 
   f32x16 acc[TM][TN];
@@ -318,14 +375,17 @@ __global__ __launch_bounds__(256, 1) void gemm_x3d(const __bf16* __restrict__ A,
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
 
   const int nk = K / BK;
+  uint32_t voff_a[BM / 16 / NW], voff_b[BN / 16 / NW];
+  dma_offsets<BM, NW>(voff_a, m0, M - 1, K, wave, lane);
+  dma_offsets<BN, NW>(voff_b, n0, N - 1, K, wave, lane);
 #define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
 #define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
 // past the end a stage re-reads the last one, so every iteration issues NLD loads (static vmcnt)
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
     const int k0_ = min((STAGE), nk - 1) * BK;                                     \
-    dma_stage<BM>(A, a_plane, m0, M - 1, K, k0_, X3D_A(BUF), wave, lane);          \
-    dma_stage<BN>(W, w_plane, n0, N - 1, K, k0_, X3D_B(BUF), wave, lane);          \
+    dma_stage<BM, NW>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave);                 \
+    dma_stage<BN, NW>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);                 \
   }
 #define X3D_ITER(KS, BUF)                                                          \
   {                                                                                \
@@ -353,52 +413,132 @@ __global__ __launch_bounds__(256, 1) void gemm_x3d(const __bf16* __restrict__ A,
 #undef X3D_B
 #undef X3D_A
   vm_wait<0>();  // no DMA may still target this workgroup's LDS when it retires
-
-  // epilogue: acc[a][b] register r is C[m0 + wm*WM + 32a + acc_row(r, hf)][n0 + wn*WN + 32b + j]
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int col = n0 + wn * WN + 32 * b + j;
-    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + 32 * a + acc_row(r, hf);
-        if (row >= M) continue;
-        float v = acc[a][b][r] + bv;
-        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-        const size_t idx = size_t(row) * N + col;
-        if (epi & EPI_RES) v += R[idx];
-        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];
-        if (C) C[idx] = v;
-        if (Cp) {
-          const __bf16 h0 = (__bf16)v;
-          const float r1 = v - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          Cp[idx] = h0;
-          Cp[c_plane + idx] = h1;
-          Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
-        }
-      }
-    }
-  }
+  store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
-template <int WM, int WN, int S>
+template <int BM, int BN, int WGM, int WGN, int S>
 int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
              const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
              hipStream_t s) {
-  constexpr int BM = 2 * WM, BN = 2 * WN;
   if (N % BN) {
     g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
     return -1;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3d<WM, WN, S>), dim3(tiles), dim3(256), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
+  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S>), dim3(tiles), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
                      cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("gemm_x3d: ") + hipGetErrorString(e);
+    return int(e);
+  }
+  return 0;
+}
+
+// Persistent (stream-of-stages) LDS-DMA GEMM: a grid of P workgroups, workgroup w owning tiles
+// w, w+P, ...; its (tile, k-stage) pairs form one continuous stage stream, so the DMA ring keeps
+// loading the next tile's first stages while the current tile's last MFMAs and its epilogue run —
+// the fill/drain every short-K (K = 384: 12 stages) tile otherwise pays once per tile.
+template <int BM, int BN, int WGM, int WGN, int S>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __restrict__ A, size_t a_plane,
+                                                              const __bf16* __restrict__ W, size_t w_plane,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ R,
+                                                              const float* __restrict__ R2, int r2_rows,
+                                                              float* __restrict__ C, __bf16* __restrict__ Cp,
+                                                              size_t c_plane, int M, int N, int K, int epi) {
+  static_assert(S >= 2 && S <= 4, "2-4 LDS stages");
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  static_assert(BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "row groups must divide over the waves");
+  constexpr int NLD = 3 * (BM / 16 / NW) + 3 * (BN / 16 / NW);
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * 32], A1[3 * BM * 32], A2[S > 2 ? 3 * BM * 32 : 8],
+      A3[S > 3 ? 3 * BM * 32 : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * 32], B1[3 * BN * 32], B2[S > 2 ? 3 * BN * 32 : 8],
+      B3[S > 3 ? 3 * BN * 32 : 8];
+
+  const int tiles_n = N / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int P = gridDim.x, w = blockIdx.x;
+  if (w >= tiles) return;
+  const int nk = K / BK;
+  const int total = ((tiles - w + P - 1) / P) * nk;  // this workgroup's stages
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int j = lane & 31, hf = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
+
+#define X3S_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
+#define X3S_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
+// stage h of the stream (past the end: the last stage again, so vmcnt accounting stays static)
+#define X3S_ISSUE(H, BUF)                                                                 \
+  {                                                                                       \
+    const int h_ = min((H), total - 1);                                                   \
+    const int ti_ = h_ / nk, ks_ = h_ - ti_ * nk, t_ = w + ti_ * P;                       \
+    uint32_t va_[BM / 16 / NW], vb_[BN / 16 / NW];                                        \
+    dma_offsets<BM, NW>(va_, (t_ / tiles_n) * BM, M - 1, K, wave, lane);                  \
+    dma_offsets<BN, NW>(vb_, (t_ % tiles_n) * BN, N - 1, K, wave, lane);                  \
+    dma_stage<BM, NW>(A, a_plane, va_, ks_ * BK, X3S_A(BUF), wave);                       \
+    dma_stage<BN, NW>(W, w_plane, vb_, ks_ * BK, X3S_B(BUF), wave);                       \
+  }
+#define X3S_ITER(G, BUF)                                                                  \
+  {                                                                                       \
+    vm_wait<(S - 2) * NLD>();                                                             \
+    raw_barrier();                                                                        \
+    X3S_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
+    compute_stage_sw<BM, BN, WM, WN>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);         \
+    if (((G) + 1) % nk == 0) {                                                            \
+      const int t_ = w + ((G) / nk) * P;                                                  \
+      store_tile<TM, TN>(acc, (t_ / tiles_n) * BM + wm * WM, (t_ % tiles_n) * BN + wn * WN, j, hf, bias, R, R2, \
+                         r2_rows, C, Cp, c_plane, M, N, epi);                             \
+      _Pragma("unroll") for (int a = 0; a < TM; ++a)                                      \
+        _Pragma("unroll") for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};             \
+    }                                                                                     \
+  }
+  X3S_ISSUE(0, 0)
+  if constexpr (S > 2) X3S_ISSUE(1, 1)
+  if constexpr (S > 3) X3S_ISSUE(2, 2)
+  int g = 0;
+  for (; g + S <= total; g += S) {
+    X3S_ITER(g, 0)
+    X3S_ITER(g + 1, 1)
+    if constexpr (S > 2) X3S_ITER(g + 2, 2)
+    if constexpr (S > 3) X3S_ITER(g + 3, 3)
+  }
+  if (g < total) X3S_ITER(g, 0)
+  if (g + 1 < total) X3S_ITER(g + 1, 1)
+  if constexpr (S > 3)
+    if (g + 2 < total) X3S_ITER(g + 2, 2)
+#undef X3S_ITER
+#undef X3S_ISSUE
+#undef X3S_B
+#undef X3S_A
+  vm_wait<0>();
+}
+
+template <int BM, int BN, int WGM, int WGN, int S>
+int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
+             const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi, int grid,
+             hipStream_t s) {
+  if (N % BN) {
+    g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
+    return -1;
+  }
+  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  const int g = std::max(1, std::min(grid, tiles));
+  hipLaunchKernelGGL((gemm_x3s<BM, BN, WGM, WGN, S>), dim3(g), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2,
+                     r2_rows, C, Cp, cp, M, N, K, epi);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("gemm_x3s: ") + hipGetErrorString(e);
     return int(e);
   }
   return 0;
@@ -413,15 +553,45 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // 2 = 64x128, 3 = 128x128 (double-buffered LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered:
 // half the LDS, more resident tiles); 7-12 = LDS-DMA pipeline with nbuf = S stages (S-1 in
 // flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2.
-static const int kCfgX3[13][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+static const int kCfgX3[15][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
-                                  {128, 128, 3}, {64, 64, 2}};
+                                  {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2}};
 
-int nos_gemm_x3_num_configs() { return 13; }
+int nos_gemm_x3_num_configs() { return 15; }
+
+// Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
+// (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
+// cfg: 0 = 64x64 S3 (4 waves), 1 = 64x64 S2, 2 = 128x128 S3 (8 waves), 3 = 64x128 S3, 4 = 128x64 S3.
+int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, const float* bias, const float* R,
+                           const float* R2, int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi,
+                           int cfg, int grid, void* stream) {
+  if (K % BK || ap % 8 || wp % 8 || cp % 8 || (!C && !Cp)) {
+    g_err = "gemm_x3s: K % 32, plane strides % 8, and an output are required";
+    return -1;
+  }
+  if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R) || ((epi & EPI_RES2) && (!R2 || r2_rows <= 0))) {
+    g_err = "gemm_x3s: epilogue operand missing";
+    return -1;
+  }
+  const __bf16* a = reinterpret_cast<const __bf16*>(A);
+  const __bf16* w = reinterpret_cast<const __bf16*>(W);
+  __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (cfg) {
+    case 0: return launch_s<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 1: return launch_s<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 2: return launch_s<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 3: return launch_s<64, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 4: return launch_s<128, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    default:
+      g_err = "gemm_x3s: unknown config";
+      return -1;
+  }
+}
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 12) return -1;
+  if (cfg < 0 || cfg > 14) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -459,12 +629,14 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 4: return launch<32, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 5: return launch<64, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 6: return launch<32, 64, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 7: return launch_d<32, 32, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 8: return launch_d<32, 32, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 9: return launch_d<64, 32, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 10: return launch_d<32, 64, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 11: return launch_d<64, 64, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 12: return launch_d<32, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 7: return launch_d<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 8: return launch_d<64, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 9: return launch_d<128, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 10: return launch_d<64, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 11: return launch_d<128, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 12: return launch_d<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 13: return launch_d<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 14: return launch_d<128, 128, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

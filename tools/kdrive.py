@@ -28,6 +28,7 @@ def main() -> int:
                     choices=("attn_x3", "attn_f32", "qkv_x3", "proj_x3", "fc1_x3", "fc2_x3", "layernorm_x3"))
     ap.add_argument("--slice", default="spx", choices=tuple(PROFILES))
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--tile", type=int, default=None, help="force an x3 GEMM tile config (no autotune dispatches)")
     a = ap.parse_args()
     torch.manual_seed(0)
     cus = slice_cus(PROFILES[a.slice], 0)
@@ -45,7 +46,7 @@ def main() -> int:
             w = torch.randn(N, xa.shape[1], device="cuda") * 0.05
             b = torch.randn(N, device="cuda")
             xa3 = K.split3(xa)
-            fn = lambda: G.gemm_x3(xa3, w, b, gelu=gelu, out_f32=not out3, out_x3=out3)  # noqa: E731
+            fn = lambda: G.gemm_x3(xa3, w, b, gelu=gelu, out_f32=not out3, out_x3=out3, tile=a.tile)  # noqa: E731
         elif a.op == "attn_x3":
             fn = lambda: K.attention_qkv_x3(planes, H, 64, 0.125)  # noqa: E731
         elif a.op == "attn_f32":

@@ -198,13 +198,18 @@ def tuning_table() -> Dict[str, str]:
 
 # ---- x3: fp32-accurate GEMM on the bf16 matrix cores (csrc/gemm_x3.hip) -------------------------
 #: config -> (BM, BN, LDS buffers, pipeline): "r" = register-staged loads one stage ahead,
-#: "d" = LDS-DMA (global_load_lds) with nbuf-1 stages in flight
+#: "d" = LDS-DMA (global_load_lds) with nbuf-1 stages in flight, "d8" = the same with 8 waves
 X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: (128, 128, 2, "r"),
             4: (64, 64, 1, "r"), 5: (128, 64, 1, "r"), 6: (64, 128, 1, "r"),
             7: (64, 64, 3, "d"), 8: (64, 64, 4, "d"), 9: (128, 64, 3, "d"), 10: (64, 128, 3, "d"),
-            11: (128, 128, 3, "d"), 12: (64, 64, 2, "d")}
+            11: (128, 128, 3, "d"), 12: (64, 64, 2, "d"),
+            13: (128, 128, 3, "d8"), 14: (128, 128, 2, "d8"),
+            # persistent stream-of-stages (grid = resident slots of the slice)
+            100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
+            104: (128, 64, 3, "p")}
 #: resident workgroups per CU (LDS- or VGPR-limited)
-X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3}
+X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
+                   13: 1, 14: 1, 100: 2, 101: 3, 102: 1, 103: 1, 104: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
@@ -215,6 +220,8 @@ def _lib_x3() -> ctypes.CDLL:
     if not _x3_bound:
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
         L.nos_gemm_x3.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32, vp]
+        L.nos_gemm_x3_persistent.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32,
+                                             i32, vp]
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         _x3_bound = True
     return L
@@ -259,13 +266,19 @@ def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
 def _launch_x3(cfg, a3, w3, bias, res, r2, out, out3, epi) -> None:
     _, M, Kd = a3.shape
     N = w3.shape[1]
-    rc = _lib_x3().nos_gemm_x3(a3.data_ptr(), a3[0].numel(), w3.data_ptr(), w3[0].numel(),
-                               bias.data_ptr() if bias is not None else None,
-                               res.data_ptr() if res is not None else None,
-                               r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
-                               out.data_ptr() if out is not None else None,
-                               out3.data_ptr() if out3 is not None else None, out3[0].numel() if out3 is not None else 0,
-                               M, N, Kd, epi, cfg, torch.cuda.current_stream().cuda_stream)
+    args = (a3.data_ptr(), a3[0].numel(), w3.data_ptr(), w3[0].numel(),
+            bias.data_ptr() if bias is not None else None,
+            res.data_ptr() if res is not None else None,
+            r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+            out.data_ptr() if out is not None else None,
+            out3.data_ptr() if out3 is not None else None, out3[0].numel() if out3 is not None else 0,
+            M, N, Kd, epi)
+    stream = torch.cuda.current_stream().cuda_stream
+    if cfg >= 100:
+        grid = X3_SLOTS_PER_CU[cfg] * K.slice_cus()
+        rc = _lib_x3().nos_gemm_x3_persistent(*args, cfg - 100, grid, stream)
+    else:
+        rc = _lib_x3().nos_gemm_x3(*args, cfg, stream)
     if rc != 0:
         raise RuntimeError(f"nos gemm_x3 failed: {_lib_x3().nos_gemm_x3_last_error().decode()} (rc={rc})")
 
