@@ -50,8 +50,11 @@ class Reporter:
             return Result()
         devices = self.pc.get_partition_devices()
         new_status = devices.as_status_annotation(self.extract)
-        old_status, _ = ann.parse_node_annotations(ko.annotations(node))
         anns = ko.annotations(node)
+        # order-insensitive comparison of the rendered status family (reporter.go:80-85's
+        # UnorderedEqual of parsed annotations, done on the key -> value map directly)
+        new_map = {s.key: s.value() for s in new_status}
+        old_map = {k: v for k, v in anns.items() if k.startswith(api.ANNOTATION_GPU_STATUS_PREFIX)}
         desired_extra: Dict[str, str] = {}
         nps = self._nps()
         if nps:
@@ -61,7 +64,7 @@ class Reporter:
         if self.extra is not None:
             desired_extra.update(self.extra())
         extra_same = all(anns.get(k) == v for k, v in desired_extra.items())
-        if ann.annotations_equal(new_status, old_status) and extra_same and \
+        if new_map == old_map and extra_same and \
                 anns.get(api.ANNOTATION_REPORTED_PARTITIONING_PLAN) == self.shared.last_parsed_plan_id:
             return Result(requeue_after=self.refresh_interval)
         updated = ko.deepcopy(node)

@@ -40,10 +40,25 @@ log = logging.getLogger("nos.partitioner")
 NodeModel = Union[PartitionedNode, SlicingNode]
 
 
+_REQ_CACHE: Dict[Tuple[str, str], Dict[str, int]] = {}
+
+
 def requested_profiles(kind: str, pod: Dict[str, Any]) -> Dict[str, int]:
-    if kind == api.PARTITIONING_KIND_XCP:
-        return xcp_node.get_requested_profiles(pod)
-    return slicing_gpu.get_requested_profiles(pod)
+    """Profiles a pod requests. Container requests are immutable once a pod exists, so the result
+    is memoised per pod UID (the planner re-reads every pending pod on every reconcile)."""
+    uid = pod.get("metadata", {}).get("uid")
+    key = (kind, uid) if uid else None
+    if key is not None:
+        hit = _REQ_CACHE.get(key)
+        if hit is not None:
+            return dict(hit)
+    out = xcp_node.get_requested_profiles(pod) if kind == api.PARTITIONING_KIND_XCP \
+        else slicing_gpu.get_requested_profiles(pod)
+    if key is not None:
+        if len(_REQ_CACHE) > 100_000:
+            _REQ_CACHE.clear()
+        _REQ_CACHE[key] = dict(out)
+    return out
 
 
 def new_node_model(kind: str, node: Dict[str, Any], scoring: str = "fraction") -> NodeModel:
@@ -230,11 +245,12 @@ class PodController:
         return podutil.is_pending(pod) and not podutil.is_scheduled(pod) and podutil.is_unschedulable(pod)
 
     def list_nodes(self) -> List[Dict[str, Any]]:
-        return self.client.list("Node", label_selector=f"{api.LABEL_GPU_PARTITIONING}={self.kind}")
+        return self.client.list("Node", label_selector=f"{api.LABEL_GPU_PARTITIONING}={self.kind}", copy=False)
 
     def pending_pods(self) -> List[Dict[str, int]]:
         """Per-pod requested profiles of the unschedulable pods, highest priority then oldest first."""
-        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending") if self.should_consider(p)]
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if self.should_consider(p)]
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
         out = []
         for p in pods:
@@ -245,7 +261,7 @@ class PodController:
 
     def pending_requests(self) -> Dict[str, int]:
         out: Dict[str, int] = {}
-        for p in self.client.list("Pod", field_selector="status.phase=Pending"):
+        for p in self.client.list("Pod", field_selector="status.phase=Pending", copy=False):
             if not self.should_consider(p):
                 continue
             for k, v in requested_profiles(self.kind, p).items():
@@ -305,6 +321,7 @@ class PodController:
 
     # -- reconcile ----------------------------------------------------------------------
     def reconcile(self, req: Request) -> Result:
+        pending: Optional[List[Dict[str, int]]] = None
         if req == self.plan_key:
             pending = self.pending_pods()
             if not pending:
@@ -354,7 +371,9 @@ class PodController:
                 for p, q in self.incoming_free(n).items():
                     incoming[p] = incoming.get(p, 0) + q
             planner = plan_cluster_fifo if self.policy == "fifo" else plan_cluster_simulate
-            changed = planner(models, self.pending_pods() or [requested], incoming)
+            if pending is None:
+                pending = self.pending_pods()
+            changed = planner(models, pending or [requested], incoming)
             need = requested
         else:
             pending = self.pending_requests() or requested

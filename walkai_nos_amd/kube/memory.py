@@ -84,6 +84,7 @@ class InMemoryAPIServer:
     def __init__(self, clock: Callable[[], float] = time.time):
         self._lock = threading.RLock()
         self._objs: Dict[Tuple[str, str, str], Obj] = {}
+        self._by_kind: Dict[str, Dict[Tuple[str, str, str], Obj]] = {}  # kind index of _objs
         self._rv = itertools.count(1)
         self._handlers: Dict[str, List[Handler]] = {}
         self.clock = clock
@@ -94,7 +95,7 @@ class InMemoryAPIServer:
     def watch(self, kind: str, handler: Handler, replay: bool = True) -> Callable[[], None]:
         with self._lock:
             self._handlers.setdefault(kind, []).append(handler)
-            existing = [fast_copy(o) for (k, _, _), o in self._objs.items() if k == kind] if replay else []
+            existing = [fast_copy(o) for o in self._by_kind.get(kind, {}).values()] if replay else []
         for o in existing:
             handler("ADDED", o, None)
 
@@ -107,10 +108,15 @@ class InMemoryAPIServer:
         return cancel
 
     def _emit(self, kind: str, etype: str, obj: Obj, old: Optional[Obj]) -> None:
+        """Deliver one event to every watcher. The handlers of one event share a single copy of
+        the objects (watch handlers only map events to requests; they must not mutate them)."""
         with self._lock:
             handlers = list(self._handlers.get(kind, []))
+        if not handlers:
+            return
+        o, prev = fast_copy(obj), (fast_copy(old) if old is not None else None)
         for h in handlers:
-            h(etype, fast_copy(obj), fast_copy(old) if old is not None else None)
+            h(etype, o, prev)
 
     # ---- CRUD -------------------------------------------------------------------------
     @staticmethod
@@ -138,6 +144,7 @@ class InMemoryAPIServer:
             md.setdefault("labels", md.get("labels") or {})
             md.setdefault("annotations", md.get("annotations") or {})
             self._objs[k] = o
+            self._by_kind.setdefault(kind, {})[k] = o
             self.stats["create"] += 1
             out = fast_copy(o)
         self._emit(kind, "ADDED", out, None)
@@ -152,20 +159,22 @@ class InMemoryAPIServer:
             return fast_copy(o)
 
     def list(self, kind: str, namespace: Optional[str] = None, label_selector: Optional[str] = None,
-             field_selector: Optional[str] = None) -> List[Obj]:
+             field_selector: Optional[str] = None, copy: bool = True) -> List[Obj]:
+        """Objects of ``kind`` matching the selectors, sorted by (namespace, name). ``copy=False``
+        returns the stored objects themselves — for read-only callers on hot paths (the stored
+        objects are never mutated in place: every write replaces them), like controller-runtime's
+        cache reads with deep copies disabled."""
         with self._lock:
             self.stats["list"] += 1
             out = []
-            for (k, ns, _), o in self._objs.items():
-                if k != kind:
-                    continue
+            for (_, ns, _), o in self._by_kind.get(kind, {}).items():
                 if namespace and kind in NAMESPACED and ns != namespace:
                     continue
                 if not ko.selector_matches(label_selector, ko.labels(o)):
                     continue
                 if not ko.field_selector_matches(field_selector, o):
                     continue
-                out.append(fast_copy(o))
+                out.append(fast_copy(o) if copy else o)
         out.sort(key=lambda o: (ko.namespace(o), ko.name(o)))
         return out
 
@@ -186,6 +195,7 @@ class InMemoryAPIServer:
                 return fast_copy(old)
             md["resourceVersion"] = str(next(self._rv))
             self._objs[k] = new
+            self._by_kind.setdefault(kind, {})[k] = new
             out, prev = fast_copy(new), fast_copy(old)
         self._emit(kind, "MODIFIED", out, prev)
         return out
@@ -221,6 +231,7 @@ class InMemoryAPIServer:
             o = self._objs.pop(k, None)
             if o is None:
                 raise NotFound(f"{kind} {namespace}/{name} not found")
+            self._by_kind.get(kind, {}).pop(k, None)
             self.stats["delete"] += 1
         self._emit(kind, "DELETED", o, None)
 

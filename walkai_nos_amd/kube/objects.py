@@ -7,6 +7,8 @@ API server (:mod:`walkai_nos_amd.kube.memory`) and a real cluster
 """
 from __future__ import annotations
 
+import functools
+
 import copy
 import datetime as _dt
 from typing import Any, Dict, Iterable, List, Optional, Tuple
@@ -126,8 +128,14 @@ def match_labels(selector: Optional[Dict[str, str]], lbls: Dict[str, str]) -> bo
     return all(lbls.get(k) == v for k, v in selector.items())
 
 
-def parse_label_selector(sel: str) -> List[Tuple[str, str, Optional[str]]]:
-    """Parse ``a=b,c!=d,e`` (equality-based + existence) selectors."""
+@functools.lru_cache(maxsize=1024)
+def parse_label_selector(sel: str) -> Tuple[Tuple[str, str, Optional[str]], ...]:
+    """Parse ``a=b,c!=d,e`` (equality-based + existence) selectors (memoised: controllers reuse a
+    handful of selector strings on every list)."""
+    return tuple(_parse_label_selector(sel))
+
+
+def _parse_label_selector(sel: str) -> List[Tuple[str, str, Optional[str]]]:
     out: List[Tuple[str, str, Optional[str]]] = []
     for part in filter(None, (p.strip() for p in sel.split(","))):
         if "!=" in part:

@@ -6,6 +6,8 @@ to :class:`fractions.Fraction` and expose helpers for the two common views.
 """
 from __future__ import annotations
 
+import functools
+
 import re
 from fractions import Fraction
 from typing import Union
@@ -42,10 +44,15 @@ def parse_quantity(q: QuantityLike) -> Fraction:
         return Fraction(q)
     if isinstance(q, float):
         return Fraction(q).limit_denominator(10**9)
-    s = str(q).strip()
+    return _parse_str(str(q).strip())
+
+
+@functools.lru_cache(maxsize=4096)
+def _parse_str(s: str) -> Fraction:
+    """Memoised string parse: a cluster's pods repeat a handful of quantity strings."""
     m = _RE.match(s)
     if not m:
-        raise ValueError(f"invalid quantity {q!r}")
+        raise ValueError(f"invalid quantity {s!r}")
     num, suf = m.group(1), m.group(2) or ""
     return Fraction(num) * _SUFFIX[suf]
 

@@ -115,7 +115,8 @@ class RESTClient:
         return self._with_kind(self._req("GET", self._path(kind, name, namespace)), kind)
 
     def list(self, kind: str, namespace: Optional[str] = None, label_selector: Optional[str] = None,
-             field_selector: Optional[str] = None) -> List[Obj]:
+             field_selector: Optional[str] = None, copy: bool = True) -> List[Obj]:
+        # every REST response is a fresh decode: ``copy`` only matters for the in-memory server
         doc = self._req("GET", self._path(kind, "", namespace or ""),
                         query={"labelSelector": label_selector or "", "fieldSelector": field_selector or ""})
         return [self._with_kind(o, kind) for o in doc.get("items", [])]

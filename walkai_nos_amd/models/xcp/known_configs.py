@@ -15,7 +15,7 @@ import copy
 import re
 import threading
 from dataclasses import dataclass, field
-from typing import Dict, Iterable, List, Mapping, Optional
+from typing import Dict, Iterable, List, Mapping, Optional, Tuple
 
 import yaml
 
@@ -106,18 +106,23 @@ def validate_specs(specs: Mapping[str, GpuModelSpec]) -> None:
             raise ValueError(f"model {name!r}: memoryGB/computeUnits/xcds must be > 0")
 
 
+_geo_cache: Dict[Tuple[str, Optional[str]], Optional[List[Tuple[Tuple[str, int], ...]]]] = {}
+
+
 def set_known_geometries(specs: Mapping[str, GpuModelSpec]) -> None:
     """Validate then atomically replace the global table (reference ``SetKnownGeometries``)."""
     validate_specs(specs)
     global _known
     with _lock:
         _known = {normalize_model(k): copy.deepcopy(v) for k, v in specs.items()}
+        _geo_cache.clear()
 
 
 def reset_known_geometries() -> None:
     global _known
     with _lock:
         _known = copy.deepcopy(_DEFAULT_SPECS)
+        _geo_cache.clear()
 
 
 def get_known_geometries() -> Dict[str, GpuModelSpec]:
@@ -132,11 +137,15 @@ def get_model_spec(model: str) -> Optional[GpuModelSpec]:
 
 
 def get_allowed_geometries(model: str, nps: Optional[str] = None) -> Optional[List[Geometry]]:
+    """Allowed geometries of ``model`` under memory mode ``nps`` (fresh dicts; the filtered table
+    is memoised per (model, nps) — every planner pass builds a model per GPU from it)."""
     with _lock:
-        s = _known.get(normalize_model(model))
-        if s is None:
-            return None
-        return s.geometries_for_nps(nps)
+        key = (model, nps)
+        if key not in _geo_cache:
+            s = _known.get(normalize_model(model))
+            _geo_cache[key] = None if s is None else [tuple(g.items()) for g in s.geometries_for_nps(nps)]
+        hit = _geo_cache[key]
+        return None if hit is None else [dict(g) for g in hit]
 
 
 def load_known_geometries(data: str) -> Dict[str, GpuModelSpec]:

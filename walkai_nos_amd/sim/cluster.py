@@ -150,7 +150,8 @@ class SimScheduler:
         self.bound = 0
 
     def reconcile(self, req: Request) -> Result:
-        pods = [p for p in self.api.list("Pod", field_selector="status.phase=Pending") if not podutil.is_scheduled(p)
+        pods = [p for p in self.api.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if not podutil.is_scheduled(p)
                 and p["spec"].get("schedulerName", "default-scheduler") == "default-scheduler"]
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
         for p in pods:
@@ -293,10 +294,12 @@ class SimCluster:
 
     # -- metrics ------------------------------------------------------------------------
     def running_pods(self) -> List[Dict[str, Any]]:
-        return [p for p in self.api.list("Pod", field_selector="status.phase=Running") if ko.namespace(p) != DP_NAMESPACE]
+        return [p for p in self.api.list("Pod", field_selector="status.phase=Running", copy=False)
+                if ko.namespace(p) != DP_NAMESPACE]
 
     def pending_pods(self) -> List[Dict[str, Any]]:
-        return [p for p in self.api.list("Pod", field_selector="status.phase=Pending") if ko.namespace(p) != DP_NAMESPACE]
+        return [p for p in self.api.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if ko.namespace(p) != DP_NAMESPACE]
 
     def gpu_allocated_fraction(self) -> Dict[Tuple[str, int], float]:
         out: Dict[Tuple[str, int], float] = {}
