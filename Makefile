@@ -21,6 +21,7 @@ test-gpu: native   ## GPU test suite (MI355X)
 lint:
 	$(PYTHON) -m ruff check walkai_nos_amd tests || true
 	$(PYTHON) -m compileall -q walkai_nos_amd tests
+	$(PYTHON) hack/check_headers.py
 
 bench: native      ## flagship benchmark, 1 GPU
 	$(PYTHON) bench.py

@@ -1,3 +1,5 @@
+"""pytest configuration: the ``gpu`` marker (tests that need an MI355X; the CPU suite runs
+``-m "not gpu"``) and the repository root on ``sys.path``."""
 import os
 import sys
 

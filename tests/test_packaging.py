@@ -139,3 +139,11 @@ def test_demo_overlays_request_valid_resources(overlay, resource):
     assert resource in k["patches"][0]["patch"]
     assert (resource == constant.RESOURCE_AMD_GPU or constant.RESOURCE_XCP_REGEX.match(resource)
             or constant.RESOURCE_SLICE_REGEX.match(resource))
+
+
+def test_every_source_file_has_a_header():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "hack", "check_headers.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
