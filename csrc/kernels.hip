@@ -1,7 +1,10 @@
 // nos workload kernels for gfx950 (MI355X): the hot ops of the fp32 YOLOS-small fractional-GPU
-// workload. Plain GEMMs stay on hipBLASLt; everything else that touches the activations is here.
+// workload (the GEMMs are in gemm.hip / gemm_x3.hip).
 //
-//  * attn_fwd_f32: flash attention over a packed [B, T, 3*H*64] fp32 QKV tensor on the exact-fp32
+//  * attn_fwd_x3p (production): fp32-accurate flash attention on the bf16 matrix cores over the
+//    exact three-bf16-plane ("x3") form of Q/K/V, software-pipelined — see "fp32 as three bf16
+//    planes" below; attn_fwd_x3 is its block-at-a-time A/B reference;
+//  * attn_fwd_f32 / attn_fwd_sk / attn_fwd_sk_lds (the f32-MFMA path, set_fp32_matmul("f32")): flash attention over a packed [B, T, 3*H*64] fp32 QKV tensor on the exact-fp32
 //    matrix cores (v_mfma_f32_32x32x2_f32, 64 FLOP/clk/SIMD). One wave owns 32 queries of one head.
 //    It computes S^T = K Q^T so that every lane owns ONE query column: the softmax row reductions
 //    are 16 in-register ops plus a single cross-half exchange (lane l <-> l^32), no LDS. The
@@ -13,7 +16,7 @@
 //    persistent grid sized to the slice's resident-wave capacity splits the (query tile x key
 //    block) work evenly, so a 32-CU CPX slice and the whole 256-CU GPU are both tail-free.
 //  * layernorm_f32: one wave per row, values kept in registers (two-pass mean/variance), wave64
-//    shuffles.
+//    shuffles; writes fp32 or the x3 planes the next GEMM consumes.
 //  * bias_gelu_f32: in-place exact (erf) GELU(y + b) epilogue, dwordx4 vectorised.
 #include <hip/hip_runtime.h>
 

@@ -1,4 +1,6 @@
-"""fp32 GEMM with fused epilogues on the hand-written MFMA kernel (``csrc/gemm.hip``).
+"""fp32 GEMMs with fused epilogues on hand-written MFMA kernels: the x3 GEMM (``csrc/gemm_x3.hip``,
+:func:`gemm_x3`, the default model path — fp32-accurate on the bf16 matrix cores) and the
+f32-input-MFMA GEMM (``csrc/gemm.hip``, :func:`gemm`).
 
 ``gemm(x, w, bias=None, gelu=False, residual=None)`` computes ``x @ w^T (+ bias) (GELU) (+ residual)``
 in one kernel. The tile shape (64x64, 128x64, 64x128 or 128x128; stage depth 32 or 64) is chosen per

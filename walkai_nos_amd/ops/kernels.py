@@ -5,17 +5,18 @@ On a GPU tensor the HIP path is mandatory unless the caller explicitly selects t
 backend (used only as the measured baseline in the benchmark's A/B mode): a missing
 ``libnos_kernels.so`` raises instead of silently falling back.
 
-Kernels (``csrc/kernels.hip``):
+Kernels (``csrc/kernels.hip``, ``csrc/gemm_x3.hip``, ``csrc/gemm.hip``):
 
-* ``layernorm``        — one wave per row, fp32, vectorised float4 loads, two-pass mean/var in
-  registers (rows of 384 floats = 6 floats per lane);
-* ``linear`` / ``linear_gelu`` / ``linear_residual`` — fp32 MFMA GEMM (``csrc/gemm.hip``) with bias,
-  exact-erf GELU or the residual add fused into the store; tile shape autotuned per (shape, slice)
-  against hipBLASLt, which stays the choice where it is faster (``ops/gemm.py``);
-* ``attention_qkv``    — flash attention over the packed ``[B, T, 3*D]`` QKV tensor on
-  ``v_mfma_f32_32x32x2_f32`` (exact fp32 MFMA), online softmax, stream-K decomposition over
-  (32-query tile x 32-key block) units with a persistent grid sized to the slice's CUs; writes
-  ``[B, T, D]`` directly so no transpose pass is needed.
+* fp32 matmuls run in the **x3** form by default (``set_fp32_matmul``): every fp32 operand as three
+  exact bf16 planes, six bf16 MFMAs per block, fp32-accurate; producers emit planes directly
+  (``layernorm_x3``, ``linear_x3(..., out_x3=True)``, ``attention_qkv_x3``);
+* ``layernorm`` / ``layernorm_x3`` — one wave per row, two-pass mean/var in registers;
+* ``linear_x3`` — x3 GEMM with bias / exact GELU / residual(s) fused into the store, tile and
+  pipeline (register-staged, LDS-DMA ring, persistent) autotuned per (shape, slice);
+* ``linear`` / ``linear_gelu`` / ``linear_residual`` — the f32-input-MFMA GEMM (``f32`` mode), tuned
+  against hipBLASLt;
+* ``attention_qkv_x3`` / ``attention_qkv`` — stream-K flash attention over the packed QKV tensor
+  (software-pipelined x3 kernel, or the f32-MFMA kernel), persistent grid sized to the slice.
 """
 from __future__ import annotations
 
