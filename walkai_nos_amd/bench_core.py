@@ -199,7 +199,9 @@ class NodeBench:
         self.pods_samples: List[int] = []
         self.pending_samples: List[int] = []
         self.slots: Dict[Tuple[str, int], Slot] = {}
-        self._inflight: List[Any] = []
+        self._inflight: List[Any] = []   # completion events of the last enqueued epoch
+        # host-side time split of the timed steps: control plane / waiting for the GPU / enqueue
+        self.host_s = {"control": 0.0, "wait": 0.0, "enqueue": 0.0}
         self.gpu = gpu_data_plane
         if self.gpu:
             import torch
@@ -226,6 +228,11 @@ class NodeBench:
 
     # -- one epoch ------------------------------------------------------------------------
     def control_step(self) -> None:
+        t0 = time.perf_counter()
+        self._control_step()
+        self.host_s["control"] += time.perf_counter() - t0
+
+    def _control_step(self) -> None:
         c = self.cluster
         for name in list(self.churn.live):
             self.churn.live[name] -= 1
@@ -262,11 +269,14 @@ class NodeBench:
         """Enqueue this epoch's inferences. The previous epoch's GPU work must be complete first
         (the control plane of this epoch ran on the CPU meanwhile): at most one epoch is in
         flight, so the slots running concurrently always belong to one partition layout and a GPU
-        never executes the backlog of an old mode alongside its new one."""
+        never executes the backlog of an old mode alongside its new one. (Queueing the next epoch
+        behind GPU-side stream waits instead measured 15% slower: 243 vs 284 inf/s.)"""
+        t0 = time.perf_counter()
         if self.gpu:
             for ev in self._inflight:
                 ev.synchronize()
             self._inflight = []
+        t1 = time.perf_counter()
         n = 0
         for prof, part, work in self.my_pods():
             if self.gpu:
@@ -275,6 +285,8 @@ class NodeBench:
                 self._inflight.append(slot.mark())
             n += work
         self.inferences += n
+        self.host_s["wait"] += t1 - t0
+        self.host_s["enqueue"] += time.perf_counter() - t1
         return n
 
     def step(self) -> int:
@@ -321,6 +333,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     if distributed:
         dist.barrier()
     nb.inferences = 0
+    nb.host_s = {k: 0.0 for k in nb.host_s}
     nb.util_samples.clear()
     nb.pods_samples.clear()
     nb.pending_samples.clear()
@@ -368,6 +381,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "pods_per_gpu": round(pods / cfg.gpus, 2),
         "pending_pods_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
         "achieved_tflops": round(value * flops / 1e12, 2),
+        "host_ms_per_step": {k: round(1000.0 * v / cfg.steps, 2) for k, v in nb.host_s.items()},
         "baseline_ref": BASELINE_LABEL,
         "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
