@@ -42,6 +42,24 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// ---- x3 helpers (fp32 as three exact bf16 terms; see "fp32 as three bf16 planes" below) ----
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <typename F, typename H>
+__device__ __forceinline__ void split3(const F& x, H& a, H& b, H& c) {
+  a = __builtin_convertvector(x, H);  // v_cvt_pk_bf16_f32: round to nearest even
+  const F r = x - __builtin_convertvector(a, F);
+  b = __builtin_convertvector(r, H);
+  c = __builtin_convertvector(r - __builtin_convertvector(b, F), H);
+}
+
 // store v as three exact bf16 terms at y[i], y[plane + i], y[2*plane + i] (x3 format, see below)
 __device__ __forceinline__ void store_x3(__bf16* __restrict__ y, size_t plane, size_t i, float v) {
   const __bf16 h0 = (__bf16)v;
@@ -53,45 +71,59 @@ __device__ __forceinline__ void store_x3(__bf16* __restrict__ y, size_t plane, s
 }
 
 // ------------------------------------------------------------------------------------------
-// LayerNorm (output fp32 y, or x3 planes yp with plane stride rows*D when yp != nullptr)
+// LayerNorm (output fp32 y, or x3 planes yp with plane stride rows*D when yp != nullptr). Lane l
+// owns the column pairs (2l + 128i, 2l + 128i + 1): 8-B loads, and packed 4-B bf16-pair stores per
+// plane on the x3 path.
 template <int NPL>
 __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, float* __restrict__ y,
                                                      __bf16* __restrict__ yp, int rows, float eps) {
-  constexpr int D = NPL * 64;
+  static_assert(NPL % 2 == 0, "hidden size must be a multiple of 128");
+  constexpr int D = NPL * 64, NP = NPL / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + wave;
   if (row >= rows) return;
-  const float* xr = x + size_t(row) * D;
-  float v[NPL];
+  const float2* xr = reinterpret_cast<const float2*>(x + size_t(row) * D);
+  float2 v[NP];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
+  for (int i = 0; i < NP; ++i) {
     v[i] = xr[i * 64 + lane];
-    s += v[i];
+    s += v[i].x + v[i].y;
   }
   const float mean = wave_sum(s) * (1.0f / D);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    v[i] -= mean;
-    q += v[i] * v[i];
+  for (int i = 0; i < NP; ++i) {
+    v[i].x -= mean;
+    v[i].y -= mean;
+    q += v[i].x * v[i].x + v[i].y * v[i].y;
   }
   const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  const float2* w2 = reinterpret_cast<const float2*>(w);
+  const float2* b2 = reinterpret_cast<const float2*>(b);
   if (yp) {
-    const size_t plane = size_t(rows) * D;
+    const size_t plane2 = size_t(rows) * D / 2;  // plane stride in bf16 pairs
+    uint32_t* dst = reinterpret_cast<uint32_t*>(yp) + size_t(row) * (D / 2);
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) {
-      const int c = i * 64 + lane;
-      store_x3(yp, plane, size_t(row) * D + c, v[i] * rstd * w[c] + b[c]);
+    for (int i = 0; i < NP; ++i) {
+      const int c2 = i * 64 + lane;
+      const float2 ww = w2[c2], bb = b2[c2];
+      const f32x2 val = {v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y};
+      bf16x2 h0, h1, h2;
+      split3(val, h0, h1, h2);
+      dst[c2] = __builtin_bit_cast(uint32_t, h0);
+      dst[plane2 + c2] = __builtin_bit_cast(uint32_t, h1);
+      dst[2 * plane2 + c2] = __builtin_bit_cast(uint32_t, h2);
     }
     return;
   }
-  float* yr = y + size_t(row) * D;
+  float2* yr = reinterpret_cast<float2*>(y + size_t(row) * D);
 #pragma unroll
-  for (int i = 0; i < NPL; ++i) {
-    const int c = i * 64 + lane;
-    yr[c] = v[i] * rstd * w[c] + b[c];
+  for (int i = 0; i < NP; ++i) {
+    const int c2 = i * 64 + lane;
+    const float2 ww = w2[c2], bb = b2[c2];
+    yr[c2] = make_float2(v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y);
   }
 }
 
@@ -604,20 +636,6 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
 // fp32 rounding level. Six bf16 MFMAs (32x32x16, 32 cycles each) replace eight f32 MFMAs
 // (32x32x2, 64 cycles each) per 32x32x16 block: 2.67x fewer matrix-pipe cycles at fp32 accuracy.
 // The small products are accumulated first so the running sum absorbs them at fp32 rounding.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-template <typename F, typename H>
-__device__ __forceinline__ void split3(const F& x, H& a, H& b, H& c) {
-  a = __builtin_convertvector(x, H);  // v_cvt_pk_bf16_f32: round to nearest even
-  const F r = x - __builtin_convertvector(a, F);
-  b = __builtin_convertvector(r, H);
-  c = __builtin_convertvector(r - __builtin_convertvector(b, F), H);
-}
 
 // Exact three-term split of acc[e0 .. e0+7] by truncation: x0 = the high 16 bits of x (its f32
 // value is x & 0xffff0000, so no conversion back is needed), x1 = the high half of x - x0, x2 =

@@ -14,6 +14,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -52,10 +53,13 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--out", default="gpurun_out/kbench.json")
-    ap.add_argument("--only", choices=("all", "attn", "gemm", "model"), default="all")
+    ap.add_argument("--only", choices=("all", "attn", "gemm", "model", "modes"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
+    ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
     a = ap.parse_args()
     torch.manual_seed(0)
+    if a.only == "modes":
+        return modes_bench(a)
     qkv = torch.randn(1, T, 3 * D, device="cuda")
     out = torch.empty(1, T, D, device="cuda")
     x = torch.randn(T, D, device="cuda")
@@ -84,6 +88,7 @@ def main() -> int:
             if a.only in ("all", "model"):
                 model_bench(r, s, max(3, a.iters // 4))
             r["layernorm_us"] = round(timeit(lambda: K.layernorm(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
+            r["layernorm_x3_us"] = round(timeit(lambda: K.layernorm_x3(x, w_o[0], w_o[1], 1e-12), s, a.iters), 1)
             for kname in list(r):
                 if isinstance(r[kname], float):
                     r[kname] = round(r[kname], 2)
@@ -121,6 +126,47 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
     for kname in [k_ for k_ in list(r) if k_.startswith("attn_") and k_.endswith("_us")
                   and not k_.startswith("split3")]:
         r[kname.replace("_us", "_tflops")] = round(attn_flops / r[kname] / 1e6, 2)
+
+
+def modes_bench(a) -> int:
+    """Whole-GPU throughput of each partition mode as the flagship bench runs it: every partition
+    of the mode busy at once (its own CU-masked stream and graph-captured model replica), each
+    running 8 x fraction inferences per round; inferences/s per GPU."""
+    from walkai_nos_amd.bench_core import BenchConfig, Slot
+    from walkai_nos_amd.models.workload.yolos import YolosSmall
+    cfg = BenchConfig()
+    template = YolosSmall()
+    results = []
+    for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
+        if prof.split("_")[0] not in a.slices.split(","):
+            continue
+        n = min(n, a.partitions) if a.partitions else n
+        slots = [Slot(prof, k, 0, cfg, template) for k in range(n)]
+        for sl in slots:
+            sl.warm()
+        torch.cuda.synchronize()
+        work = 8 // n
+        rounds = 3
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            evs = []
+            for sl in slots:
+                sl.run(work)
+                evs.append(sl.mark())
+            for ev in evs:
+                ev.synchronize()
+        dt = time.perf_counter() - t0
+        r = {"mode": prof, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
+             "ms_per_round": round(1000 * dt / rounds, 2)}
+        print(json.dumps(r), flush=True)
+        results.append(r)
+        for sl in slots:
+            sl.close()
+        torch.cuda.synchronize()
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(results, f, indent=1)
+    return 0
 
 
 def model_bench(r, s, iters):
