@@ -118,3 +118,43 @@ def test_probe_on_commit_with_real_kernels(gpu):
     assert whole["n_cus"] >= 256 and cpx["n_cus"] == 32
     assert 300 < whole["bf16_tflops"] < 2600 and whole["hbm_gbps"] > 1000
     assert 3 < whole["bf16_tflops"] / cpx["bf16_tflops"] < 12
+
+
+def test_torch_barrier_vote_does_not_wait_for_cu_masked_work(gpu):
+    # the bench's multi-GPU commit vote (RCCL all-reduce, here a 1-rank communicator) must not queue
+    # behind inference work on the partitions' CU-masked streams (which are blocking streams: an op
+    # on the legacy default stream would wait for all of them)
+    import socket
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from walkai_nos_amd.ops.probe import Stream
+    from walkai_nos_amd.parallel.barrier import TorchBarrier
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        b = TorchBarrier()
+        assert b.vote(True) and not b.vote(False)
+        a = torch.randn(4096, 4096, device="cuda")
+        with Stream(0, list(range(32))) as hs:
+            st = hs.torch_stream()
+            with torch.cuda.stream(st):
+                t_k = time.perf_counter()
+                for _ in range(40):
+                    a = a @ a * 1e-4
+                ev = torch.cuda.Event()
+                ev.record(st)
+            t0 = time.perf_counter()
+            assert b.vote(True)
+            t_vote = time.perf_counter() - t0
+            ev.synchronize()
+            t_work = time.perf_counter() - t_k
+        assert t_work > 0.05, t_work          # the masked work really was long
+        assert t_vote < 0.25 * t_work, (t_vote, t_work)
+    finally:
+        dist.destroy_process_group()

@@ -21,7 +21,7 @@ from __future__ import annotations
 import ctypes
 import threading
 import time
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from ..utils.metrics import REGISTRY
 
@@ -69,7 +69,16 @@ class LocalBarrier(CommitBarrier):
         return all(votes) and len(votes) == self.n
 
 
+# per (group, device): the side stream and vote buffer of the RCCL barrier, created once
+_TORCH_BARRIER_STATE: Dict[Tuple[int, str], Tuple[Any, Any]] = {}
+
+
 class TorchBarrier(CommitBarrier):
+    """One int32 all-reduce per commit. With RCCL the vote runs on its own non-blocking HIP stream:
+    on the legacy default stream it would wait for every blocking stream of the process — e.g. the
+    CU-masked streams of the partitions' inference work — and serialise each commit behind the
+    GPU's queued work."""
+
     def __init__(self, group: Any = None, device: Optional[Any] = None):
         import torch
         import torch.distributed as dist
@@ -79,13 +88,29 @@ class TorchBarrier(CommitBarrier):
         backend = dist.get_backend(group)
         self.device = device if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu"))
-        self._buf = torch.zeros(1, dtype=torch.int32, device=self.device)
+        key = (id(group), str(self.device))
+        st = _TORCH_BARRIER_STATE.get(key)
+        if st is None:
+            if self.device.type == "cuda":
+                stream = torch.cuda.Stream(device=self.device)
+                with torch.cuda.stream(stream):
+                    buf = torch.zeros(1, dtype=torch.int32, device=self.device)
+                stream.synchronize()
+            else:
+                stream, buf = None, torch.zeros(1, dtype=torch.int32)
+            st = _TORCH_BARRIER_STATE[key] = (stream, buf)
+        self._stream, self._buf = st
 
     def vote(self, ok: bool) -> bool:
+        import contextlib
+
+        import torch
         t0 = time.perf_counter()
-        self._buf.fill_(1 if ok else 0)
-        self.dist.all_reduce(self._buf, group=self.group)
-        res = int(self._buf.item()) == self.world
+        ctx = torch.cuda.stream(self._stream) if self._stream is not None else contextlib.nullcontext()
+        with ctx:
+            self._buf.fill_(1 if ok else 0)
+            self.dist.all_reduce(self._buf, group=self.group)
+            res = int(self._buf.item()) == self.world
         REGISTRY.phase_seconds.labels(phase="commit_barrier").observe(time.perf_counter() - t0)
         return res
 
