@@ -36,8 +36,11 @@ def main() -> int:
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=300))
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        # RCCL between the GPU ranks; NOS_BENCH_DIST_BACKEND=gloo rehearses the multi-rank path with
+        # several ranks sharing fewer GPUs (RCCL refuses two ranks on one device)
+        dist.init_process_group(os.environ.get("NOS_BENCH_DIST_BACKEND", "nccl"),
+                                timeout=datetime.timedelta(seconds=300))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} != WORLD_SIZE {world}; using {world}", file=sys.stderr)
     gpus = world if world > 1 else args.gpus

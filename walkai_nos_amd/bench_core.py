@@ -209,7 +209,7 @@ class NodeBench:
             from .models.workload.yolos import YolosSmall
             from .ops import kernels as K
             K.set_backend(cfg.backend)
-            self.device = int(os.environ.get("LOCAL_RANK", "0"))
+            self.device = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
             torch.cuda.set_device(self.device)
             template = YolosSmall()
             for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
@@ -344,7 +344,9 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stats = torch.tensor([elapsed, float(nb.inferences)], dtype=torch.float64, device=f"cuda:{nb.device}")
+    on_gpu = dist.get_backend() == "nccl" if distributed else True
+    stats = torch.tensor([elapsed, float(nb.inferences)], dtype=torch.float64,
+                         device=f"cuda:{nb.device}" if on_gpu else "cpu")
     if distributed:
         t = stats[:1].clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
