@@ -553,12 +553,13 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // 2 = 64x128, 3 = 128x128 (double-buffered LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered:
 // half the LDS, more resident tiles); 7-12 = LDS-DMA pipeline with nbuf = S stages (S-1 in
 // flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2.
-static const int kCfgX3[15][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+static const int kCfgX3[18][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
-                                  {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2}};
+                                  {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
+                                  {32, 64, 3}, {32, 64, 2}, {64, 32, 2}};
 
-int nos_gemm_x3_num_configs() { return 15; }
+int nos_gemm_x3_num_configs() { return 18; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
@@ -591,7 +592,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 14) return -1;
+  if (cfg < 0 || cfg > 17) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -637,6 +638,9 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 12: return launch_d<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 13: return launch_d<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 14: return launch_d<128, 128, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 15: return launch_d<32, 64, 1, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 16: return launch_d<32, 64, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 17: return launch_d<64, 32, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

@@ -200,18 +200,20 @@ def tuning_table() -> Dict[str, str]:
 
 # ---- x3: fp32-accurate GEMM on the bf16 matrix cores (csrc/gemm_x3.hip) -------------------------
 #: config -> (BM, BN, LDS buffers, pipeline): "r" = register-staged loads one stage ahead,
-#: "d" = LDS-DMA (global_load_lds) with nbuf-1 stages in flight, "d8" = the same with 8 waves
+#: "d" = LDS-DMA (global_load_lds) with nbuf-1 stages in flight, "d8" / "d2" = the same with 8 / 2
+#: waves per workgroup
 X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: (128, 128, 2, "r"),
             4: (64, 64, 1, "r"), 5: (128, 64, 1, "r"), 6: (64, 128, 1, "r"),
             7: (64, 64, 3, "d"), 8: (64, 64, 4, "d"), 9: (128, 64, 3, "d"), 10: (64, 128, 3, "d"),
             11: (128, 128, 3, "d"), 12: (64, 64, 2, "d"),
             13: (128, 128, 3, "d8"), 14: (128, 128, 2, "d8"),
+            15: (32, 64, 3, "d2"), 16: (32, 64, 2, "d2"), 17: (64, 32, 2, "d2"),
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
             104: (128, 64, 3, "p")}
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
-                   13: 1, 14: 1, 100: 2, 101: 3, 102: 1, 103: 1, 104: 1}
+                   13: 1, 14: 1, 15: 2, 16: 4, 17: 4, 100: 2, 101: 3, 102: 1, 103: 1, 104: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
