@@ -560,7 +560,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
                                                          int B, int T, int H, int P, __bf16* __restrict__ outp) {
-  __shared__ float s_mmax[32], s_inv[32];
   __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
   const long long U = (long long)B * H * QG * NK;
@@ -582,35 +581,43 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
     if (s == (w + 1) * U / P) return -1;  // empty range
     return (w * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
   };
-  if (tid < 32) {
-    float mmax = -INFINITY;
-    for (long long w = w_lo; w <= w_hi; ++w) {
-      const long long sl = slot_of(w);
-      if (sl >= 0) mmax = fmaxf(mmax, part_ml[sl * 64 + tid]);
-    }
-    float den = 0.f;
-    for (long long w = w_lo; w <= w_hi; ++w) {
-      const long long sl = slot_of(w);
-      if (sl >= 0) den += part_ml[sl * 64 + 32 + tid] * __builtin_amdgcn_exp2f(part_ml[sl * 64 + tid] - mmax);
-    }
-    s_mmax[tid] = mmax;
-    s_inv[tid] = 1.f / den;
-  }
-  __syncthreads();
+  // one online-softmax merge pass over the contributors, their loads issued up to four at a time
+  // (every thread merges its own query's m/l redundantly: no serial phase, no extra barrier)
   const int q = tid & 31;
-  const float mq = s_mmax[q];
+  float M = -INFINITY, L = 0.f;
   float acc[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-  for (long long w = w_lo; w <= w_hi; ++w) {
-    const long long sl = slot_of(w);
-    if (sl < 0) continue;
-    const float sc = __builtin_amdgcn_exp2f(part_ml[sl * 64 + q] - mq);
-    const float* po = part_o + sl * (HD * 32);
+  for (long long w0 = w_lo; w0 <= w_hi; w0 += 4) {
+    float mw[4], lw[4], ow[4][8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] += po[tid + 256 * i] * sc;
+    for (int c = 0; c < 4; ++c) {
+      const long long w = w0 + c;
+      const long long sl = w <= w_hi ? slot_of(w) : -1;
+      mw[c] = -INFINITY;
+      lw[c] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ow[c][i] = 0.f;
+      if (sl >= 0) {
+        mw[c] = part_ml[sl * 64 + q];
+        lw[c] = part_ml[sl * 64 + 32 + q];
+        const float* po = part_o + sl * (HD * 32);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ow[c][i] = po[tid + 256 * i];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (mw[c] == -INFINITY) continue;
+      const float Mn = fmaxf(M, mw[c]);
+      const float so = __builtin_amdgcn_exp2f(M - Mn), sn = __builtin_amdgcn_exp2f(mw[c] - Mn);
+      L = L * so + lw[c] * sn;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = acc[i] * so + ow[c][i] * sn;
+      M = Mn;
+    }
   }
-  const float inv = s_inv[q];
+  const float inv = 1.f / L;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s_tile[(tid + 256 * i) >> 5][q] = acc[i] * inv;
   __syncthreads();
