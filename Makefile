@@ -4,7 +4,7 @@ IMG ?= ghcr.io/walkai/nos-mi355x:0.1.0
 CLIENT_IMG ?= ghcr.io/walkai/nos-mi355x-client:0.1.0
 NAMESPACE ?= nos-system
 
-.PHONY: all native test test-gpu lint bench bench-8 smoke simulate kbench docker-build docker-push \
+.PHONY: all native test test-gpu lint sanitize bench bench-8 smoke simulate kbench docker-build docker-push \
         deploy undeploy install-crds helm-install helm-uninstall kind-up clean
 
 all: native test
@@ -22,6 +22,9 @@ lint:
 	$(PYTHON) -m ruff check walkai_nos_amd tests || true
 	$(PYTHON) -m compileall -q walkai_nos_amd tests
 	$(PYTHON) hack/check_headers.py
+
+sanitize:          ## host-code sanitizers (ASan+UBSan, TSan) over the HBM-limit shim's self-test
+	$(PYTHON) -m pytest tests/test_native_sanitizers.py -q
 
 bench: native      ## flagship benchmark, 1 GPU
 	$(PYTHON) bench.py
