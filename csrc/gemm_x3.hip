@@ -34,8 +34,25 @@ constexpr int BK = 32, LSTR = 40;
 
 __device__ __forceinline__ int acc_row(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
+// Logical tile of physical workgroup `phys` in a grid of n: workgroups are dealt round-robin over the
+// 8 XCDs (phys % 8 = XCD, observed placement — speed only, never correctness), so XCD x gets the
+// contiguous logical range starting at x*(n/8) + min(x, n%8): a band of whole tile rows whose A
+// rows stay in that XCD's L2 while it sweeps the weight columns. A bijection for every n.
 __device__ __forceinline__ int xcd_major(int phys, int n) {
-  return (n % 8 == 0) ? (phys % 8) * (n / 8) + phys / 8 : phys;
+  const int x = phys % 8, q = n / 8, r = n % 8;
+  return x * q + min(x, r) + phys / 8;
+}
+
+// Persistent grids: workgroup w's tiles are base + i*stride, i < count — the XCD's band again, dealt
+// over the XCD's P/8 workgroups (P % 8 == 0; otherwise a plain w + i*P sweep).
+__device__ __forceinline__ void xcd_band(int w, int P, int tiles, int& base, int& stride, int& count) {
+  if (P % 8) {
+    base = w, stride = P, count = w < tiles ? (tiles - w + P - 1) / P : 0;
+    return;
+  }
+  const int x = w % 8, li = w / 8, px = P / 8, q = tiles / 8, r = tiles % 8;
+  const int n = q + (x < r ? 1 : 0);
+  base = x * q + min(x, r) + li, stride = px, count = li < n ? (n - li + px - 1) / px : 0;
 }
 
 __device__ __forceinline__ f32x16 mfma_x3(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
@@ -277,55 +294,71 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Stage depth BKS (32 or 64 bf16 per plane) sets the LDS row: CPR = BKS/8 16-byte chunks, so one
+// wave DMA instruction (64 lanes x 16 B) covers RPI = 64/CPR rows. BKS = 64 reads whole 128-byte
+// row segments: half the cache lines per byte moved of BKS = 32 (the texture-address path, not
+// HBM, bounds these short-K GEMMs even when every line hits L2). Chunk c of local row r sits at
+// slot c ^ swz(r), swz(r) = (r / (16/CPR)) % CPR, which makes the fragment reads (lanes j, j+32
+// on rows j of a 32-row block) conflict-free for both depths.
+template <int BKS>
+__device__ __forceinline__ int dma_swz(int r) {
+  constexpr int CPR = BKS / 8;
+  return (r / (16 / CPR)) % CPR;
+}
+
 // Per-lane byte offsets of this wave's DMA rows inside one plane (fixed for the whole K loop):
-// row groups g = wave + 4i of 16 rows; lane -> row 16g + lane/4, k-chunk (lane%4) ^ ((lane/16)%4).
-template <int ROWS, int NW>
-__device__ __forceinline__ void dma_offsets(uint32_t (&voff)[ROWS / 16 / NW], int r0, int rmax, int K, int wave,
-                                            int lane) {
-  const int rl = lane >> 2, c = (lane & 3) ^ ((lane >> 4) & 3);
+// row groups g = wave + NW*i of RPI rows; lane -> row RPI*g + lane/CPR, chunk (lane%CPR) ^ swz(row).
+template <int ROWS, int NW, int BKS = 32>
+__device__ __forceinline__ void dma_offsets(uint32_t (&voff)[ROWS * BKS / 512 / NW], int r0, int rmax, int K,
+                                            int wave, int lane) {
+  constexpr int CPR = BKS / 8, RPI = 64 / CPR;
 #pragma unroll
-  for (int i = 0; i < ROWS / 16 / NW; ++i) {
-    const int row = min(r0 + 16 * (wave + NW * i) + rl, rmax);
+  for (int i = 0; i < ROWS / RPI / NW; ++i) {
+    const int rl = RPI * (wave + NW * i) + lane / CPR;
+    const int c = (lane % CPR) ^ dma_swz<BKS>(rl);
+    const int row = min(r0 + rl, rmax);
     voff[i] = uint32_t(row) * uint32_t(K) * 2u + 16u * uint32_t(c);
   }
 }
 
-// one stage of ROWS x 32 bf16 per plane for this wave (NW waves share the row groups): a wave-uniform base (plane, k0) plus the
+// one stage of ROWS x BKS bf16 per plane for this wave (NW waves share the row groups): a wave-uniform base (plane, k0) plus the
 // lane's fixed 32-bit offset, so the loads take the SGPR-base + VGPR-offset form and a stage costs
 // no per-lane address arithmetic
-template <int ROWS, int NW>
+template <int ROWS, int NW, int BKS = 32>
 __device__ __forceinline__ void dma_stage(const __bf16* __restrict__ X, size_t plane,
-                                          const uint32_t (&voff)[ROWS / 16 / NW], int k0, __bf16* lds, int wave) {
+                                          const uint32_t (&voff)[ROWS * BKS / 512 / NW], int k0, __bf16* lds,
+                                          int wave) {
+  constexpr int RPI = 512 / BKS;
 #pragma unroll
-  for (int i = 0; i < ROWS / 16 / NW; ++i) {
+  for (int i = 0; i < ROWS / RPI / NW; ++i) {
     const int g = wave + NW * i;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const char* src = reinterpret_cast<const char*>(X + q * plane + k0) + voff[i];
-      __builtin_amdgcn_global_load_lds(src, (lds_void*)(lds + q * ROWS * 32 + 16 * g * 32), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_void*)(lds + q * ROWS * BKS + RPI * g * BKS), 16, 0, 0);
     }
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BKS = 32>
 __device__ __forceinline__ void compute_stage_sw(f32x16 (&acc)[WM / 32][WN / 32], const __bf16* __restrict__ as,
                                                  const __bf16* __restrict__ bs, int wm, int wn, int j, int hf) {
   constexpr int TM = WM / 32, TN = WN / 32;
-  const int sw = (j >> 2) & 3;  // rows j and j + 32a share (row >> 2) & 3
+  const int sw = dma_swz<BKS>(j);  // rows j and j + 32a share the swizzle
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < BKS / 16; ++s) {
     const int ch = (2 * s + hf) ^ sw;
     bf16x8 af[TM][3], bfr[TN][3];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        af[a][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * 32 + (wm * WM + 32 * a + j) * 32 + 8 * ch]);
+        af[a][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * BKS + (wm * WM + 32 * a + j) * BKS + 8 * ch]);
 #pragma unroll
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * 32 + (wn * WN + 32 * b + j) * 32 + 8 * ch]);
+        bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * BKS + (wn * WN + 32 * b + j) * BKS + 8 * ch]);
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -336,7 +369,7 @@ __device__ __forceinline__ void compute_stage_sw(f32x16 (&acc)[WM / 32][WN / 32]
 
 // BM x BN tile on a WGM x WGN grid of waves (4 or 8 waves: 8 gives each SIMD two waves of one
 // workgroup, so a 128x128 tile — half the bytes per MFMA of 64x64 — still hides its load latency)
-template <int BM, int BN, int WGM, int WGN, int S>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __restrict__ A, size_t a_plane,
                                                   const __bf16* __restrict__ W, size_t w_plane,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
@@ -347,15 +380,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  static_assert(BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "row groups must divide over the waves");
-  constexpr int NLD = 3 * (BM / 16 / NW) + 3 * (BN / 16 / NW);  // DMA instructions per wave per stage
+  constexpr int RPI = 512 / BKS;  // rows per DMA instruction
+  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "row groups must divide over the waves");
+  constexpr int NLD = 3 * (BM / RPI / NW) + 3 * (BN / RPI / NW);  // DMA instructions per wave per stage
   // one __shared__ object per stage buffer: the compiler's LDS-DMA wait tracking can then tell the
   // buffer being read from the buffers being filled (one array indexed by stage would make every
   // fragment read wait for ALL outstanding DMA, vmcnt(0), and serialise the pipeline)
-  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * 32], A1[3 * BM * 32], A2[S > 2 ? 3 * BM * 32 : 8],
-      A3[S > 3 ? 3 * BM * 32 : 8];
-  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * 32], B1[3 * BN * 32], B2[S > 2 ? 3 * BN * 32 : 8],
-      B3[S > 3 ? 3 * BN * 32 : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * BKS], A1[3 * BM * BKS], A2[S > 2 ? 3 * BM * BKS : 8],
+      A3[S > 3 ? 3 * BM * BKS : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS], B2[S > 2 ? 3 * BN * BKS : 8],
+      B3[S > 3 ? 3 * BN * BKS : 8];
 
   const int tiles_n = N / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
@@ -374,25 +408,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
 
-  const int nk = K / BK;
-  uint32_t voff_a[BM / 16 / NW], voff_b[BN / 16 / NW];
-  dma_offsets<BM, NW>(voff_a, m0, M - 1, K, wave, lane);
-  dma_offsets<BN, NW>(voff_b, n0, N - 1, K, wave, lane);
+  const int nk = K / BKS;
+  uint32_t voff_a[BM / RPI / NW], voff_b[BN / RPI / NW];
+  dma_offsets<BM, NW, BKS>(voff_a, m0, M - 1, K, wave, lane);
+  dma_offsets<BN, NW, BKS>(voff_b, n0, N - 1, K, wave, lane);
 #define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
 #define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
 // past the end a stage re-reads the last one, so every iteration issues NLD loads (static vmcnt)
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
-    const int k0_ = min((STAGE), nk - 1) * BK;                                     \
-    dma_stage<BM, NW>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave);                 \
-    dma_stage<BN, NW>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);                 \
+    const int k0_ = min((STAGE), nk - 1) * BKS;                                    \
+    dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave);            \
+    dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);                 \
   }
 #define X3D_ITER(KS, BUF)                                                          \
   {                                                                                \
     vm_wait<(S - 2) * NLD>(); /* this wave's DMA of stage KS has landed */         \
     raw_barrier();            /* everyone's has; stage KS-1's buffer is free */    \
     X3D_ISSUE((KS) + S - 1, ((BUF) + S - 1) % S)                                   \
-    compute_stage_sw<BM, BN, WM, WN>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf);  \
+    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf); \
   }
   X3D_ISSUE(0, 0)
   if constexpr (S > 2) X3D_ISSUE(1, 1)
@@ -416,7 +450,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
 int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
              const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
              hipStream_t s) {
@@ -424,8 +458,12 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
     return -1;
   }
+  if (K % BKS) {
+    g_err = "gemm_x3: K must be a multiple of the stage depth " + std::to_string(BKS);
+    return -1;
+  }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S>), dim3(tiles), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
+  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS>), dim3(tiles), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
                      cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -439,7 +477,7 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
 // w, w+P, ...; its (tile, k-stage) pairs form one continuous stage stream, so the DMA ring keeps
 // loading the next tile's first stages while the current tile's last MFMAs and its epilogue run —
 // the fill/drain every short-K (K = 384: 12 stages) tile otherwise pays once per tile.
-template <int BM, int BN, int WGM, int WGN, int S>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __restrict__ A, size_t a_plane,
                                                               const __bf16* __restrict__ W, size_t w_plane,
                                                               const float* __restrict__ bias,
@@ -451,19 +489,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  static_assert(BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "row groups must divide over the waves");
-  constexpr int NLD = 3 * (BM / 16 / NW) + 3 * (BN / 16 / NW);
-  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * 32], A1[3 * BM * 32], A2[S > 2 ? 3 * BM * 32 : 8],
-      A3[S > 3 ? 3 * BM * 32 : 8];
-  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * 32], B1[3 * BN * 32], B2[S > 2 ? 3 * BN * 32 : 8],
-      B3[S > 3 ? 3 * BN * 32 : 8];
+  constexpr int RPI = 512 / BKS;
+  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "row groups must divide over the waves");
+  constexpr int NLD = 3 * (BM / RPI / NW) + 3 * (BN / RPI / NW);
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * BKS], A1[3 * BM * BKS],
+      A2[S > 2 ? 3 * BM * BKS : 8], A3[S > 3 ? 3 * BM * BKS : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS],
+      B2[S > 2 ? 3 * BN * BKS : 8], B3[S > 3 ? 3 * BN * BKS : 8];
 
   const int tiles_n = N / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_n;
-  const int P = gridDim.x, w = blockIdx.x;
-  if (w >= tiles) return;
-  const int nk = K / BK;
-  const int total = ((tiles - w + P - 1) / P) * nk;  // this workgroup's stages
+  int tb, ts, tcount;
+  xcd_band(blockIdx.x, gridDim.x, tiles, tb, ts, tcount);
+  if (tcount <= 0) return;
+  const int nk = K / BKS;
+  const int total = tcount * nk;  // this workgroup's stages
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -482,21 +522,21 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
 #define X3S_ISSUE(H, BUF)                                                                 \
   {                                                                                       \
     const int h_ = min((H), total - 1);                                                   \
-    const int ti_ = h_ / nk, ks_ = h_ - ti_ * nk, t_ = w + ti_ * P;                       \
-    uint32_t va_[BM / 16 / NW], vb_[BN / 16 / NW];                                        \
-    dma_offsets<BM, NW>(va_, (t_ / tiles_n) * BM, M - 1, K, wave, lane);                  \
-    dma_offsets<BN, NW>(vb_, (t_ % tiles_n) * BN, N - 1, K, wave, lane);                  \
-    dma_stage<BM, NW>(A, a_plane, va_, ks_ * BK, X3S_A(BUF), wave);                       \
-    dma_stage<BN, NW>(W, w_plane, vb_, ks_ * BK, X3S_B(BUF), wave);                       \
+    const int ti_ = h_ / nk, ks_ = h_ - ti_ * nk, t_ = tb + ti_ * ts;                     \
+    uint32_t va_[BM / RPI / NW], vb_[BN / RPI / NW];                                      \
+    dma_offsets<BM, NW, BKS>(va_, (t_ / tiles_n) * BM, M - 1, K, wave, lane);             \
+    dma_offsets<BN, NW, BKS>(vb_, (t_ % tiles_n) * BN, N - 1, K, wave, lane);             \
+    dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3S_A(BUF), wave);                 \
+    dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3S_B(BUF), wave);                 \
   }
 #define X3S_ITER(G, BUF)                                                                  \
   {                                                                                       \
     vm_wait<(S - 2) * NLD>();                                                             \
     raw_barrier();                                                                        \
     X3S_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
-    compute_stage_sw<BM, BN, WM, WN>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);         \
+    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);    \
     if (((G) + 1) % nk == 0) {                                                            \
-      const int t_ = w + ((G) / nk) * P;                                                  \
+      const int t_ = tb + ((G) / nk) * ts;                                                \
       store_tile<TM, TN>(acc, (t_ / tiles_n) * BM + wm * WM, (t_ % tiles_n) * BN + wn * WN, j, hf, bias, R, R2, \
                          r2_rows, C, Cp, c_plane, M, N, epi);                             \
       _Pragma("unroll") for (int a = 0; a < TM; ++a)                                      \
@@ -524,7 +564,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
   vm_wait<0>();
 }
 
-template <int BM, int BN, int WGM, int WGN, int S>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
 int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
              const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi, int grid,
              hipStream_t s) {
@@ -532,9 +572,13 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
     return -1;
   }
+  if (K % BKS) {
+    g_err = "gemm_x3s: K must be a multiple of the stage depth " + std::to_string(BKS);
+    return -1;
+  }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const int g = std::max(1, std::min(grid, tiles));
-  hipLaunchKernelGGL((gemm_x3s<BM, BN, WGM, WGN, S>), dim3(g), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2,
+  hipLaunchKernelGGL((gemm_x3s<BM, BN, WGM, WGN, S, BKS>), dim3(g), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2,
                      r2_rows, C, Cp, cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -552,23 +596,28 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // Tile configurations (BM x BN, LDS buffers, load stages in flight): 0 = 64x64, 1 = 128x64,
 // 2 = 64x128, 3 = 128x128 (double-buffered LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered:
 // half the LDS, more resident tiles); 7-12 = LDS-DMA pipeline with nbuf = S stages (S-1 in
-// flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2.
-static const int kCfgX3[18][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2; 13/14 = 128x128 on 8 waves
+// S3/S2; 15-17 = 2-wave 32x64 S3/S2, 64x32 S2; 18-22 = 64-deep stages (128-byte row segments):
+// 64x64 S2/S3, 64x32 S2, 32x64 S2, 64x32 S3; 23/24 = 64-deep on 8 waves: 128x64 S2, 64x128 S2.
+static const int kCfgX3[25][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
-                                  {32, 64, 3}, {32, 64, 2}, {64, 32, 2}};
+                                  {32, 64, 3}, {32, 64, 2}, {64, 32, 2},
+                                  {64, 64, 2}, {64, 64, 3}, {64, 32, 2}, {32, 64, 2}, {64, 32, 3},
+                                  {128, 64, 2}, {64, 128, 2}};
 
-int nos_gemm_x3_num_configs() { return 18; }
+int nos_gemm_x3_num_configs() { return 25; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
-// cfg: 0 = 64x64 S3 (4 waves), 1 = 64x64 S2, 2 = 128x128 S3 (8 waves), 3 = 64x128 S3, 4 = 128x64 S3.
+// cfg: 0 = 64x64 S3 (4 waves), 1 = 64x64 S2, 2 = 128x128 S3 (8 waves), 3 = 64x128 S3, 4 = 128x64 S3;
+// 64-deep stages: 5 = 64x64 S2, 6 = 64x32 S2 (2 waves), 7 = 128x64 S2 (8 waves).
 int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, const float* bias, const float* R,
                            const float* R2, int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi,
                            int cfg, int grid, void* stream) {
   if (K % BK || ap % 8 || wp % 8 || cp % 8 || (!C && !Cp)) {
-    g_err = "gemm_x3s: K % 32, plane strides % 8, and an output are required";
+    g_err = "gemm_x3s: K % 32 (K % 64 for 64-deep stages), plane strides % 8, and an output are required";
     return -1;
   }
   if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R) || ((epi & EPI_RES2) && (!R2 || r2_rows <= 0))) {
@@ -585,6 +634,9 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
     case 2: return launch_s<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 3: return launch_s<64, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 4: return launch_s<128, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 5: return launch_s<64, 64, 2, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 6: return launch_s<64, 32, 2, 1, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 7: return launch_s<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     default:
       g_err = "gemm_x3s: unknown config";
       return -1;
@@ -592,7 +644,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 17) return -1;
+  if (cfg < 0 || cfg > 24) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -641,6 +693,13 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 15: return launch_d<32, 64, 1, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 16: return launch_d<32, 64, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 17: return launch_d<64, 32, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 18: return launch_d<64, 64, 2, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 19: return launch_d<64, 64, 2, 2, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 20: return launch_d<64, 32, 2, 1, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 21: return launch_d<32, 64, 1, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 22: return launch_d<64, 32, 2, 1, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 23: return launch_d<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 24: return launch_d<64, 128, 2, 4, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

@@ -82,14 +82,31 @@ void track(void* p, size_t bytes) {
   if (live > g_peak.load()) g_peak = live;
 }
 
-void untrack(void* p) {
-  if (!p) return;
+// Removes p's entry BEFORE the real free and returns its size (0 if untracked): once the runtime
+// has freed p, another thread's allocation may get the same address and track it, so an entry
+// removed after the free could be that thread's. The bytes stay charged until the free succeeded.
+size_t take(void* p) {
+  if (!p) return 0;
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_sizes->find(p);
-  if (it != g_sizes->end()) {
-    g_live -= it->second;
-    g_sizes->erase(it);
+  if (it == g_sizes->end()) return 0;
+  const size_t n = it->second;
+  g_sizes->erase(it);
+  return n;
+}
+
+template <typename Free>
+hipErr guarded_free(void* ptr, Free&& free_fn) {
+  init_once();
+  const size_t n = take(ptr);
+  const hipErr rc = free_fn();
+  if (rc == kSuccess) {
+    g_live -= n;
+  } else if (n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    (*g_sizes)[ptr] = n;  // still allocated: keep it on the books
   }
+  return rc;
 }
 
 template <typename Alloc>
@@ -134,18 +151,12 @@ hipErr hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
 
 hipErr hipFree(void* ptr) {
   static auto real = next<hipErr (*)(void*)>("hipFree");
-  init_once();
-  hipErr rc = real(ptr);
-  if (rc == kSuccess) untrack(ptr);
-  return rc;
+  return guarded_free(ptr, [&] { return real(ptr); });
 }
 
 hipErr hipFreeAsync(void* ptr, void* stream) {
   static auto real = next<hipErr (*)(void*, void*)>("hipFreeAsync");
-  init_once();
-  hipErr rc = real(ptr, stream);
-  if (rc == kSuccess) untrack(ptr);
-  return rc;
+  return guarded_free(ptr, [&] { return real(ptr, stream); });
 }
 
 hipErr hipMemGetInfo(size_t* free_b, size_t* total_b) {

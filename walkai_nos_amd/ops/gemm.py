@@ -208,12 +208,17 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             11: (128, 128, 3, "d"), 12: (64, 64, 2, "d"),
             13: (128, 128, 3, "d8"), 14: (128, 128, 2, "d8"),
             15: (32, 64, 3, "d2"), 16: (32, 64, 2, "d2"), 17: (64, 32, 2, "d2"),
+            # 64-deep stages: whole 128-byte row segments per DMA lane group (K % 64 == 0)
+            18: (64, 64, 2, "d64"), 19: (64, 64, 3, "d64"), 20: (64, 32, 2, "d64"), 21: (32, 64, 2, "d64"),
+            22: (64, 32, 3, "d64"), 23: (128, 64, 2, "d864"), 24: (64, 128, 2, "d864"),
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
-            104: (128, 64, 3, "p")}
+            104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864")}
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
-                   13: 1, 14: 1, 15: 2, 16: 4, 17: 4, 100: 2, 101: 3, 102: 1, 103: 1, 104: 1}
+                   13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
+                   18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1,
+                   100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
@@ -252,7 +257,8 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
 def x3_eligible(N: int, Kd: int) -> list:
     if Kd % 32:
         return []
-    return [c for c, (bm, bn, _, _) in X3_TILES.items() if N % bn == 0]
+    return [c for c, (bm, bn, _, kind) in X3_TILES.items()
+            if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0)]
 
 
 def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
