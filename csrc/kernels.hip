@@ -153,6 +153,18 @@ constexpr int HD = 64;
 
 __device__ __forceinline__ int key_of(int reg, int half) { return (reg & 3) + 8 * (reg >> 2) + 4 * half; }
 
+// lane l and lane l^32 combined without the LDS crossbar: v_permlane32_swap with the value as both
+// operands leaves {x[l%32]} in one result and {x[32 + l%32]} in the other, on every lane (a VALU op,
+// where __shfl_xor's ds_bpermute is an LDS round trip on the softmax critical path)
+__device__ __forceinline__ float half_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float half_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Online-softmax flash attention over key blocks [kb0, kb1) (32 keys each) for the 32 queries
 // q0..q0+31 of one head. Returns the unnormalised O^T accumulators and the running (m, l).
 struct AttnAcc {
@@ -224,7 +236,7 @@ __device__ __forceinline__ AttnAcc attn_segment(const float* __restrict__ base, 
     float mx = s[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s[r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = half_max(mx);
     const float m_new = fmaxf(a.m, mx);
     const float alpha = __builtin_amdgcn_exp2f(a.m - m_new);
     float psum = 0.f;
@@ -233,7 +245,7 @@ __device__ __forceinline__ AttnAcc attn_segment(const float* __restrict__ base, 
       s[r] = __builtin_amdgcn_exp2f(s[r] - m_new);
       psum += s[r];
     }
-    psum += __shfl_xor(psum, 32, 64);
+    psum = half_sum(psum);
     a.l = a.l * alpha + psum;
     a.m = m_new;
 #pragma unroll
@@ -491,7 +503,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
         float mx = sacc[0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sacc[r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = half_max(mx);
         const float m_new = fmaxf(m, mx);
         const float alpha = __builtin_amdgcn_exp2f(m - m_new);
         float psum = 0.f;
@@ -500,7 +512,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
           sacc[r] = __builtin_amdgcn_exp2f(sacc[r] - m_new);
           psum += sacc[r];
         }
-        psum += __shfl_xor(psum, 32, 64);
+        psum = half_sum(psum);
         l = l * alpha + psum;
         m = m_new;
 #pragma unroll
@@ -805,7 +817,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
     }                                                                                                \
     float mx = fmaxf(sacc[0], sacc[1]);                                                              \
     _Pragma("unroll") for (int r = 2; r < 16; ++r) mx = fmaxf(mx, sacc[r]);                          \
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));                                                          \
+    mx = half_max(mx);                                                          \
     if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {                                 \
       const float m_new = fmaxf(m, mx);                                                              \
       const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);                         \
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
       sacc[r] = __builtin_amdgcn_exp2f(fmaf(sacc[r], scale_log2e, -mc));                             \
       psum += sacc[r];                                                                               \
     }                                                                                                \
-    psum += __shfl_xor(psum, 32, 64);                                                                \
+    psum = half_sum(psum);                                                                \
     l += psum;                                                                                       \
     const __bf16* vs = &lds_v[buf * 3 * XV_PLANE + vtr];                                             \
     _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                                               \
@@ -988,70 +1000,71 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
     float m = -INFINITY, l = 0.f;
     if (active) X3P_QK(scur, 0)
     __syncthreads();  // iteration 0 refills K buffer 0, which the line above reads
-    for (int i = 0; i < nb; ++i) {
-      const int blk = kb0 + i;
-      const bool more_k = i + 2 < nb, more_v = i + 1 < nb;
-      if (more_k) fetch_k(blk + 2);
-      if (more_v) fetch_v(blk + 1);
-      if (active) {
-        if (blk * 32 + 32 > T) {
-          asm volatile("; tail block: mask keys >= T" ::: "memory");
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (blk * 32 + key_of(r, hf) >= T) scur[r] = -INFINITY;
-        }
-        float mx = fmaxf(scur[0], scur[1]);
-#pragma unroll
-        for (int r = 2; r < 16; ++r) mx = fmaxf(mx, scur[r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {
-          const float m_new = fmaxf(m, mx);
-          const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);
-          l *= alpha;
-          o0 *= alpha;
-          o1 *= alpha;
-          m = m_new;
-        }
-        // block i+1's scores (the last iteration computes a throwaway product of the other
-        // K buffer: an unconditional MFMA burst keeps this one basic block for the scheduler)
-        f32x16 snext;
-        X3P_QK(snext, (i + 1) & 1)
-        const float mc = m * scale_log2e;
-        float psum = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          scur[r] = __builtin_amdgcn_exp2f(fmaf(scur[r], scale_log2e, -mc));
-          psum += scur[r];
-        }
-        psum += __shfl_xor(psum, 32, 64);
-        l += psum;
-        const __bf16* vs = &lds_v[(i & 1) * 3 * XV_PLANE + vtr];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          bf16x8 p0, p1, p2;
-          split3_trunc8(scur, 8 * s2, p0, p1, p2);
-#pragma unroll
-          for (int dh = 0; dh < 2; ++dh) {
-            bf16x8 vf[3];
-#pragma unroll
-            for (int p = 0; p < 3; ++p) {
-              const __bf16* a = vs + p * XV_PLANE + 16 * s2 * XV_STR + 32 * dh;
-              const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));
-              const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 8 * XV_STR));
-              vf[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            }
-            if (dh == 0)
-              o0 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o0);
-            else
-              o1 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o1);
-          }
-        }
-        scur = snext;
-      }
-      if (more_k) stash_k(i & 1);
-      if (more_v) stash_v((i + 1) & 1);
-      __syncthreads();
+// One key block: softmax + P.V of block i from SC while block i+1's scores go to SN; the loop
+// alternates the two registers sets (no copy of the 16 scores per block).
+#define X3P_ITER(SC, SN)                                                                                  \
+  {                                                                                                       \
+      const int blk = kb0 + i;                                                                            \
+      const bool more_k = i + 2 < nb, more_v = i + 1 < nb;                                                \
+      if (more_k) fetch_k(blk + 2);                                                                       \
+      if (more_v) fetch_v(blk + 1);                                                                       \
+      if (active) {                                                                                       \
+        if (blk * 32 + 32 > T) {                                                                          \
+          asm volatile("; tail block: mask keys >= T" ::: "memory");                                      \
+          _Pragma("unroll") for (int r = 0; r < 16; ++r)                                                  \
+            if (blk * 32 + key_of(r, hf) >= T) SC[r] = -INFINITY;                                         \
+        }                                                                                                 \
+        float mx = fmaxf(SC[0], SC[1]);                                                                   \
+        _Pragma("unroll") for (int r = 2; r < 16; ++r) mx = fmaxf(mx, SC[r]);                             \
+        mx = half_max(mx);                                                                                \
+        if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {                                  \
+          const float m_new = fmaxf(m, mx);                                                               \
+          const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);                          \
+          l *= alpha;                                                                                     \
+          o0 *= alpha;                                                                                    \
+          o1 *= alpha;                                                                                    \
+          m = m_new;                                                                                      \
+        }                                                                                                 \
+                /* block i+1's scores (the last block: a throwaway product keeps one basic block) */ X3P_QK(SN, (i + 1) & 1)                                                                   \
+        const float mc = m * scale_log2e;                                                                 \
+        float psum = 0.f;                                                                                 \
+        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                                  \
+          SC[r] = __builtin_amdgcn_exp2f(fmaf(SC[r], scale_log2e, -mc));                                  \
+          psum += SC[r];                                                                                  \
+        }                                                                                                 \
+        psum = half_sum(psum);                                                                            \
+        l += psum;                                                                                        \
+        const __bf16* vs = &lds_v[(i & 1) * 3 * XV_PLANE + vtr];                                          \
+        _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                                                \
+          bf16x8 p0, p1, p2;                                                                              \
+          split3_trunc8(SC, 8 * s2, p0, p1, p2);                                                          \
+          _Pragma("unroll") for (int dh = 0; dh < 2; ++dh) {                                              \
+            bf16x8 vf[3];                                                                                 \
+            _Pragma("unroll") for (int p = 0; p < 3; ++p) {                                               \
+              const __bf16* a = vs + p * XV_PLANE + 16 * s2 * XV_STR + 32 * dh;                           \
+              const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));               \
+              const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 8 * XV_STR));  \
+              vf[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};                     \
+            }                                                                                             \
+            if (dh == 0)                                                                                  \
+              o0 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o0);                                          \
+            else                                                                                          \
+              o1 = mfma_x3(vf[0], vf[1], vf[2], p0, p1, p2, o1);                                          \
+          }                                                                                               \
+        }                                                                                                 \
+      }                                                                                                   \
+      if (more_k) stash_k(i & 1);                                                                         \
+      if (more_v) stash_v((i + 1) & 1);                                                                   \
+      __syncthreads();                                                                                    \
+  }
+    f32x16 snext;
+    for (int i = 0; i < nb;) {
+      X3P_ITER(scur, snext)
+      if (++i >= nb) break;
+      X3P_ITER(snext, scur)
+      ++i;
     }
+#undef X3P_ITER
 #undef X3P_QK
 
     if (active) {
