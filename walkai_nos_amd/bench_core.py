@@ -199,7 +199,8 @@ class NodeBench:
         self.pods_samples: List[int] = []
         self.pending_samples: List[int] = []
         self.slots: Dict[Tuple[str, int], Slot] = {}
-        self._inflight: List[Any] = []   # completion events of the last enqueued epoch
+        self._inflight: List[List[Any]] = []  # completion events of the enqueued epochs, oldest first
+        self._mode: frozenset = frozenset()   # compute modes of this GPU's pods in the last epoch
         # host-side time split of the timed steps: control plane / waiting for the GPU / enqueue
         self.host_s = {"control": 0.0, "wait": 0.0, "enqueue": 0.0}
         self.gpu = gpu_data_plane
@@ -266,24 +267,35 @@ class NodeBench:
         return out
 
     def data_step(self) -> int:
-        """Enqueue this epoch's inferences. The previous epoch's GPU work must be complete first
-        (the control plane of this epoch ran on the CPU meanwhile): at most one epoch is in
-        flight, so the slots running concurrently always belong to one partition layout and a GPU
-        never executes the backlog of an old mode alongside its new one. (Queueing the next epoch
-        behind GPU-side stream waits instead measured 15% slower: 243 vs 284 inf/s.)"""
+        """Enqueue this epoch's inferences on the partitions' streams.
+
+        While this GPU keeps its compute mode, the pods' partitions are unchanged and their streams
+        simply run on: the epoch is queued behind the previous one (at most two epochs in flight,
+        so the host never runs far ahead), as pods on real partitions keep serving while the
+        control plane works. When the mode changes (a flip re-partitions the GPU, which the agent
+        only does on an idle GPU), every queued inference of the old layout must finish first, so
+        the slots of two layouts never run side by side. (Queueing every epoch behind GPU-side
+        stream waits instead measured slower: 243 vs 284 inf/s.)"""
         t0 = time.perf_counter()
+        pods = self.my_pods()
+        mode = frozenset(prof.split("_")[0] for prof, _, _ in pods)
         if self.gpu:
-            for ev in self._inflight:
-                ev.synchronize()
-            self._inflight = []
+            keep = 1 if mode == self._mode else 0
+            while len(self._inflight) > keep:
+                for ev in self._inflight.pop(0):
+                    ev.synchronize()
+        self._mode = mode
         t1 = time.perf_counter()
         n = 0
-        for prof, part, work in self.my_pods():
+        marks = []
+        for prof, part, work in pods:
             if self.gpu:
                 slot = self.slots[(prof, part)]
                 slot.run(work)
-                self._inflight.append(slot.mark())
+                marks.append(slot.mark())
             n += work
+        if self.gpu:
+            self._inflight.append(marks)
         self.inferences += n
         self.host_s["wait"] += t1 - t0
         self.host_s["enqueue"] += time.perf_counter() - t1
