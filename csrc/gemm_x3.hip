@@ -236,34 +236,64 @@ int launch(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* 
 // Fused epilogue of a wave's TM x TN accumulators at rows r0.., columns c0..: register r of
 // acc[a][b] is C[r0 + 32a + acc_row(r, hf)][c0 + 32b + j]; bias, exact GELU, residuals; fp32 and/or
 // x3 planes out.
+__device__ __forceinline__ void store_one(float v, size_t idx, float* __restrict__ C, __bf16* __restrict__ Cp,
+                                          size_t c_plane) {
+  if (C) C[idx] = v;
+  if (Cp) {
+    const __bf16 h0 = (__bf16)v;
+    const float r1 = v - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    Cp[idx] = h0;
+    Cp[c_plane + idx] = h1;
+    Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
+  }
+}
+
 template <int TM, int TN>
 __device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][TN], int r0, int c0, int j, int hf,
                                            const float* __restrict__ bias, const float* __restrict__ R,
                                            const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
                                            __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int epi) {
+  // Epilogue operands are loaded for all 16 rows of an accumulator at once, from clamped (always
+  // valid) rows, and only the stores are predicated on row < M: a per-element "if (row < M) load"
+  // becomes a branch and a vmcnt(0) per element (16 dependent memory round trips per accumulator).
 #pragma unroll
   for (int b = 0; b < TN; ++b) {
     const int col = c0 + 32 * b + j;
     const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
+      float v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = r0 + 32 * a + acc_row(r, hf);
-        if (row >= M) continue;
-        float v = acc[a][b][r] + bv;
-        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-        const size_t idx = size_t(row) * N + col;
-        if (epi & EPI_RES) v += R[idx];
-        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];
-        if (C) C[idx] = v;
-        if (Cp) {
-          const __bf16 h0 = (__bf16)v;
-          const float r1 = v - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          Cp[idx] = h0;
-          Cp[c_plane + idx] = h1;
-          Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
+      for (int r = 0; r < 16; ++r) v[r] = acc[a][b][r] + bv;
+      if (epi & EPI_RES) {
+        float rv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) rv[r] = R[size_t(min(r0 + 32 * a + acc_row(r, hf), M - 1)) * N + col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] += rv[r];
+      }
+      if (epi & EPI_RES2) {
+        float rv[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          rv[r] = R2[size_t(min(r0 + 32 * a + acc_row(r, hf), M - 1) % r2_rows) * N + col];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] += rv[r];
+      }
+      if (epi & EPI_GELU) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
+      }
+      // full 32-row blocks (all but the last row of tiles) store without per-element predicates
+      if (r0 + 32 * a + 32 <= M) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) store_one(v[r], size_t(r0 + 32 * a + acc_row(r, hf)) * N + col, C, Cp, c_plane);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = r0 + 32 * a + acc_row(r, hf);
+          if (row < M) store_one(v[r], size_t(row) * N + col, C, Cp, c_plane);
         }
       }
     }
@@ -426,6 +456,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
     vm_wait<(S - 2) * NLD>(); /* this wave's DMA of stage KS has landed */         \
     raw_barrier();            /* everyone's has; stage KS-1's buffer is free */    \
     X3D_ISSUE((KS) + S - 1, ((BUF) + S - 1) % S)                                   \
+    __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */ \
     compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf); \
   }
   X3D_ISSUE(0, 0)
@@ -534,6 +565,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
     vm_wait<(S - 2) * NLD>();                                                             \
     raw_barrier();                                                                        \
     X3S_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
+    __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */         \
     compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);    \
     if (((G) + 1) % nk == 0) {                                                            \
       const int t_ = tb + ((G) / nk) * ts;                                                \
@@ -598,21 +630,22 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // half the LDS, more resident tiles); 7-12 = LDS-DMA pipeline with nbuf = S stages (S-1 in
 // flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2; 13/14 = 128x128 on 8 waves
 // S3/S2; 15-17 = 2-wave 32x64 S3/S2, 64x32 S2; 18-22 = 64-deep stages (128-byte row segments):
-// 64x64 S2/S3, 64x32 S2, 32x64 S2, 64x32 S3; 23/24 = 64-deep on 8 waves: 128x64 S2, 64x128 S2.
-static const int kCfgX3[25][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// 64x64 S2/S3, 64x32 S2, 32x64 S2, 64x32 S3; 23/24 = 64-deep on 8 waves: 128x64 S2, 64x128 S2;
+// 25/26 = 128x64 S4, 64x128 S4 (three stages in flight).
+static const int kCfgX3[27][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
                                   {32, 64, 3}, {32, 64, 2}, {64, 32, 2},
                                   {64, 64, 2}, {64, 64, 3}, {64, 32, 2}, {32, 64, 2}, {64, 32, 3},
-                                  {128, 64, 2}, {64, 128, 2}};
+                                  {128, 64, 2}, {64, 128, 2}, {128, 64, 4}, {64, 128, 4}};
 
-int nos_gemm_x3_num_configs() { return 25; }
+int nos_gemm_x3_num_configs() { return 27; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
 // cfg: 0 = 64x64 S3 (4 waves), 1 = 64x64 S2, 2 = 128x128 S3 (8 waves), 3 = 64x128 S3, 4 = 128x64 S3;
-// 64-deep stages: 5 = 64x64 S2, 6 = 64x32 S2 (2 waves), 7 = 128x64 S2 (8 waves).
+// 64-deep stages: 5 = 64x64 S2, 6 = 64x32 S2 (2 waves), 7 = 128x64 S2 (8 waves); 8/9 = 128x64, 64x128 S4.
 int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, const float* bias, const float* R,
                            const float* R2, int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi,
                            int cfg, int grid, void* stream) {
@@ -637,6 +670,8 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
     case 5: return launch_s<64, 64, 2, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 6: return launch_s<64, 32, 2, 1, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 7: return launch_s<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 8: return launch_s<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 9: return launch_s<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     default:
       g_err = "gemm_x3s: unknown config";
       return -1;
@@ -644,7 +679,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 24) return -1;
+  if (cfg < 0 || cfg > 26) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -700,6 +735,8 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 22: return launch_d<64, 32, 2, 1, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 23: return launch_d<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 24: return launch_d<64, 128, 2, 4, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 25: return launch_d<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 26: return launch_d<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

@@ -211,14 +211,16 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             # 64-deep stages: whole 128-byte row segments per DMA lane group (K % 64 == 0)
             18: (64, 64, 2, "d64"), 19: (64, 64, 3, "d64"), 20: (64, 32, 2, "d64"), 21: (32, 64, 2, "d64"),
             22: (64, 32, 3, "d64"), 23: (128, 64, 2, "d864"), 24: (64, 128, 2, "d864"),
+            25: (128, 64, 4, "d"), 26: (64, 128, 4, "d"),
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
-            104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864")}
+            104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
+            108: (128, 64, 4, "p"), 109: (64, 128, 4, "p")}
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
-                   18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1,
-                   100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1}
+                   18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1,
+                   100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
