@@ -29,6 +29,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 namespace {
 thread_local std::string g_err;
 
+
 enum : int { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RES = 4, EPI_RES2 = 8 };
 constexpr int BK = 32, LSTR = 40;
 
@@ -119,6 +120,75 @@ __device__ __forceinline__ void compute_stage(f32x16 (&acc)[WM / 32][WN / 32], c
   }
 }
 
+__device__ __forceinline__ void store_one(float v, size_t idx, float* __restrict__ C, __bf16* __restrict__ Cp,
+                                          size_t c_plane) {
+  if (C) C[idx] = v;
+  if (Cp) {
+    const __bf16 h0 = (__bf16)v;
+    const float r1 = v - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    Cp[idx] = h0;
+    Cp[c_plane + idx] = h1;
+    Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
+  }
+}
+
+// Epilogue math of one 32x32 accumulator: bias, GELU, residuals (the API order). Operands are loaded for all 16
+// rows at once, from clamped (always valid) rows: a per-element "if (row < M) load" becomes a
+// branch and a vmcnt(0) per element (16 dependent memory round trips per accumulator).
+__device__ __forceinline__ void epi_values(const f32x16& acc, float (&v)[16], int rb, int col, int hf, float bv,
+                                           const float* __restrict__ R, const float* __restrict__ R2, int r2_rows,
+                                           int M, int N, int epi) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = acc[r] + bv;
+  if (epi & EPI_GELU) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
+  }
+  if (epi & EPI_RES) {
+    float rv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rv[r] = R[size_t(min(rb + acc_row(r, hf), M - 1)) * N + col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += rv[r];
+  }
+  if (epi & EPI_RES2) {
+    float rv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rv[r] = R2[size_t(min(rb + acc_row(r, hf), M - 1) % r2_rows) * N + col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] += rv[r];
+  }
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][TN], int r0, int c0, int j, int hf,
+                                           const float* __restrict__ bias, const float* __restrict__ R,
+                                           const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
+                                           __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int epi) {
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = c0 + 32 * b + j;
+    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      float v[16];
+      epi_values(acc[a][b], v, r0 + 32 * a, col, hf, bv, R, R2, r2_rows, M, N, epi);
+      // full 32-row blocks (all but the last row of tiles) store without per-element predicates
+      if (r0 + 32 * a + 32 <= M) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) store_one(v[r], size_t(r0 + 32 * a + acc_row(r, hf)) * N + col, C, Cp, c_plane);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = r0 + 32 * a + acc_row(r, hf);
+          if (row < M) store_one(v[r], size_t(row) * N + col, C, Cp, c_plane);
+        }
+      }
+    }
+  }
+}
+
 template <int WM, int WN, int NBUF>
 __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, size_t a_plane,
                                                  const __bf16* __restrict__ W, size_t w_plane,
@@ -185,33 +255,7 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
 #undef X3_LOAD
 
   // epilogue: acc[a][b] register r is C[m0 + wm*WM + 32a + acc_row(r, hf)][n0 + wn*WN + 32b + j]
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int col = n0 + wn * WN + 32 * b + j;
-    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * WM + 32 * a + acc_row(r, hf);
-        if (row >= M) continue;
-        float v = acc[a][b][r] + bv;
-        if (epi & EPI_GELU) v = 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-        const size_t idx = size_t(row) * N + col;
-        if (epi & EPI_RES) v += R[idx];
-        if (epi & EPI_RES2) v += R2[size_t(row % r2_rows) * N + col];
-        if (C) C[idx] = v;
-        if (Cp) {
-          const __bf16 h0 = (__bf16)v;
-          const float r1 = v - (float)h0;
-          const __bf16 h1 = (__bf16)r1;
-          Cp[idx] = h0;
-          Cp[c_plane + idx] = h1;
-          Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
-        }
-      }
-    }
-  }
+  store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
 template <int WM, int WN, int NBUF>
@@ -236,70 +280,6 @@ int launch(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* 
 // Fused epilogue of a wave's TM x TN accumulators at rows r0.., columns c0..: register r of
 // acc[a][b] is C[r0 + 32a + acc_row(r, hf)][c0 + 32b + j]; bias, exact GELU, residuals; fp32 and/or
 // x3 planes out.
-__device__ __forceinline__ void store_one(float v, size_t idx, float* __restrict__ C, __bf16* __restrict__ Cp,
-                                          size_t c_plane) {
-  if (C) C[idx] = v;
-  if (Cp) {
-    const __bf16 h0 = (__bf16)v;
-    const float r1 = v - (float)h0;
-    const __bf16 h1 = (__bf16)r1;
-    Cp[idx] = h0;
-    Cp[c_plane + idx] = h1;
-    Cp[2 * c_plane + idx] = (__bf16)(r1 - (float)h1);
-  }
-}
-
-template <int TM, int TN>
-__device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][TN], int r0, int c0, int j, int hf,
-                                           const float* __restrict__ bias, const float* __restrict__ R,
-                                           const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
-                                           __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int epi) {
-  // Epilogue operands are loaded for all 16 rows of an accumulator at once, from clamped (always
-  // valid) rows, and only the stores are predicated on row < M: a per-element "if (row < M) load"
-  // becomes a branch and a vmcnt(0) per element (16 dependent memory round trips per accumulator).
-#pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int col = c0 + 32 * b + j;
-    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-      float v[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = acc[a][b][r] + bv;
-      if (epi & EPI_RES) {
-        float rv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) rv[r] = R[size_t(min(r0 + 32 * a + acc_row(r, hf), M - 1)) * N + col];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] += rv[r];
-      }
-      if (epi & EPI_RES2) {
-        float rv[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          rv[r] = R2[size_t(min(r0 + 32 * a + acc_row(r, hf), M - 1) % r2_rows) * N + col];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] += rv[r];
-      }
-      if (epi & EPI_GELU) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
-      }
-      // full 32-row blocks (all but the last row of tiles) store without per-element predicates
-      if (r0 + 32 * a + 32 <= M) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) store_one(v[r], size_t(r0 + 32 * a + acc_row(r, hf)) * N + col, C, Cp, c_plane);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = r0 + 32 * a + acc_row(r, hf);
-          if (row < M) store_one(v[r], size_t(row) * N + col, C, Cp, c_plane);
-        }
-      }
-    }
-  }
-}
-
 // ---- LDS-DMA variant ---------------------------------------------------------------------------
 // Same math and epilogue; the operand tiles go global -> LDS with global_load_lds_dwordx4 (no
 // register staging), S LDS buffers deep, so S-1 stages of loads are in flight behind the MFMAs at
@@ -316,6 +296,27 @@ template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// Wait until this wave's DMA of the current stage has landed when `rem` younger stages (at most
+// S-2) have been issued behind it: vmcnt needs an immediate, so the tail of the K loop (fewer
+// younger stages in flight) takes the smaller waits by a wave-uniform branch.
+template <int S, int NLD>
+__device__ __forceinline__ void vm_wait_stage(int rem) {
+  const int r = min(S - 2, rem);
+  if constexpr (S > 3) {
+    if (r >= 2) {
+      vm_wait<2 * NLD>();
+      return;
+    }
+  }
+  if constexpr (S > 2) {
+    if (r >= 1) {
+      vm_wait<NLD>();
+      return;
+    }
+  }
+  vm_wait<0>();
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -444,12 +445,16 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   dma_offsets<BN, NW, BKS>(voff_b, n0, N - 1, K, wave, lane);
 #define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
 #define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
-// past the end a stage re-reads the last one, so every iteration issues NLD loads (static vmcnt)
+// No DMA is issued past the last stage: a load still landing in a buffer after the loop would
+// race with the epilogue's reuse of the stage buffers (measured: corrupted epilogue rows on the
+// 2-workgroups-per-CU 64x64 S3 tile when the tail re-issued the last stage into A0/A1). The steady
+// loop only runs while every issue is in range (static vmcnt, unconditional DMA); the last
+// iterations run a tail with a bounds-checked issue and the smaller waits (vm_wait_stage).
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
-    const int k0_ = min((STAGE), nk - 1) * BKS;                                    \
+    const int k0_ = (STAGE) * BKS;                                                 \
     dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave);            \
-    dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);                 \
+    dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);            \
   }
 #define X3D_ITER(KS, BUF)                                                          \
   {                                                                                \
@@ -459,25 +464,30 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
     __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */ \
     compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf); \
   }
-  X3D_ISSUE(0, 0)
-  if constexpr (S > 2) X3D_ISSUE(1, 1)
-  if constexpr (S > 3) X3D_ISSUE(2, 2)
+  for (int st = 0; st < S - 1; ++st)
+    if (st < nk) X3D_ISSUE(st, st)
   int ks = 0;
-  for (; ks + S <= nk; ks += S) {
+  for (; ks + 2 * S - 1 <= nk; ks += S) {
     X3D_ITER(ks, 0)
     X3D_ITER(ks + 1, 1)
     if constexpr (S > 2) X3D_ITER(ks + 2, 2)
     if constexpr (S > 3) X3D_ITER(ks + 3, 3)
   }
-  if (ks < nk) X3D_ITER(ks, 0)
-  if (ks + 1 < nk) X3D_ITER(ks + 1, 1)
-  if constexpr (S > 3)
-    if (ks + 2 < nk) X3D_ITER(ks + 2, 2)
+  for (; ks < nk; ++ks) {
+    const int buf = ks % S;
+    vm_wait_stage<S, NLD>(nk - 1 - ks);
+    raw_barrier();
+    if (ks + S - 1 < nk) X3D_ISSUE(ks + S - 1, (buf + S - 1) % S)
+    __builtin_amdgcn_sched_barrier(0);
+    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(buf), X3D_B(buf), wm, wn, j, hf);
+  }
 #undef X3D_ITER
 #undef X3D_ISSUE
 #undef X3D_B
 #undef X3D_A
   vm_wait<0>();  // no DMA may still target this workgroup's LDS when it retires
+  // direct stores: each instruction writes whole 64/128-byte row segments of two rows (measured
+  // faster here than re-shaping the tile for wider per-lane vectors, through LDS or lane quads)
   store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
@@ -549,10 +559,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
 
 #define X3S_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
 #define X3S_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
-// stage h of the stream (past the end: the last stage again, so vmcnt accounting stays static)
+// stage h of the stream (none past the end: steady loop + bounds-checked tail, as in gemm_x3d)
 #define X3S_ISSUE(H, BUF)                                                                 \
   {                                                                                       \
-    const int h_ = min((H), total - 1);                                                   \
+    const int h_ = (H);                                                                   \
     const int ti_ = h_ / nk, ks_ = h_ - ti_ * nk, t_ = tb + ti_ * ts;                     \
     uint32_t va_[BM / RPI / NW], vb_[BN / RPI / NW];                                      \
     dma_offsets<BM, NW, BKS>(va_, (t_ / tiles_n) * BM, M - 1, K, wave, lane);             \
@@ -560,12 +570,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
     dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3S_A(BUF), wave);                 \
     dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3S_B(BUF), wave);                 \
   }
-#define X3S_ITER(G, BUF)                                                                  \
+#define X3S_BODY(G, BUF)                                                                  \
   {                                                                                       \
-    vm_wait<(S - 2) * NLD>();                                                             \
-    raw_barrier();                                                                        \
-    X3S_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
-    __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */         \
     compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);    \
     if (((G) + 1) % nk == 0) {                                                            \
       const int t_ = tb + ((G) / nk) * ts;                                                \
@@ -575,20 +581,32 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
         _Pragma("unroll") for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};             \
     }                                                                                     \
   }
-  X3S_ISSUE(0, 0)
-  if constexpr (S > 2) X3S_ISSUE(1, 1)
-  if constexpr (S > 3) X3S_ISSUE(2, 2)
+#define X3S_ITER(G, BUF)                                                                  \
+  {                                                                                       \
+    vm_wait<(S - 2) * NLD>();                                                             \
+    raw_barrier();                                                                        \
+    X3S_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
+    __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */         \
+    X3S_BODY(G, BUF)                                                                      \
+  }
+  for (int st = 0; st < S - 1; ++st)
+    if (st < total) X3S_ISSUE(st, st)
   int g = 0;
-  for (; g + S <= total; g += S) {
+  for (; g + 2 * S - 1 <= total; g += S) {
     X3S_ITER(g, 0)
     X3S_ITER(g + 1, 1)
     if constexpr (S > 2) X3S_ITER(g + 2, 2)
     if constexpr (S > 3) X3S_ITER(g + 3, 3)
   }
-  if (g < total) X3S_ITER(g, 0)
-  if (g + 1 < total) X3S_ITER(g + 1, 1)
-  if constexpr (S > 3)
-    if (g + 2 < total) X3S_ITER(g + 2, 2)
+  for (; g < total; ++g) {
+    const int buf = g % S;
+    vm_wait_stage<S, NLD>(total - 1 - g);
+    raw_barrier();
+    if (g + S - 1 < total) X3S_ISSUE(g + S - 1, (buf + S - 1) % S)
+    __builtin_amdgcn_sched_barrier(0);
+    X3S_BODY(g, buf)
+  }
+#undef X3S_BODY
 #undef X3S_ITER
 #undef X3S_ISSUE
 #undef X3S_B
