@@ -445,11 +445,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   dma_offsets<BN, NW, BKS>(voff_b, n0, N - 1, K, wave, lane);
 #define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
 #define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
-// No DMA is issued past the last stage: a load still landing in a buffer after the loop would
-// race with the epilogue's reuse of the stage buffers (measured: corrupted epilogue rows on the
-// 2-workgroups-per-CU 64x64 S3 tile when the tail re-issued the last stage into A0/A1). The steady
-// loop only runs while every issue is in range (static vmcnt, unconditional DMA); the last
-// iterations run a tail with a bounds-checked issue and the smaller waits (vm_wait_stage).
+// No DMA is issued past the last stage, so when the loop ends no load can still be landing in a
+// stage buffer (and no bandwidth goes to dead re-reads). The steady loop only runs while every
+// issue is in range (static vmcnt, unconditional DMA); the last iterations run a tail with a
+// bounds-checked issue and the smaller waits (vm_wait_stage).
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
     const int k0_ = (STAGE) * BKS;                                                 \
@@ -486,8 +485,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #undef X3D_B
 #undef X3D_A
   vm_wait<0>();  // no DMA may still target this workgroup's LDS when it retires
-  // direct stores: each instruction writes whole 64/128-byte row segments of two rows (measured
-  // faster here than re-shaping the tile for wider per-lane vectors, through LDS or lane quads)
+  // direct stores: each instruction writes whole 64/128-byte row segments of two rows. Re-shaping
+  // the tile for wider per-lane vectors was measured: through lane-quad DPP transposes it was
+  // slower; through an LDS scratch in the freed stage buffers it was faster but produced
+  // run-to-run differences whenever several workgroups shared a CU (tools/x3_gemm_stress.py),
+  // cause not pinned down, so it is not used.
   store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
