@@ -201,6 +201,8 @@ class NodeBench:
         self.slots: Dict[Tuple[str, int], Slot] = {}
         self._inflight: List[List[Any]] = []  # completion events of the enqueued epochs, oldest first
         self._mode: frozenset = frozenset()   # compute modes of this GPU's pods in the last epoch
+        self.mode_drains = 0                  # epochs that had to drain the GPU (its mode changed)
+        self.empty_epochs = 0                 # epochs with no pod on this rank's GPU
         # host-side time split of the timed steps: control plane / waiting for the GPU / enqueue
         self.host_s = {"control": 0.0, "wait": 0.0, "enqueue": 0.0}
         self.gpu = gpu_data_plane
@@ -281,6 +283,8 @@ class NodeBench:
         mode = frozenset(prof.split("_")[0] for prof, _, _ in pods)
         if self.gpu:
             keep = 1 if mode == self._mode else 0
+            if not keep and self._inflight:
+                self.mode_drains += 1
             while len(self._inflight) > keep:
                 for ev in self._inflight.pop(0):
                     ev.synchronize()
@@ -296,6 +300,8 @@ class NodeBench:
             n += work
         if self.gpu:
             self._inflight.append(marks)
+        if n == 0:
+            self.empty_epochs += 1
         self.inferences += n
         self.host_s["wait"] += t1 - t0
         self.host_s["enqueue"] += time.perf_counter() - t1
@@ -345,6 +351,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     if distributed:
         dist.barrier()
     nb.inferences = 0
+    nb.mode_drains = 0
+    nb.empty_epochs = 0
     nb.host_s = {k: 0.0 for k in nb.host_s}
     nb.util_samples.clear()
     nb.pods_samples.clear()
@@ -396,6 +404,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "pending_pods_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
         "achieved_tflops": round(value * flops / 1e12, 2),
         "host_ms_per_step": {k: round(1000.0 * v / cfg.steps, 2) for k, v in nb.host_s.items()},
+        "mode_drains": nb.mode_drains,
+        "empty_epochs": nb.empty_epochs,
         "baseline_ref": BASELINE_LABEL,
         "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
