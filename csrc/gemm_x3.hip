@@ -331,22 +331,29 @@ __device__ __forceinline__ void raw_barrier() {
 // HBM, bounds these short-K GEMMs even when every line hits L2). Chunk c of local row r sits at
 // slot c ^ swz(r), swz(r) = (r / (16/CPR)) % CPR, which makes the fragment reads (lanes j, j+32
 // on rows j of a 32-row block) conflict-free for both depths.
-template <int BKS>
+template <int BKS, bool M16 = false>
 __device__ __forceinline__ int dma_swz(int r) {
-  constexpr int CPR = BKS / 8;
-  return (r / (16 / CPR)) % CPR;
+  if constexpr (M16) {
+    // 16x16x32 fragment reads (lane l: row l%16, chunk l/16 of a 64-byte row): slot c ^ 2((r>>2)&1)
+    // puts every ds_read_b128 lane group on 16 distinct 16-byte bank slots
+    static_assert(BKS == 32, "the 16x16x32 image is defined for 32-deep stages");
+    return ((r >> 2) & 1) << 1;
+  } else {
+    constexpr int CPR = BKS / 8;
+    return (r / (16 / CPR)) % CPR;
+  }
 }
 
 // Per-lane byte offsets of this wave's DMA rows inside one plane (fixed for the whole K loop):
 // row groups g = wave + NW*i of RPI rows; lane -> row RPI*g + lane/CPR, chunk (lane%CPR) ^ swz(row).
-template <int ROWS, int NW, int BKS = 32>
+template <int ROWS, int NW, int BKS = 32, bool M16 = false>
 __device__ __forceinline__ void dma_offsets(uint32_t (&voff)[ROWS * BKS / 512 / NW], int r0, int rmax, int K,
                                             int wave, int lane) {
   constexpr int CPR = BKS / 8, RPI = 64 / CPR;
 #pragma unroll
   for (int i = 0; i < ROWS / RPI / NW; ++i) {
     const int rl = RPI * (wave + NW * i) + lane / CPR;
-    const int c = (lane % CPR) ^ dma_swz<BKS>(rl);
+    const int c = (lane % CPR) ^ dma_swz<BKS, M16>(rl);
     const int row = min(r0 + rl, rmax);
     voff[i] = uint32_t(row) * uint32_t(K) * 2u + 16u * uint32_t(c);
   }
@@ -398,9 +405,96 @@ __device__ __forceinline__ void compute_stage_sw(f32x16 (&acc)[WM / 32][WN / 32]
   }
 }
 
+// ---- 16x16x32 variant --------------------------------------------------------------------------
+// The same x3 product on v_mfma_f32_16x16x32_bf16: equal matrix-pipe cycles per FLOP, and on random
+// data the smaller shape holds a higher clock when the whole chip is power-limited (the concurrent
+// partitions of the bench). Fragment: lane l = row l%16, k 8(l/16)..+7 of a 32-deep stage; result:
+// lane l = column l%16, rows 4(l/16)..+3 of a 16x16 block.
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ f32x4 mfma_x3_16(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
+                                            const bf16x8& b1, const bf16x8& b2, f32x4 d) {
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, d, 0, 0, 0);
+  d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, d, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, d, 0, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void compute_stage16(f32x4 (&acc)[WM / 16][WN / 16], const __bf16* __restrict__ as,
+                                                const __bf16* __restrict__ bs, int wm, int wn, int lane) {
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int r16 = lane & 15;
+  const int ch = (lane >> 4) ^ dma_swz<32, true>(r16);  // rows r16 + 16a share the swizzle
+  bf16x8 af[TM][3], bfr[TN][3];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      af[a][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * 32 + (wm * WM + 16 * a + r16) * 32 + 8 * ch]);
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * 32 + (wn * WN + 16 * b + r16) * 32 + 8 * ch]);
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+      acc[a][b] = mfma_x3_16(af[a][0], af[a][1], af[a][2], bfr[b][0], bfr[b][1], bfr[b][2], acc[a][b]);
+}
+
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile16(const f32x4 (&acc)[TM][TN], int r0, int c0, int lane,
+                                             const float* __restrict__ bias, const float* __restrict__ R,
+                                             const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
+                                             __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int epi) {
+  const int cl = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = c0 + 16 * b + cl;
+    const float bv = (epi & EPI_BIAS) ? bias[col] : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+      const int rb = r0 + 16 * a + rq;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[a][b][i] + bv;
+      if (epi & EPI_GELU) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = 0.5f * v[i] * (1.f + erff(v[i] * 0.70710678118654752f));
+      }
+      if (epi & EPI_RES) {
+        float rv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[i] = R[size_t(min(rb + i, M - 1)) * N + col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += rv[i];
+      }
+      if (epi & EPI_RES2) {
+        float rv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rv[i] = R2[size_t(min(rb + i, M - 1) % r2_rows) * N + col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] += rv[i];
+      }
+      if (rb + 4 <= M) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) store_one(v[i], size_t(rb + i) * N + col, C, Cp, c_plane);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (rb + i < M) store_one(v[i], size_t(rb + i) * N + col, C, Cp, c_plane);
+      }
+    }
+  }
+}
+
 // BM x BN tile on a WGM x WGN grid of waves (4 or 8 waves: 8 gives each SIMD two waves of one
 // workgroup, so a 128x128 tile — half the bytes per MFMA of 64x64 — still hides its load latency)
-template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32, bool M16 = false>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __restrict__ A, size_t a_plane,
                                                   const __bf16* __restrict__ W, size_t w_plane,
                                                   const float* __restrict__ bias, const float* __restrict__ R,
@@ -411,6 +505,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int TM16 = WM / 16, TN16 = WN / 16;
+  static_assert(!M16 || BKS == 32, "16x16x32 tiles use 32-deep stages");
   constexpr int RPI = 512 / BKS;  // rows per DMA instruction
   static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "row groups must divide over the waves");
   constexpr int NLD = 3 * (BM / RPI / NW) + 3 * (BN / RPI / NW);  // DMA instructions per wave per stage
@@ -433,17 +529,29 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   const int wm = wave / WGN, wn = wave % WGN;
   const int j = lane & 31, hf = lane >> 5;
 
-  f32x16 acc[TM][TN];
+  f32x16 acc[M16 ? 1 : TM][M16 ? 1 : TN];
+  f32x4 acc16[M16 ? TM16 : 1][M16 ? TN16 : 1];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
+    for (int b = 0; b < TN; ++b) acc[M16 ? 0 : a][M16 ? 0 : b] = f32x16{0};
+#pragma unroll
+  for (int a = 0; a < TM16; ++a)
+#pragma unroll
+    for (int b = 0; b < TN16; ++b) acc16[M16 ? a : 0][M16 ? b : 0] = f32x4{0};
 
   const int nk = K / BKS;
   uint32_t voff_a[BM / RPI / NW], voff_b[BN / RPI / NW];
-  dma_offsets<BM, NW, BKS>(voff_a, m0, M - 1, K, wave, lane);
-  dma_offsets<BN, NW, BKS>(voff_b, n0, N - 1, K, wave, lane);
+  dma_offsets<BM, NW, BKS, M16>(voff_a, m0, M - 1, K, wave, lane);
+  dma_offsets<BN, NW, BKS, M16>(voff_b, n0, N - 1, K, wave, lane);
 #define X3D_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
+#define X3D_COMPUTE(AS, BS)                                                        \
+  {                                                                                \
+    if constexpr (M16)                                                             \
+      compute_stage16<BM, BN, WM, WN>(acc16, AS, BS, wm, wn, lane);                \
+    else                                                                           \
+      compute_stage_sw<BM, BN, WM, WN, BKS>(acc, AS, BS, wm, wn, j, hf);           \
+  }
 #define X3D_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
 // No DMA is issued past the last stage, so when the loop ends no load can still be landing in a
 // stage buffer (and no bandwidth goes to dead re-reads). The steady loop only runs while every
@@ -461,7 +569,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
     raw_barrier();            /* everyone's has; stage KS-1's buffer is free */    \
     X3D_ISSUE((KS) + S - 1, ((BUF) + S - 1) % S)                                   \
     __builtin_amdgcn_sched_barrier(0); /* issue the DMA before the stage's MFMAs */ \
-    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(BUF), X3D_B(BUF), wm, wn, j, hf); \
+    X3D_COMPUTE(X3D_A(BUF), X3D_B(BUF))                                            \
   }
   for (int st = 0; st < S - 1; ++st)
     if (st < nk) X3D_ISSUE(st, st)
@@ -478,9 +586,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
     raw_barrier();
     if (ks + S - 1 < nk) X3D_ISSUE(ks + S - 1, (buf + S - 1) % S)
     __builtin_amdgcn_sched_barrier(0);
-    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3D_A(buf), X3D_B(buf), wm, wn, j, hf);
+    X3D_COMPUTE(X3D_A(buf), X3D_B(buf))
   }
 #undef X3D_ITER
+#undef X3D_COMPUTE
 #undef X3D_ISSUE
 #undef X3D_B
 #undef X3D_A
@@ -490,10 +599,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   // slower; through an LDS scratch in the freed stage buffers it was faster but produced
   // run-to-run differences whenever several workgroups shared a CU (tools/x3_gemm_stress.py),
   // cause not pinned down, so it is not used.
-  store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
+  if constexpr (M16)
+    store_tile16<TM16, TN16>(acc16, m0 + wm * WM, n0 + wn * WN, lane, bias, R, R2, r2_rows, C, Cp, c_plane, M, N,
+                             epi);
+  else
+    store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
-template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32, bool M16 = false>
 int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
              const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
              hipStream_t s) {
@@ -506,7 +619,7 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     return -1;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS>), dim3(tiles), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
+  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(tiles), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
                      cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -651,16 +764,18 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // flight): 64x64 S3/S4, 128x64 S3, 64x128 S3, 128x128 S3, 64x64 S2; 13/14 = 128x128 on 8 waves
 // S3/S2; 15-17 = 2-wave 32x64 S3/S2, 64x32 S2; 18-22 = 64-deep stages (128-byte row segments):
 // 64x64 S2/S3, 64x32 S2, 32x64 S2, 64x32 S3; 23/24 = 64-deep on 8 waves: 128x64 S2, 64x128 S2;
-// 25/26 = 128x64 S4, 64x128 S4 (three stages in flight).
-static const int kCfgX3[27][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// 25/26 = 128x64 S4, 64x128 S4 (three stages in flight); 27-31 = v_mfma 16x16x32: 64x64 S2,
+// 64x64 S3, 128x128 S2 (8 waves), 32x64 S2 (2 waves), 64x32 S2 (2 waves).
+static const int kCfgX3[32][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
                                   {32, 64, 3}, {32, 64, 2}, {64, 32, 2},
                                   {64, 64, 2}, {64, 64, 3}, {64, 32, 2}, {32, 64, 2}, {64, 32, 3},
-                                  {128, 64, 2}, {64, 128, 2}, {128, 64, 4}, {64, 128, 4}};
+                                  {128, 64, 2}, {64, 128, 2}, {128, 64, 4}, {64, 128, 4},
+                                  {64, 64, 2}, {64, 64, 3}, {128, 128, 2}, {32, 64, 2}, {64, 32, 2}};
 
-int nos_gemm_x3_num_configs() { return 27; }
+int nos_gemm_x3_num_configs() { return 32; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
@@ -699,7 +814,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 26) return -1;
+  if (cfg < 0 || cfg > 31) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -757,6 +872,11 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 24: return launch_d<64, 128, 2, 4, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 25: return launch_d<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 26: return launch_d<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 27: return launch_d<64, 64, 2, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 28: return launch_d<64, 64, 2, 2, 3, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 29: return launch_d<128, 128, 2, 4, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 30: return launch_d<32, 64, 1, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 31: return launch_d<64, 32, 2, 1, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

@@ -14,6 +14,7 @@ count that best fills the slice's workgroup slots).
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Dict, Optional, Tuple
 
@@ -212,6 +213,9 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             18: (64, 64, 2, "d64"), 19: (64, 64, 3, "d64"), 20: (64, 32, 2, "d64"), 21: (32, 64, 2, "d64"),
             22: (64, 32, 3, "d64"), 23: (128, 64, 2, "d864"), 24: (64, 128, 2, "d864"),
             25: (128, 64, 4, "d"), 26: (64, 128, 4, "d"),
+            # v_mfma_f32_16x16x32_bf16 tiles
+            27: (64, 64, 2, "m16"), 28: (64, 64, 3, "m16"), 29: (128, 128, 2, "m16w8"), 30: (32, 64, 2, "m16w2"),
+            31: (64, 32, 2, "m16w2"),
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
             104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
@@ -219,7 +223,7 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
-                   18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1,
+                   18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 3, 28: 2, 29: 1, 30: 4, 31: 4,
                    100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
 _x3_bound = False
@@ -257,10 +261,13 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
 
 
 def x3_eligible(N: int, Kd: int) -> list:
+    """Tiles that can run this shape; ``NOS_X3_EXCLUDE`` (comma-separated kind prefixes, e.g.
+    ``m16,p``) drops tile families from autotuning for A/B measurements."""
     if Kd % 32:
         return []
+    skip = tuple(x for x in os.environ.get("NOS_X3_EXCLUDE", "").split(",") if x)
     return [c for c, (bm, bn, _, kind) in X3_TILES.items()
-            if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0)]
+            if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))]
 
 
 def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
