@@ -262,12 +262,30 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
 
 def x3_eligible(N: int, Kd: int) -> list:
     """Tiles that can run this shape; ``NOS_X3_EXCLUDE`` (comma-separated kind prefixes, e.g.
-    ``m16,p``) drops tile families from autotuning for A/B measurements."""
+    ``m16,p``) and ``NOS_X3_MIN_TILE`` (minimum BM*BN) drop tiles from autotuning for A/B runs."""
     if Kd % 32:
         return []
     skip = tuple(x for x in os.environ.get("NOS_X3_EXCLUDE", "").split(",") if x)
+    min_area = int(os.environ.get("NOS_X3_MIN_TILE", "0"))
     return [c for c, (bm, bn, _, kind) in X3_TILES.items()
-            if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))]
+            if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))
+            and bm * bn >= min_area]
+
+
+#: tiles at least this large (BM*BN) on a partition that shares the GPU with sibling partitions
+SHARED_SLICE_MIN_TILE = 8192
+
+
+def shared_slice_tiles(cands: list, cus: int) -> list:
+    """Tiles for a slice smaller than the GPU. Autotuning times each tile alone on its slice, but a
+    partition runs beside its siblings and they share every XCD's L2 and the Infinity Cache:
+    there a 128-wide tile, which moves half the operand bytes of a 64x64 one, wins although
+    the isolated timing calls them even (measured on concurrent partitions: QPX +3%, CPX +2-4%,
+    DPX/SPX unchanged; `profiles/kbench_r1_modes_min_tile.txt`). Whole-GPU slices keep every tile."""
+    if cus >= K.total_cus() or "NOS_X3_MIN_TILE" in os.environ:
+        return cands
+    big = [c for c in cands if X3_TILES[c][0] * X3_TILES[c][1] >= SHARED_SLICE_MIN_TILE]
+    return big or cands
 
 
 def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
@@ -342,6 +360,7 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
             cands = x3_eligible(N, Kd)
             if not cands:
                 raise ValueError(f"gemm_x3: unsupported shape N={N} K={Kd}")
+            cands = shared_slice_tiles(cands, cus)
             if torch.cuda.is_current_stream_capturing():
                 tile = x3_heuristic(M, N, cus, cands)
             else:

@@ -46,7 +46,23 @@ def set_slice_cus(n: Optional[int]) -> None:
 
 
 def slice_cus() -> int:
-    return getattr(_slice, "cus", None) or 256
+    return getattr(_slice, "cus", None) or total_cus()
+
+
+def total_cus() -> int:
+    """CUs of the whole device (256 on MI355X; the device query when a GPU is visible)."""
+    global _total_cus
+    if _total_cus is None:
+        try:
+            import torch
+            _total_cus = int(torch.cuda.get_device_properties(0).multi_processor_count) \
+                if torch.cuda.is_available() else 256
+        except Exception:  # noqa: BLE001 - CPU-only hosts, early import
+            _total_cus = 256
+    return _total_cus
+
+
+_total_cus: Optional[int] = None
 
 
 _waves_per_cu: Optional[int] = None
