@@ -569,16 +569,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
 // 8 KB image is read with fully coalesced 1 KB wave loads, scaled by exp2(m_w[q] - m_max[q]) and
 // accumulated in registers; the normalised tile is transposed through LDS so the [q][d] output rows
 // are written as 256-B runs.
+template <int G>
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
                                                          int B, int T, int H, int P, __bf16* __restrict__ outp) {
   __shared__ float s_tile[64][33];
-  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
-  const int wv = blockIdx.x & 3;
-  const long long grp = blockIdx.x >> 2;
+  const int wv = blockIdx.x % G;
+  const long long grp = blockIdx.x / G;
   const int qg = int(grp % QG);
-  const int qt = qg * 4 + wv;
+  const int qt = qg * G + wv;
   if (qt >= QT) return;
   const long long t0 = grp * NK, t1 = t0 + NK;
   const long long w_lo = ((t0 + 1) * P + U - 1) / U - 1;
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   auto slot_of = [&](long long w) -> long long {
     const long long s = w * U / P;
     if (s == (w + 1) * U / P) return -1;  // empty range
-    return (w * 2 + (s >= t0 ? 0 : 1)) * 4 + wv;
+    return (w * 2 + (s >= t0 ? 0 : 1)) * G + wv;
   };
   // one online-softmax merge pass over the contributors, their loads issued up to four at a time
   // (every thread merges its own query's m/l redundantly: no serial phase, no extra barrier)
@@ -907,21 +908,28 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
 // stream, so the ~190 vector instructions per block issue in the matrix pipe's shadow instead of
 // between its bursts. K and V have their own double-buffered rings (iteration i reads K of block
 // i+1 and V of block i), one barrier per iteration. Same units, partials and fixup as attn_fwd_x3.
-__global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
-                                                       float* __restrict__ out, __bf16* __restrict__ outp,
-                                                       float* __restrict__ part_o, float* __restrict__ part_ml, int B,
-                                                       int T, int H, float scale_log2e, int P) {
+// G = query tiles (waves) per workgroup sharing each K/V block: 4 (two workgroups per CU) or 8 (one
+// 512-thread workgroup per CU: half the K/V bytes per query, the L2/Infinity-Cache traffic that
+// concurrent partitions share; the K and V loads are split between the two halves of the group).
+template <int G>
+__global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
+                                                             float* __restrict__ out, __bf16* __restrict__ outp,
+                                                             float* __restrict__ part_o, float* __restrict__ part_ml,
+                                                             int B, int T, int H, float scale_log2e, int P) {
+  static_assert(G == 4 || G == 8, "4 or 8 query tiles per workgroup");
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
   const int w = sk_logical(blockIdx.x, P);
-  const int NK = (T + 31) / 32, QT = NK, QG = (QT + 3) / 4;
+  const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
   long long u = sk_begin(w, U, P);
   const long long u1 = sk_begin(w + 1, U, P);
   const int D = H * HD, ld = 3 * D;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int j = lane & 31, hf = lane >> 5;
-  const int lrow = tid >> 3, lch = tid & 7;
+  const int lrow = (tid & 255) >> 3, lch = tid & 7;
+  const bool kload = G == 4 || tid < 256;  // G = 8: waves 0-3 stage K, waves 4-7 stage V
+  const bool vload = G == 4 || tid >= 256;
   const int gi = lane & 15, gg = lane >> 4;
   const int vtr = (4 * hf + (gi >> 2)) * XV_STR + 16 * (gg & 1) + 4 * (gi & 3);
   bool first = true;
@@ -934,7 +942,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
     const int head = int((grp / QG) % H);
     const int b = int(grp / ((long long)QG * H));
     const __bf16* base = qkv3 + size_t(b) * T * ld;
-    const int qt = qg * 4 + wv;
+    const int qt = qg * G + wv;
     const bool active = qt < QT;
     const int q0 = qt * 32;
 
@@ -986,13 +994,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
     }                                                                                            \
   }
     __syncthreads();  // the previous segment's last blocks are no longer being read
-    fetch_k(kb0);
-    fetch_v(kb0);
-    stash_k(0);
-    stash_v(0);
-    if (nb > 1) {
-      fetch_k(kb0 + 1);
-      stash_k(1);
+    if (kload) {
+      fetch_k(kb0);
+      stash_k(0);
+      if (nb > 1) {
+        fetch_k(kb0 + 1);
+        stash_k(1);
+      }
+    }
+    if (vload) {
+      fetch_v(kb0);
+      stash_v(0);
     }
     __syncthreads();
 
@@ -1006,8 +1018,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
   {                                                                                                       \
       const int blk = kb0 + i;                                                                            \
       const bool more_k = i + 2 < nb, more_v = i + 1 < nb;                                                \
-      if (more_k) fetch_k(blk + 2);                                                                       \
-      if (more_v) fetch_v(blk + 1);                                                                       \
+      if (kload && more_k) fetch_k(blk + 2);                                                                      \
+      if (vload && more_v) fetch_v(blk + 1);                                                                      \
       if (active) {                                                                                       \
         if (blk * 32 + 32 > T) {                                                                          \
           asm volatile("; tail block: mask keys >= T" ::: "memory");                                      \
@@ -1053,8 +1065,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
           }                                                                                               \
         }                                                                                                 \
       }                                                                                                   \
-      if (more_k) stash_k(i & 1);                                                                         \
-      if (more_v) stash_v((i + 1) & 1);                                                                   \
+      if (kload && more_k) stash_k(i & 1);                                                                 \
+      if (vload && more_v) stash_v((i + 1) & 1);                                                           \
       __syncthreads();                                                                                    \
   }
     f32x16 snext;
@@ -1091,7 +1103,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3p(const __bf16* __restrict_
           }
         }
       } else {
-        const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * 4 + wv;
+        const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * G + wv;
         float* po = part_o + slot * (HD * 32);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1130,6 +1142,19 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
 }
 
 static int g_x3_pipelined = 1;
+static int g_x3_group = 8;  // query tiles per workgroup of the pipelined x3 kernel (4 or 8; 8 measured faster)
+
+// 4 = two 256-thread workgroups per CU, 8 = one 512-thread workgroup sharing K/V (default)
+int nos_attention_x3_set_group(int g) {
+  if (g != 4 && g != 8) {
+    g_err = "attention x3: group must be 4 or 8";
+    return -1;
+  }
+  g_x3_group = g;
+  return 0;
+}
+
+int nos_attention_x3_group() { return g_x3_pipelined ? g_x3_group : 4; }
 
 // 1 = software-pipelined x3 kernel (default), 0 = the block-at-a-time x3 kernel (A/B reference)
 int nos_attention_x3_set_pipelined(int on) {
@@ -1140,8 +1165,10 @@ int nos_attention_x3_set_pipelined(int on) {
 // workgroups per CU of the x3 attention kernel (persistent grid = this x slice CUs)
 int nos_attention_x3_wg_per_cu() {
   int n = 0;
-  const hipError_t e = g_x3_pipelined ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3p, 256, 0)
-                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3, 256, 0);
+  const hipError_t e =
+      !g_x3_pipelined  ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3, 256, 0)
+      : g_x3_group == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3p<8>, 512, 0)
+                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, attn_fwd_x3p<4>, 256, 0);
   if (e != hipSuccess || n <= 0) n = 1;
   return n;
 }
@@ -1169,19 +1196,29 @@ int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void*
     return -1;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int NK = (T + 31) / 32, QG = (NK + 3) / 4;
+  const int G = nos_attention_x3_group();
+  const int NK = (T + 31) / 32, QG = (NK + G - 1) / G;
   float* part_o = ws;
-  float* part_ml = ws + size_t(waves) * 8 * HD * 32;
+  float* part_ml = ws + size_t(waves) * 2 * G * HD * 32;
   __bf16* op = reinterpret_cast<__bf16*>(outp);
-  if (g_x3_pipelined)
-    hipLaunchKernelGGL(attn_fwd_x3p, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3),
-                       plane_stride, out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+  const float sl2 = scale * 1.4426950408889634f;
+  const __bf16* q3 = reinterpret_cast<const __bf16*>(qkv3);
+  if (!g_x3_pipelined)
+    hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
+                       sl2, waves);
+  else if (G == 8)
+    hipLaunchKernelGGL(attn_fwd_x3p<8>, dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
+                       T, H, sl2, waves);
   else
-    hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, reinterpret_cast<const __bf16*>(qkv3),
-                       plane_stride, out, op, part_o, part_ml, B, T, H, scale * 1.4426950408889634f, waves);
+    hipLaunchKernelGGL(attn_fwd_x3p<4>, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
+                       T, H, sl2, waves);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
-  hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
-                     op);
+  if (G == 8)
+    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(B * H * QG * 8), dim3(256), 0, s, part_o, part_ml, out, B, T, H,
+                       waves, op);
+  else
+    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H,
+                       waves, op);
   return check_launch("attn_sk_lds_fixup");
 }
 
@@ -1272,7 +1309,7 @@ int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, 
     hipLaunchKernelGGL(attn_fwd_sk_lds, dim3(waves), dim3(256), 0, s, qkv, out, part_o, part_ml, B, T, H,
                        scale_log2e, waves);
     if (int rc = check_launch("attn_fwd_sk_lds")) return rc;
-    hipLaunchKernelGGL(attn_sk_lds_fixup, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
+    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
                        static_cast<__bf16*>(nullptr));
     return check_launch("attn_sk_lds_fixup");
   }

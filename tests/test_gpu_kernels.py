@@ -231,16 +231,18 @@ def test_attention_x3_fp32_accurate_any_grid(K, T, H, B):
     torch.cuda.synchronize()
     err_f32 = (f32 - ref).abs().max().item()
     try:
-        for pipelined in (True, False):
+        for pipelined, group in ((True, 4), (True, 8), (False, 4)):
             K.set_attention_x3_pipelined(pipelined)
+            K.set_attention_x3_group(group)
             for waves in (1, 3, 7, 64, 333, 512, units + 5):
                 out = torch.full((B, T, H * 64), float("nan"), device="cuda")
                 K.attention_x3(planes, out, H, 64, 0.125, waves)
                 torch.cuda.synchronize()
                 err = (out - ref).abs().max().item()
-                assert err < max(2.0 * err_f32, 2e-6), (pipelined, waves, err, err_f32)
+                assert err < max(2.0 * err_f32, 2e-6), (pipelined, group, waves, err, err_f32)
     finally:
         K.set_attention_x3_pipelined(True)
+        K.set_attention_x3_group(8)
 
 
 def test_attention_x3_asymmetric_values(K):

@@ -117,6 +117,11 @@ def attn_bench(r, qkv, out, q, k, v, n, s, iters, attn_flops, variants=(0, 2, 3)
     r["attn_x3_grid"] = wx
     for mult in (1, 2):
         r[f"attn_x3g{mult}_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, mult * n), s, iters)
+    K.set_attention_x3_group(4)  # the default is 8 query tiles per workgroup: time 4 as the A/B
+    w4 = K.attention_x3_waves(n, 1, T, H)
+    r["attn_x3q4_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, w4), s, iters)
+    r["attn_x3q4_grid"] = w4
+    K.set_attention_x3_group(8)
     K.set_attention_x3_pipelined(False)
     wnp = K.attention_x3_waves(n, 1, T, H)
     r["attn_x3np_us"] = timeit(lambda: K.attention_x3(planes, out, H, HD, 0.125, wnp), s, iters)

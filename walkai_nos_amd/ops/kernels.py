@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import threading
 from typing import Optional
 
@@ -137,6 +138,18 @@ def set_attention_x3_pipelined(on: bool) -> None:
     _x3_wg = None
 
 
+def set_attention_x3_group(g: int) -> None:
+    """Query tiles per workgroup of the pipelined x3 kernel: 4 (two 256-thread workgroups per CU)
+    or 8 (one 512-thread workgroup per CU sharing every K/V block: half the K/V traffic)."""
+    global _x3_wg
+    _check(_L().nos_attention_x3_set_group(int(g)))
+    _x3_wg = None
+
+
+def attention_x3_group() -> int:
+    return int(_L().nos_attention_x3_group())
+
+
 def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
     """Persistent grid of the x3 attention kernel (same sizing rule as the f32 LDS kernel)."""
     global _x3_wg
@@ -145,7 +158,8 @@ def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
     per_cu = _x3_wg
     if T:
         nk = (T + 31) // 32
-        units = B * H * ((nk + 3) // 4) * nk
+        g = attention_x3_group()
+        units = B * H * ((nk + g - 1) // g) * nk
         while per_cu > 1 and units / (per_cu * cus) < 30:
             per_cu -= 1
     return per_cu * cus
@@ -156,7 +170,7 @@ def attention_x3(planes: torch.Tensor, out: torch.Tensor, heads: int, head_dim: 
     """Stream-K attention over the x3 planes ``[3, B, T, 3*H*64]`` of a packed QKV tensor. ``out`` is
     fp32 ``[B, T, H*64]`` or bf16 ``[3, B, T, H*64]`` (the output leaves as x3 planes)."""
     _, B, T, _ = planes.shape
-    ws = torch.empty(waves * 2 * (64 * 32 + 64) * 4, dtype=torch.float32, device=planes.device)
+    ws = torch.empty(waves * 2 * (64 * 32 + 64) * attention_x3_group(), dtype=torch.float32, device=planes.device)
     x3_out = out.dtype == torch.bfloat16
     _check(_L().nos_attention_x3_sk(planes.data_ptr(), planes[0].numel(), None if x3_out else out.data_ptr(),
                                     out.data_ptr() if x3_out else None, ws.data_ptr(), B, T, heads, head_dim, scale,
@@ -204,7 +218,11 @@ def _L() -> ctypes.CDLL:
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
+            L.nos_attention_x3_set_group.argtypes = [i32]
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            group = os.environ.get("NOS_ATTN_X3_GROUP")  # A/B switch for whole-model runs
+            if group and L.nos_attention_x3_set_group(int(group)) != 0:
+                raise RuntimeError(f"NOS_ATTN_X3_GROUP={group}: {L.nos_kernels_last_error().decode()}")
             _lib = L
         return _lib
 
