@@ -1014,6 +1014,29 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     __syncthreads();  // iteration 0 refills K buffer 0, which the line above reads
 // One key block: softmax + P.V of block i from SC while block i+1's scores go to SN; the loop
 // alternates the two registers sets (no copy of the 16 scores per block).
+// P.V of one key block from the P planes pa*/pb* (keys 0-15 / 16-31) and V buffer VB
+#define X3P_PV(VB)                                                                                        \
+  {                                                                                                       \
+    const __bf16* vs_ = &lds_v[(VB) * 3 * XV_PLANE + vtr];                                                \
+    _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                                                    \
+      _Pragma("unroll") for (int dh = 0; dh < 2; ++dh) {                                                  \
+        bf16x8 vf[3];                                                                                     \
+        _Pragma("unroll") for (int p = 0; p < 3; ++p) {                                                   \
+          const __bf16* a = vs_ + p * XV_PLANE + 16 * s2 * XV_STR + 32 * dh;                              \
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a));                   \
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a + 8 * XV_STR));      \
+          vf[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};                         \
+        }                                                                                                 \
+        const bf16x8 q0_ = s2 ? pb0 : pa0;                                                                \
+        const bf16x8 q1_ = s2 ? pb1 : pa1;                                                                \
+        const bf16x8 q2_ = s2 ? pb2 : pa2;                                                                \
+        if (dh == 0)                                                                                      \
+          o0 = mfma_x3(vf[0], vf[1], vf[2], q0_, q1_, q2_, o0);                                           \
+        else                                                                                              \
+          o1 = mfma_x3(vf[0], vf[1], vf[2], q0_, q1_, q2_, o1);                                           \
+      }                                                                                                   \
+    }                                                                                                     \
+  }
 #define X3P_ITER(SC, SN)                                                                                  \
   {                                                                                                       \
       const int blk = kb0 + i;                                                                            \
@@ -1069,14 +1092,71 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
       if (vload && more_v) stash_v((i + 1) & 1);                                                           \
       __syncthreads();                                                                                    \
   }
+#define X3P_ITER_LATE(SC, SN)                                                                                  \
+  {                                                                                                       \
+      const int blk = kb0 + i;                                                                            \
+      const bool more_k = i + 2 < nb, more_v = i + 1 < nb;                                                \
+      if (kload && more_k) fetch_k(blk + 2);                                                                      \
+      if (vload && more_v) fetch_v(blk + 1);                                                                      \
+      if (active) {                                                                                       \
+        if (i > 0) X3P_PV((i - 1) & 1) /* the previous block's P.V, half a block behind waves 0-3 */   \
+        if (blk * 32 + 32 > T) {                                                                          \
+          asm volatile("; tail block: mask keys >= T" ::: "memory");                                      \
+          _Pragma("unroll") for (int r = 0; r < 16; ++r)                                                  \
+            if (blk * 32 + key_of(r, hf) >= T) SC[r] = -INFINITY;                                         \
+        }                                                                                                 \
+        float mx = fmaxf(SC[0], SC[1]);                                                                   \
+        _Pragma("unroll") for (int r = 2; r < 16; ++r) mx = fmaxf(mx, SC[r]);                             \
+        mx = half_max(mx);                                                                                \
+        if (__builtin_amdgcn_ballot_w64((mx - m) * scale_log2e > 8.f)) {                                  \
+          const float m_new = fmaxf(m, mx);                                                               \
+          const float alpha = __builtin_amdgcn_exp2f((m - m_new) * scale_log2e);                          \
+          l *= alpha;                                                                                     \
+          o0 *= alpha;                                                                                    \
+          o1 *= alpha;                                                                                    \
+          m = m_new;                                                                                      \
+        }                                                                                                 \
+                /* block i+1's scores (the last block: a throwaway product keeps one basic block) */ X3P_QK(SN, (i + 1) & 1)                                                                   \
+        const float mc = m * scale_log2e;                                                                 \
+        float psum = 0.f;                                                                                 \
+        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                                  \
+          SC[r] = __builtin_amdgcn_exp2f(fmaf(SC[r], scale_log2e, -mc));                                  \
+          psum += SC[r];                                                                                  \
+        }                                                                                                 \
+        psum = half_sum(psum);                                                                            \
+        l += psum;                                                                                        \
+        split3_trunc8(SC, 0, pa0, pa1, pa2);                                                              \
+        split3_trunc8(SC, 8, pb0, pb1, pb2);                                                              \
+      }                                                                                                   \
+      if (kload && more_k) stash_k(i & 1);                                                                 \
+      if (vload && more_v) stash_v((i + 1) & 1);                                                           \
+      __syncthreads();                                                                                    \
+  }
     f32x16 snext;
-    for (int i = 0; i < nb;) {
-      X3P_ITER(scur, snext)
-      if (++i >= nb) break;
-      X3P_ITER(snext, scur)
-      ++i;
+    // G = 8: waves 4-7 run each block's P.V half a block late (after the barrier, beside waves
+    // 0-3's score MFMAs and softmax), so the two waves sharing a SIMD stop reaching their MFMA and
+    // VALU phases together; their P planes wait in registers and the V block stays in its buffer
+    // (its next refill is staged by these same waves, after the deferred P.V)
+    bf16x8 pa0, pa1, pa2, pb0, pb1, pb2;
+    if (G == 8 && wv >= 4) {
+      for (int i = 0; i < nb;) {
+        X3P_ITER_LATE(scur, snext)
+        if (++i >= nb) break;
+        X3P_ITER_LATE(snext, scur)
+        ++i;
+      }
+      if (active && nb > 0) X3P_PV((nb - 1) & 1)
+    } else {
+      for (int i = 0; i < nb;) {
+        X3P_ITER(scur, snext)
+        if (++i >= nb) break;
+        X3P_ITER(snext, scur)
+        ++i;
+      }
     }
 #undef X3P_ITER
+#undef X3P_ITER_LATE
+#undef X3P_PV
 #undef X3P_QK
 
     if (active) {
