@@ -136,3 +136,59 @@ def test_slice_probe_targets_cover_each_live_slice_cu_set():
     assert set(t) == {"g::s0", "g::s1", "h::s0"}
     assert len(t["g::s0"][1]) == 32 and len(t["g::s1"][1]) == 64 and t["g::s1"][0] == 0
     assert t["h::s0"][0] == 1 and len(t["h::s0"][1]) == 256  # memory-only slice runs on the shared pool
+
+
+# -- slice-agent reporter (reference internal/controllers/gpuagent/reporter_int_test.go:61-177) --
+class _SliceDevices:
+    """Slicing client stub: the reporter only calls ``get_partition_devices``."""
+
+    def __init__(self, devs):
+        self.devs = devs
+
+    def get_partition_devices(self):
+        from walkai_nos_amd.models.device import devices
+        return devices(self.devs)
+
+
+def _slice_reporter(devs):
+    from walkai_nos_amd.api import v1alpha1 as api
+    from walkai_nos_amd.controllers.agent.reporter import Reporter
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    from walkai_nos_amd.kube.memory import InMemoryAPIServer
+    srv = InMemoryAPIServer()
+    srv.create(ko.new_node("node-s", {api.LABEL_GPU_PARTITIONING: "cumask"}))
+    rep = Reporter(srv, _SliceDevices(devs), SharedState(), refresh_interval=5,
+                   profile_extractor=extract_profile_name)
+    return srv, rep
+
+
+def _status(srv):
+    from walkai_nos_amd.api import v1alpha1 as api
+    return {k: v for k, v in ko.annotations(srv.get("Node", "node-s")).items()
+            if k.startswith(api.ANNOTATION_GPU_STATUS_PREFIX)}
+
+
+def test_slice_reporter_without_gpus_writes_no_status_annotations():
+    from walkai_nos_amd.kube.runtime import Request
+    srv, rep = _slice_reporter([])
+    assert rep.reconcile(Request("node-s")).requeue_after == 5
+    assert _status(srv) == {}
+
+
+def test_slice_reporter_groups_slices_and_excludes_whole_gpu_resource():
+    from walkai_nos_amd.kube.runtime import Request
+    from walkai_nos_amd.models.device import GpuDevice
+    devs = [GpuDevice("amd.com/gpu-32cu.36gb", "g0/s0", "used", 0),
+            GpuDevice("amd.com/gpu-32cu.36gb", "g0/s1", "used", 0),
+            GpuDevice("amd.com/gpu-64cu.72gb", "g0/s2", "free", 0),
+            GpuDevice("amd.com/gpu-128cu.144gb", "g1/s0", "free", 1),
+            GpuDevice("amd.com/gpu", "g2", "used", 2)]  # plain whole-GPU resource: never reported
+    srv, rep = _slice_reporter(devs)
+    rep.reconcile(Request("node-s"))
+    assert _status(srv) == {"nos.nebuly.com/status-gpu-0-32cu.36gb-used": "2",
+                            "nos.nebuly.com/status-gpu-0-64cu.72gb-free": "1",
+                            "nos.nebuly.com/status-gpu-1-128cu.144gb-free": "1"}
+    # unchanged devices: the next report does not patch the node again
+    rv = srv.get("Node", "node-s")["metadata"]["resourceVersion"]
+    rep.reconcile(Request("node-s"))
+    assert srv.get("Node", "node-s")["metadata"]["resourceVersion"] == rv
