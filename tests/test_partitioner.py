@@ -180,3 +180,27 @@ def test_simulate_policy_end_to_end_on_the_in_memory_cluster():
     # partitions are homogeneous per GPU: 10 x 1/8 + 1 x 1/2 cannot all fit on 2 GPUs; the
     # simulation keeps the layout that runs the most pods (both GPUs CPX)
     assert len(c.running_pods()) == 10 and [ko.name(p) for p in c.pending_pods()] == ["d0"]
+
+
+def test_read_only_plan_pass_is_reused_until_the_api_changes():
+    """A requeued plan key on an unchanged cluster reuses the last read-only answer; any write
+    (here: the blocking pods finish) makes the next pass plan again."""
+    import walkai_nos_amd.controllers.partitioner.pod_controller as pcm
+    api_ = InMemoryAPIServer()
+    api_.create(xnode(gpus=1))
+    _settled(api_, {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8"})
+    pc = PodController(api_, retry_after=7)
+    api_.create(unschedulable_pod("p", {"amd.com/spx_nps1": 1}))
+    calls = []
+    orig = pcm.plan_cluster_fifo
+    pcm.plan_cluster_fifo = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    try:
+        assert pc.reconcile(pc.plan_key).requeue_after == 7
+        assert pc.reconcile(pc.plan_key).requeue_after == 7
+        assert len(calls) == 1 and pc.plans_written == 0
+        _settled(api_, {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "0",
+                        "nos.nebuly.com/status-gpu-0-cpx_nps1-free": "8"})
+        pc.reconcile(pc.plan_key)
+        assert len(calls) == 2 and pc.plans_written == 1
+    finally:
+        pcm.plan_cluster_fifo = orig

@@ -90,6 +90,9 @@ class InMemoryAPIServer:
         self.clock = clock
         # request counters, useful for tests / benchmarks
         self.stats: Dict[str, int] = {"create": 0, "update": 0, "patch": 0, "delete": 0, "get": 0, "list": 0}
+        # bumped by every write (create / update / patch / delete / bind): equal revisions mean no
+        # object changed in between, so read-only reconciles may reuse their last answer
+        self.revision = 0
 
     # ---- watch ------------------------------------------------------------------------
     def watch(self, kind: str, handler: Handler, replay: bool = True) -> Callable[[], None]:
@@ -111,6 +114,7 @@ class InMemoryAPIServer:
         """Deliver one event to every watcher. The handlers of one event share a single copy of
         the objects (watch handlers only map events to requests; they must not mutate them)."""
         with self._lock:
+            self.revision += 1
             handlers = list(self._handlers.get(kind, []))
         if not handlers:
             return
