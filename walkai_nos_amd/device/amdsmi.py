@@ -91,9 +91,17 @@ class AmdSmi:
     def gpu_index_of(self, device_id: str) -> int:
         """Map a device id (GPU UUID, BDF or ``<bdf>/xcp<k>``) to the physical GPU index."""
         base = device_id.split("/xcp", 1)[0].split("::", 1)[0]
-        for g in self.list_gpus():
-            if base in (g.uuid, g.bdf, str(g.index)):
-                return g.index
+        # the GPU set of a node is fixed for the process: index the ids once (re-scanned on a miss),
+        # the device plugin and the reporters resolve every allocated device on each pass
+        ids = getattr(self, "_gpu_ids", None)
+        if ids is None or base not in ids:
+            ids = {}
+            for g in self.list_gpus():
+                for k in (g.uuid, g.bdf, str(g.index)):
+                    ids.setdefault(k, g.index)
+            self._gpu_ids = ids
+        if base in ids:
+            return ids[base]
         raise GpuError(f"device {device_id!r} not found", GpuError.NOT_FOUND)
 
     def close(self) -> None:
