@@ -5,8 +5,15 @@
 // SPX/DPX/QPX/CPX) plus an optional node-wide memory-partition (NPS) change, so the reference's
 // GPU-instance/compute-instance bookkeeping and its n! creation-order search disappear.
 //
-// One amd-smi session is kept for the life of the process (the reference re-initialises NVML on
-// every call). Return codes: 0 ok, 1 generic, 2 permission, 3 not found, 4 busy.
+// What does NOT disappear is re-enumeration: after SPX -> CPX amd-smi reports one processor per
+// partition (8 per GPU), each with its own UUID, KFD node, render node and HIP ordinal, and the
+// handles taken before the switch are stale. So this backend exposes *processors* (not GPUs), and
+// nos_smi_enumerate(reinit=1) shuts the session down and re-initialises it before listing them
+// again. Grouping processors into physical GPUs (by BDF) is done by the caller
+// (walkai_nos_amd/device/topology.py). The reference reaches the same freshness by running
+// nvml.Init/Shutdown around every call (client.go:46-57).
+//
+// Return codes: 0 ok, 1 generic, 2 permission, 3 not found, 4 busy. No HIP is linked or loaded.
 #include <amd_smi/amdsmi.h>
 
 #include <cstdint>
@@ -20,7 +27,7 @@ namespace {
 
 std::mutex g_mu;
 bool g_init = false;
-std::vector<amdsmi_processor_handle> g_gpus;
+std::vector<amdsmi_processor_handle> g_procs;
 thread_local std::string g_err;
 
 int map_status(amdsmi_status_t st, const char* what) {
@@ -38,21 +45,60 @@ int map_status(amdsmi_status_t st, const char* what) {
 
 int handle(uint32_t idx, amdsmi_processor_handle* h) {
   if (!g_init) { g_err = "amdsmi not initialised"; return 1; }
-  if (idx >= g_gpus.size()) { g_err = "GPU index out of range"; return 3; }
-  *h = g_gpus[idx];
+  if (idx >= g_procs.size()) { g_err = "processor index out of range (re-enumerate after a partition change)"; return 3; }
+  *h = g_procs[idx];
   return 0;
+}
+
+// caller holds g_mu
+int list_processors() {
+  g_procs.clear();
+  uint32_t nsock = 0;
+  amdsmi_status_t st = amdsmi_get_socket_handles(&nsock, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  st = amdsmi_get_socket_handles(&nsock, socks.data());
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t n = 0;
+    if (amdsmi_get_processor_handles(socks[s], &n, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> hs(n);
+    if (amdsmi_get_processor_handles(socks[s], &n, hs.data()) != AMDSMI_STATUS_SUCCESS) continue;
+    for (uint32_t i = 0; i < n; ++i) {
+      processor_type_t t;
+      if (amdsmi_get_processor_type(hs[i], &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        g_procs.push_back(hs[i]);
+    }
+  }
+  return 0;
+}
+
+// caller holds g_mu
+int open_session() {
+  amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_init");
+  g_init = true;
+  return list_processors();
 }
 
 }  // namespace
 
 extern "C" {
 
-struct nos_gpu_info {
-  uint32_t index;
+struct nos_proc_info {
+  uint32_t ordinal;
   char uuid[64];
-  char bdf[32];
+  char bdf[32];          // physical GPU, "dddd:bb:dd.f"
   char market_name[64];
+  char hip_uuid[64];
+  uint64_t bdf_id;       // KFD location id incl. partition bits [31:28]
+  uint64_t kfd_id;
   uint64_t vram_bytes;
+  uint32_t partition_id; // 0xFFFFFFFF if the driver does not report one
+  int32_t kfd_node;
+  int32_t hip_id;
+  int32_t hsa_id;
+  int32_t render_minor;
   uint32_t cu_count;
   uint32_t xcds;
 };
@@ -62,50 +108,39 @@ const char* nos_smi_last_error() { return g_err.c_str(); }
 int nos_smi_init() {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_init) return 0;
-  amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
-  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_init");
-  uint32_t nsock = 0;
-  st = amdsmi_get_socket_handles(&nsock, nullptr);
-  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
-  std::vector<amdsmi_socket_handle> socks(nsock);
-  st = amdsmi_get_socket_handles(&nsock, socks.data());
-  if (st != AMDSMI_STATUS_SUCCESS) return map_status(st, "amdsmi_get_socket_handles");
-  g_gpus.clear();
-  for (uint32_t s = 0; s < nsock; ++s) {
-    uint32_t n = 0;
-    st = amdsmi_get_processor_handles(socks[s], &n, nullptr);
-    if (st != AMDSMI_STATUS_SUCCESS) continue;
-    std::vector<amdsmi_processor_handle> hs(n);
-    if (amdsmi_get_processor_handles(socks[s], &n, hs.data()) != AMDSMI_STATUS_SUCCESS) continue;
-    for (uint32_t i = 0; i < n; ++i) {
-      processor_type_t t;
-      if (amdsmi_get_processor_type(hs[i], &t) == AMDSMI_STATUS_SUCCESS && t == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
-        g_gpus.push_back(hs[i]);
-    }
-  }
-  g_init = true;
-  return 0;
+  return open_session();
 }
 
 int nos_smi_shutdown() {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!g_init) return 0;
-  g_gpus.clear();
+  g_procs.clear();
   g_init = false;
   return map_status(amdsmi_shut_down(), "amdsmi_shut_down");
 }
 
-int nos_smi_gpu_count() {
+// Re-list processors; with reinit the session is closed and reopened first, which is required
+// after a compute/memory partition change. Returns the processor count, or -1.
+int nos_smi_enumerate(int reinit) {
   std::lock_guard<std::mutex> lk(g_mu);
-  return g_init ? int(g_gpus.size()) : -1;
+  int rc = 0;
+  if (g_init && reinit) {
+    g_procs.clear();
+    g_init = false;
+    amdsmi_shut_down();
+  }
+  rc = g_init ? list_processors() : open_session();
+  return rc ? -1 : int(g_procs.size());
 }
 
-int nos_smi_gpu_info(uint32_t idx, nos_gpu_info* out) {
+int nos_smi_proc_info(uint32_t idx, nos_proc_info* out) {
   std::lock_guard<std::mutex> lk(g_mu);
   amdsmi_processor_handle h;
   if (int rc = handle(idx, &h)) return rc;
   std::memset(out, 0, sizeof(*out));
-  out->index = idx;
+  out->ordinal = idx;
+  out->partition_id = 0xFFFFFFFFu;
+  out->kfd_node = out->hip_id = out->hsa_id = out->render_minor = -1;
   unsigned int ulen = sizeof(out->uuid);
   amdsmi_get_gpu_device_uuid(h, &ulen, out->uuid);
   amdsmi_bdf_t bdf;
@@ -114,6 +149,21 @@ int nos_smi_gpu_info(uint32_t idx, nos_gpu_info* out) {
                   (unsigned long long)bdf.domain_number, (unsigned long long)bdf.bus_number,
                   (unsigned long long)bdf.device_number, (unsigned long long)bdf.function_number);
   }
+  uint64_t bdfid = 0;
+  if (amdsmi_get_gpu_bdf_id(h, &bdfid) == AMDSMI_STATUS_SUCCESS) out->bdf_id = bdfid;
+  amdsmi_kfd_info_t kfd;
+  if (amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS) {
+    out->kfd_id = kfd.kfd_id;
+    if (kfd.node_id != 0xFFFFFFFFu) out->kfd_node = int32_t(kfd.node_id);
+    out->partition_id = kfd.current_partition_id;
+  }
+  amdsmi_enumeration_info_t en;
+  if (amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {
+    out->hip_id = int32_t(en.hip_id);
+    out->hsa_id = int32_t(en.hsa_id);
+    out->render_minor = int32_t(en.drm_render);
+    std::snprintf(out->hip_uuid, sizeof(out->hip_uuid), "%.63s", en.hip_uuid);
+  }
   amdsmi_asic_info_t asic;
   if (amdsmi_get_gpu_asic_info(h, &asic) == AMDSMI_STATUS_SUCCESS) {
     std::snprintf(out->market_name, sizeof(out->market_name), "%.63s", asic.market_name);
@@ -121,7 +171,8 @@ int nos_smi_gpu_info(uint32_t idx, nos_gpu_info* out) {
   }
   uint64_t total = 0;
   if (amdsmi_get_gpu_memory_total(h, AMDSMI_MEM_TYPE_VRAM, &total) == AMDSMI_STATUS_SUCCESS) out->vram_bytes = total;
-  out->xcds = 8;
+  uint16_t xcd = 0;
+  if (amdsmi_get_gpu_xcd_counter(h, &xcd) == AMDSMI_STATUS_SUCCESS && xcd > 0) out->xcds = xcd;
   return 0;
 }
 
@@ -168,6 +219,7 @@ int nos_smi_set_memory_partition(uint32_t idx, const char* mode) {
   return map_status(amdsmi_set_gpu_memory_partition(h, t), "amdsmi_set_gpu_memory_partition");
 }
 
+// Processes with a KFD context on this processor (a compute-partition switch destroys them all).
 int nos_smi_process_count(uint32_t idx) {
   std::lock_guard<std::mutex> lk(g_mu);
   amdsmi_processor_handle h;

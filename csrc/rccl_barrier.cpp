@@ -6,8 +6,10 @@
 // spanning the node's devices is that barrier: each rank contributes 1 if its local apply+verify
 // succeeded, so the sum equals nranks iff the whole node committed.
 //
-// The communicator is created per commit and destroyed before the next mode flip, because a flip
-// re-enumerates devices and invalidates every handle. A 4-byte all-reduce is latency bound (tens of
+// The communicator is created per commit, in a short-lived helper process the partition agent
+// spawns (walkai_nos_amd/cmd/gpuhelper.py), and destroyed with it before the next mode flip: a flip
+// re-enumerates devices and invalidates every handle, and a process holding a KFD context on the
+// GPU is exactly what makes the flip fail with "busy". A 4-byte all-reduce is latency bound (tens of
 // microseconds), so link bandwidth (7 x ~153 GB/s xGMI per GPU) is irrelevant here.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
@@ -57,17 +59,27 @@ int nos_barrier_unique_id(char* out, int len) {
   return 0;
 }
 
+static void release(Barrier* b) {
+  if (b == nullptr) return;
+  (void)hipSetDevice(b->device);
+  if (b->dbuf) (void)hipFree(b->dbuf);
+  if (b->stream) (void)hipStreamDestroy(b->stream);
+  delete b;
+}
+
 int nos_barrier_init(int nranks, int rank, const char* id_bytes, int device, void** handle) {
   auto* b = new Barrier();
   b->device = device;
-  if (int rc = hip_check(hipSetDevice(device), "hipSetDevice")) { delete b; return rc; }
-  if (int rc = hip_check(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), "hipStreamCreate")) { delete b; return rc; }
-  if (int rc = hip_check(hipMalloc(&b->dbuf, sizeof(int32_t)), "hipMalloc")) { delete b; return rc; }
-  ncclUniqueId id;
-  std::memcpy(&id, id_bytes, sizeof(id));
-  if (int rc = nccl_check(ncclCommInitRank(&b->comm, nranks, id, rank), "ncclCommInitRank")) {
-    (void)hipFree(b->dbuf);
-    delete b;
+  int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+  if (!rc) rc = hip_check(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking), "hipStreamCreate");
+  if (!rc) rc = hip_check(hipMalloc(&b->dbuf, sizeof(int32_t)), "hipMalloc");
+  if (!rc) {
+    ncclUniqueId id;
+    std::memcpy(&id, id_bytes, sizeof(id));
+    rc = nccl_check(ncclCommInitRank(&b->comm, nranks, id, rank), "ncclCommInitRank");
+  }
+  if (rc) {
+    release(b);  // every partially created resource, not just the struct
     return rc;
   }
   *handle = b;
@@ -88,10 +100,18 @@ int nos_barrier_destroy(void* handle) {
   auto* b = static_cast<Barrier*>(handle);
   int rc = 0;
   if (b->comm) rc = nccl_check(ncclCommDestroy(b->comm), "ncclCommDestroy");
-  if (b->dbuf) (void)hipFree(b->dbuf);
-  if (b->stream) (void)hipStreamDestroy(b->stream);
-  delete b;
+  b->comm = nullptr;
+  release(b);
   return rc;
+}
+
+// Number of HIP devices this process sees (after a compute-partition flip: the partitions). The
+// node barrier runs in a freshly spawned helper so that this count, and the HIP context it
+// creates, never live in the partition agent itself.
+int nos_barrier_device_count() {
+  int n = 0;
+  if (hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount")) return -1;
+  return n;
 }
 
 // ---- single-process node barrier: one communicator clique over every local device ------------
@@ -105,20 +125,34 @@ struct NodeBarrier {
   std::vector<int> devs;
 };
 
+static void release_all(NodeBarrier* b) {
+  if (b == nullptr) return;
+  for (int i = 0; i < b->n; ++i) {
+    (void)hipSetDevice(b->devs[i]);
+    if (b->bufs[i]) (void)hipFree(b->bufs[i]);
+    if (b->streams[i]) (void)hipStreamDestroy(b->streams[i]);
+  }
+  delete b;
+}
+
 int nos_barrier_init_all(int ndev, const int* devlist, void** handle) {
   auto* b = new NodeBarrier();
   b->n = ndev;
   b->devs.assign(devlist, devlist + ndev);
-  b->comms.resize(ndev);
-  b->streams.resize(ndev);
-  b->bufs.resize(ndev);
-  for (int i = 0; i < ndev; ++i) {
-    if (int rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice")) { delete b; return rc; }
-    if (int rc = hip_check(hipStreamCreateWithFlags(&b->streams[i], hipStreamNonBlocking), "hipStreamCreate")) { delete b; return rc; }
-    if (int rc = hip_check(hipMalloc(&b->bufs[i], sizeof(int32_t)), "hipMalloc")) { delete b; return rc; }
+  b->comms.assign(ndev, nullptr);
+  b->streams.assign(ndev, nullptr);
+  b->bufs.assign(ndev, nullptr);
+  int rc = 0;
+  for (int i = 0; i < ndev && !rc; ++i) {
+    rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice");
+    if (!rc) rc = hip_check(hipStreamCreateWithFlags(&b->streams[i], hipStreamNonBlocking), "hipStreamCreate");
+    if (!rc) rc = hip_check(hipMalloc(&b->bufs[i], sizeof(int32_t)), "hipMalloc");
   }
-  if (int rc = nccl_check(ncclCommInitAll(b->comms.data(), ndev, b->devs.data()), "ncclCommInitAll")) {
-    delete b;
+  if (!rc) rc = nccl_check(ncclCommInitAll(b->comms.data(), ndev, b->devs.data()), "ncclCommInitAll");
+  if (rc) {
+    for (int i = 0; i < ndev; ++i)
+      if (b->comms[i]) (void)ncclCommDestroy(b->comms[i]);
+    release_all(b);
     return rc;
   }
   *handle = b;
@@ -147,13 +181,9 @@ int nos_barrier_allreduce_all(void* handle, const int32_t* votes, int32_t* resul
 int nos_barrier_destroy_all(void* handle) {
   auto* b = static_cast<NodeBarrier*>(handle);
   int rc = 0;
-  for (int i = 0; i < b->n; ++i) {
+  for (int i = 0; i < b->n; ++i)
     if (b->comms[i]) rc |= nccl_check(ncclCommDestroy(b->comms[i]), "ncclCommDestroy");
-    (void)hipSetDevice(b->devs[i]);
-    if (b->bufs[i]) (void)hipFree(b->bufs[i]);
-    if (b->streams[i]) (void)hipStreamDestroy(b->streams[i]);
-  }
-  delete b;
+  release_all(b);
   return rc;
 }
 

@@ -269,16 +269,3 @@ def test_probe_runner_survives_a_failing_slice():
     s.record_commit(False)  # a vetoed commit does not trigger a new round
     r.poll()
     assert r.results["commit"] == 1
-
-
-def test_gpu_index_of_resolves_every_id_form_and_rejects_unknown():
-    from walkai_nos_amd.models.errors import GpuError
-    smi = FakeAmdSmi(n_gpus=3)
-    for g in smi.list_gpus():
-        assert smi.gpu_index_of(g.uuid) == g.index
-        assert smi.gpu_index_of(g.bdf) == g.index
-        assert smi.gpu_index_of(f"{g.bdf}/xcp3") == g.index
-        assert smi.gpu_index_of(str(g.index)) == g.index
-    with pytest.raises(GpuError):
-        smi.gpu_index_of("0000:ff:00.0")
-    assert smi.gpu_index_of(smi.list_gpus()[2].bdf) == 2  # a miss re-scans, later hits still resolve

@@ -5,6 +5,7 @@ import os
 import tempfile
 
 import grpc
+import pytest
 
 from walkai_nos_amd.device.protos import dp
 from walkai_nos_amd.device.slicing_client import MemorySliceStore
@@ -148,3 +149,34 @@ def test_amdsmi_metrics_poller_publishes_activity_vram_and_mode():
     text = REGISTRY.render().decode()
     assert 'nos_amdsmi_partition_info{compute="CPX",gpu="0",memory="NPS1",node="node-m"} 8.0' in text
     assert 'compute="SPX",gpu="0",memory="NPS1",node="node-m"' not in text  # stale mode series removed
+
+
+def test_device_plugin_keeps_a_two_slice_request_on_one_gpu():
+    from walkai_nos_amd.deviceplugin.server import preferred_same_gpu
+    store = MemorySliceStore()
+    store.save({0: [Slice("g0::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9),
+                    Slice("g0::s1", "32cu.36gb", [4, 5, 6, 7], 36 * 10**9)],
+                1: [Slice("g1::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9),
+                    Slice("g1::s1", "32cu.36gb", [4, 5, 6, 7], 36 * 10**9),
+                    Slice("g1::s2", "32cu.36gb", [8, 9, 10, 11], 36 * 10**9)]})
+    plug = SliceDevicePlugin("amd.com/gpu-32cu.36gb", store, {0: "/dev/dri/renderD128", 1: "/dev/dri/renderD136"},
+                             socket_dir=tempfile.gettempdir())
+    req = dp.PreferredAllocationRequest()
+    # g0::s0 is in use (not available): GPU 0 is the more-used GPU but has only one free slice left,
+    # so a 2-slice request goes to GPU 1, never across GPUs
+    req.container_requests.add(available_deviceIDs=["g0::s1", "g1::s0", "g1::s1", "g1::s2"], allocation_size=2)
+    req.container_requests.add(available_deviceIDs=["g0::s1", "g1::s0", "g1::s1", "g1::s2"], allocation_size=1)
+    resp = plug.GetPreferredAllocation(req, None)
+    assert list(resp.container_responses[0].deviceIDs) == ["g1::s0", "g1::s1"]
+    assert list(resp.container_responses[1].deviceIDs) == ["g0::s1"]  # packs onto the busier GPU
+    gpu_of = {"a0": 0, "a1": 0, "b0": 1}
+    assert preferred_same_gpu(["b0"], ["a0", "a1", "b0"], 2, gpu_of, {0: 2, 1: 1}) == ["b0", "a0"]  # fallback
+    a = dp.AllocateRequest()
+    a.container_requests.add(devicesIDs=["g0::s1", "g1::s0"])
+    with pytest.raises(ValueError):
+        plug.Allocate(a, None)
+    a = dp.AllocateRequest()
+    a.container_requests.add(devicesIDs=["g1::s0", "g1::s1"])
+    r = plug.Allocate(a, None).container_responses[0]
+    assert dict(r.envs)["HSA_CU_MASK"] == "0:0-63"
+    assert [x.host_path for x in r.devices] == ["/dev/kfd", "/dev/dri/renderD136"]

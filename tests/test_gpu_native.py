@@ -158,3 +158,38 @@ def test_torch_barrier_vote_does_not_wait_for_cu_masked_work(gpu):
         assert t_vote < 0.25 * t_work, (t_vote, t_work)
     finally:
         dist.destroy_process_group()
+
+
+def test_native_device_map_matches_the_box(gpu):
+    import torch
+
+    from walkai_nos_amd.device.amdsmi import NativeAmdSmi
+    smi = NativeAmdSmi()
+    m = smi.device_map()
+    assert m.gpus and m.devices
+    mode = smi.get_compute_partition(0)
+    n_parts = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}[mode]
+    assert len(m.partitions_of(0)) == n_parts
+    for d in m.devices:
+        assert d.hip_id >= 0 and d.render_minor >= 128, d
+        assert smi.resolve(d.uuid) == d and smi.resolve(f"renderD{d.render_minor}") == d
+    assert smi.resolve(m.gpus[0].bdf).partition_index == 0
+    assert sorted(m.hip_ids()) == list(range(torch.cuda.device_count()))
+    if mode == "SPX":
+        assert m.gpus[0].cu_count == 256 and m.gpus[0].xcds == 8
+    # re-enumeration (a new amd-smi session) yields the same layout and generation
+    uuids, gen = [d.uuid for d in m.devices], m.generation
+    m2 = smi.enumerate(reinit=True)
+    assert [d.uuid for d in m2.devices] == uuids and m2.generation == gen
+
+
+def test_agent_keeps_hip_in_spawned_helpers(gpu):
+    from walkai_nos_amd.testing.hygiene import run_agent_cycle
+    r = run_agent_cycle(backend="native", barrier_backend="rccl", probe_backend="hip", target="",
+                        direct_barrier=True)
+    assert not r["hip_loaded"] and not r["torch"] and not r["kfd_open"], r
+    slices = r["probe"]["slices"]
+    assert "gpu0.p0" in slices and slices["gpu0.p0"].get("bf16_tflops", 0) > 300, slices
+    db = r["direct_barrier"]
+    assert db["ok"] is True and db["veto"] is False, db
+    assert db["info"]["seen"] == r["devices"] and db["info"]["sum"] == r["devices"]

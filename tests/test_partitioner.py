@@ -204,3 +204,32 @@ def test_read_only_plan_pass_is_reused_until_the_api_changes():
         assert len(calls) == 2 and pc.plans_written == 1
     finally:
         pcm.plan_cluster_fifo = orig
+
+
+def test_pod_controller_plan_memo_skips_replanning_until_the_api_changes():
+    from walkai_nos_amd.controllers.partitioner import pod_controller as pcm
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=1)
+    c.run(30)
+    ctl = c.pod_controllers[0] if isinstance(c.pod_controllers, list) else c.pod_controllers
+    calls = []
+    orig = pcm.plan_cluster_fifo
+
+    def counting(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    pcm.plan_cluster_fifo = counting
+    try:
+        # an unsatisfiable pod keeps the plan key requeued with nothing to change
+        c.submit({"amd.com/spx_nps1": 2}, name="big")
+        c.run(5)
+        n = len(calls)
+        assert n >= 1
+        for _ in range(5):
+            ctl.reconcile(ctl.plan_key)
+        assert len(calls) == n                       # same revision: memoised answer
+        c.api.patch("Node", "node-0", {"metadata": {"annotations": {"touch": "1"}}})
+        ctl.reconcile(ctl.plan_key)
+        assert len(calls) == n + 1                   # a node write forces a re-plan
+    finally:
+        pcm.plan_cluster_fifo = orig

@@ -37,6 +37,10 @@ ANNOTATION_MEMORY_PARTITION_SPEC = "nos.nebuly.com/spec-memory-partition"
 ANNOTATION_MEMORY_PARTITION_STATUS = "nos.nebuly.com/status-memory-partition"
 # MI355X: outcome of the node-atomic commit barrier for the last plan ("ok" / "failed:<reason>")
 ANNOTATION_COMMIT_STATUS = "nos.nebuly.com/status-partitioning-commit"
+# MI355X: write-ahead journal of the plan the agent is applying (JSON {plan, from, to}); written
+# before the first mode flip and removed after the commit, so an agent that crashes between two
+# flips finds the half-applied plan at start-up (see Actuator.startup)
+ANNOTATION_INFLIGHT_PLAN = "nos.nebuly.com/status-partitioning-inflight"
 # MI355X: probe-kernel measurement published by the agent (JSON: per slice TFLOP/s per CU)
 ANNOTATION_PROBE_RESULT = "nos.nebuly.com/status-probe"
 

@@ -262,9 +262,12 @@ class NodeBench:
         for devs in sn.kubelet.allocations.values():
             for r, dev_id in devs:
                 prof = extract_profile_name(r)
-                if prof is None or sn.smi.gpu_index_of(dev_id) != self.cfg.rank:
+                if prof is None:
                     continue
-                part = int(dev_id.rsplit("xcp", 1)[1])
+                d = sn.smi.resolve(dev_id)
+                if d.gpu_index != self.cfg.rank:
+                    continue
+                part = d.partition_index
                 out.append((prof, part, 8 // COMPUTE_MODES[prof.split("_")[0]]))
         return out
 

@@ -2,8 +2,13 @@
 
 Per-node DaemonSet: reads ``NODE_NAME``; builds the kubelet PodResources client (its error is
 fatal here), one amd-smi session and the partition client; at startup checks that the
-node has at least one compute-partition-capable GPU; then runs the reporter and the actuator
-sharing a :class:`SharedState`, with the RCCL node commit barrier over all local GPUs.
+node has at least one compute-partition-capable GPU and runs the start-up reconciliation
+(:meth:`Actuator.startup`: a plan journalled but not committed before a crash is rolled forward);
+then runs the reporter and the actuator sharing a :class:`SharedState`.
+
+The agent process never initialises HIP: the RCCL commit barrier (one communicator over every
+logical device of the re-enumerated node, 64 in CPX on 8 GPUs) and the probe-on-commit kernels run
+in spawned helper processes (``cmd/gpuhelper.py``) that exit before the next flip.
 """
 from __future__ import annotations
 
@@ -23,14 +28,11 @@ from .common import base_parser, make_client, make_manager, run_until_signal, se
 log = logging.getLogger("nos.partitionagent")
 
 
-def node_barrier_factory(smi):
-    """One RCCL communicator over every local GPU, created per commit (a flip re-enumerates)."""
-    from ..parallel.barrier import LocalBarrier
-    try:
-        from ..parallel.node_barrier import RcclNodeBarrier
-    except ImportError:  # pragma: no cover
-        return lambda n: LocalBarrier(n)
-    return lambda n: RcclNodeBarrier(len(smi.list_gpus()))
+def node_barrier_factory(registry, backend: str = "rccl"):
+    """Commit barrier per commit: a spawned helper voting over ``n`` logical devices (the actuator
+    passes one vote per device of the re-enumerated map)."""
+    from ..parallel.spawned import SpawnedNodeBarrier
+    return lambda n: SpawnedNodeBarrier(n, backend=backend, registry=registry)
 
 
 def main(argv=None) -> int:
@@ -48,13 +50,18 @@ def main(argv=None) -> int:
     pc = PartitionClient(resources, smi)
     dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
     mgr = make_manager(client, cfg, "partitionagent")
-    bf = node_barrier_factory(smi) if cfg.commitBarrier == "rccl" else None
+    from ..parallel.spawned import HelperRegistry
+    helpers = HelperRegistry()
+    bf = node_barrier_factory(helpers) if cfg.commitBarrier == "rccl" else None
     probe = None
     if cfg.probeOnCommit:
-        from ..controllers.agent.probe import ProbeRunner
-        probe = lambda shared: ProbeRunner(shared, node).annotations  # noqa: E731
-    setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
-                          refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe)
+        from ..controllers.agent.probe import ProbeRunner, device_map_targets
+        probe = lambda shared: ProbeRunner(shared, node, targets=device_map_targets(smi)).annotations  # noqa: E731
+    _, _, actuator = setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
+                                           refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe,
+                                           helpers=helpers)
+    log.info("device map: %s", smi.device_map().describe())
+    log.info("start-up reconciliation: %s", actuator.startup())
     from ..exporters.gpu_metrics import GpuMetricsPoller
     GpuMetricsPoller(smi, node).register(mgr)
     serve_endpoints(mgr, cfg)

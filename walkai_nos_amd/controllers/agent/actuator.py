@@ -8,17 +8,34 @@ Reconcile, per annotation change on its own node:
 4. plan from the *actual* state (kubelet devices + amd-smi modes); devices NotFound → re-register
    the device plugin;
 5. skip an empty plan, or one identical to the last applied with an unchanged status;
-6. apply: node-wide NPS change first (only on an idle node), then one mode flip per GPU; if any
-   flip fails, **roll back** the GPUs already flipped in this plan to their previous mode (the
-   reference re-creates deleted MIG profiles, ``actuator.go:181-184``);
-7. **node-atomic commit**: every GPU is re-enumerated and verified, then all participants vote
-   through the RCCL commit barrier; a failed vote rolls the plan back too;
-8. re-register the device plugin when anything changed.
+6. apply:
+
+   * write the plan to the ``status-partitioning-inflight`` journal annotation first (no journal,
+     no flip), and stop every spawned GPU helper of this agent (a helper still holding a KFD
+     context would make the flip fail);
+   * node-wide NPS change first (only on an idle node);
+   * one mode flip per GPU, each only if amd-smi reports **no process** on any partition of that
+     GPU (the MI355X form of ref ``actuator.go:221-229``'s "never delete used devices": a flip
+     destroys every partition).  A busy GPU is skipped and the plan retried with back-off;
+   * if a flip fails, **roll back** the GPUs already flipped in this plan (ref re-creates deleted
+     MIG profiles, ``actuator.go:181-184``);
+
+7. **node-atomic commit**: the backend re-enumerated the device map after the flips; every
+   logical device of the node gets a vote (its GPU in the planned mode, with the planned number
+   of partitions, and ``verify`` passing), and the votes go through the commit barrier — in
+   production a spawned helper that sees exactly those devices and all-reduces over RCCL.  A veto
+   rolls the plan back;
+8. re-register the device plugin when anything changed; clear the journal.
+
+:meth:`Actuator.startup` is the start-up pass (ref ``cmd/migagent/migagent.go:165-199``'s
+``initAgent``): it finds a journal left by a crash between two flips and rolls the node forward to
+the current spec (or leaves it to the normal plan if the spec moved on) before the controllers run.
 
 Fixes vs the reference: a deleted node (NotFound) is ignored instead of retried forever (Q13).
 """
 from __future__ import annotations
 
+import json
 import logging
 import time
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -29,6 +46,7 @@ from ...kube.errors import NotFound
 from ...kube.runtime import Request, Result
 from ...models import annotation as ann
 from ...models.errors import GpuError, is_not_found
+from ...models.xcp.profile import parse_profile
 from ...parallel.barrier import CommitBarrier
 from ...utils.metrics import REGISTRY
 from .plan import XcpConfigPlan, XcpState, new_xcp_config_plan
@@ -42,7 +60,8 @@ BarrierFactory = Callable[[int], CommitBarrier]
 class Actuator:
     def __init__(self, client: Any, partition_client: Any, shared: SharedState, node_name: str,
                  device_plugin: Any = None, barrier_factory: Optional[BarrierFactory] = None,
-                 verify: Optional[Callable[[int, str], bool]] = None, clock: Callable[[], float] = time.time):
+                 verify: Optional[Callable[[int, str], bool]] = None, clock: Callable[[], float] = time.time,
+                 journal: bool = True):
         self.client = client
         self.pc = partition_client
         self.shared = shared
@@ -51,9 +70,11 @@ class Actuator:
         self.barrier_factory = barrier_factory
         self.verify = verify
         self.clock = clock
+        self.journal = journal
         self.last_applied_plan: Optional[XcpConfigPlan] = None
         self.last_applied_status: Optional[list] = None
         self.applied_plans = 0
+        self.last_votes: List[bool] = []
 
     def reconcile(self, req: Request) -> Result:
         if not self.shared.at_least_one_report_since_last_apply():
@@ -65,7 +86,8 @@ class Actuator:
             except NotFound:
                 return Result()
             anns = ko.annotations(node)
-            self.shared.last_parsed_plan_id = anns.get(api.ANNOTATION_PARTITIONING_PLAN, "")
+            plan_id = anns.get(api.ANNOTATION_PARTITIONING_PLAN, "")
+            self.shared.last_parsed_plan_id = plan_id
             status, spec = ann.parse_node_annotations(anns)
             spec_nps = anns.get(api.ANNOTATION_MEMORY_PARTITION_SPEC)
             status_nps = anns.get(api.ANNOTATION_MEMORY_PARTITION_STATUS)
@@ -84,7 +106,7 @@ class Actuator:
                         ann.annotations_equal(status, self.last_applied_status):
                     log.debug("plan already applied and status unchanged")
                     return Result()
-                err = self.apply(plan)
+                err = self.apply(plan, plan_id)
                 if err is not None:
                     # a failed plan is retried (with the runtime's back-off) instead of being
                     # remembered as applied: the reference records it anyway (defer at
@@ -114,26 +136,44 @@ class Actuator:
                 return XcpConfigPlan()
         return new_xcp_config_plan(state, current, spec, spec_nps, cur_nps)
 
-    def apply(self, plan: XcpConfigPlan) -> Optional[Exception]:
+    # -- apply --------------------------------------------------------------------------------
+    def apply(self, plan: XcpConfigPlan, plan_id: str = "") -> Optional[Exception]:
         t0 = time.perf_counter()
         errors: List[str] = []
+        busy: List[int] = []
         flipped: List[Tuple[int, Optional[str]]] = []
         changed = False
+        try:
+            self._write_journal(plan, plan_id)
+        except Exception as e:  # noqa: BLE001 - no durable record, no flip
+            REGISTRY.apply_errors.labels(node=self.node_name, op="journal").inc()
+            return GpuError(f"unable to journal plan {plan_id!r} before applying it: {e}")
+        stopped = self.shared.helpers.quiesce()
+        if stopped:
+            log.info("stopped %d GPU helper process(es) before flipping", stopped)
         if plan.memory_partition:
             try:
                 self.pc.set_memory_partition(plan.memory_partition)
                 changed = True
             except GpuError as e:
                 REGISTRY.apply_errors.labels(node=self.node_name, op="memory_partition").inc()
+                self._clear_journal()
                 return e
             # the driver reload re-derived every GPU's compute mode; re-read before flipping
             current = self.pc.current_profiles()
             plan.changes = [c.__class__(c.gpu_index, current.get(c.gpu_index), c.to_profile)
                             for c in plan.changes if current.get(c.gpu_index) != c.to_profile]
+        applied = []
         for ch in plan.changes:
+            if self._gpu_busy(ch.gpu_index):
+                busy.append(ch.gpu_index)
+                REGISTRY.apply_errors.labels(node=self.node_name, op="gpu_busy").inc()
+                log.info("GPU %d has processes on its partitions: not flipping it to %s", ch.gpu_index, ch.to_profile)
+                continue
             try:
                 self.pc.set_profile(ch.gpu_index, ch.to_profile)
                 flipped.append((ch.gpu_index, ch.from_profile))
+                applied.append(ch)
                 changed = True
             except GpuError as e:
                 REGISTRY.apply_errors.labels(node=self.node_name, op="compute_partition").inc()
@@ -141,32 +181,40 @@ class Actuator:
                 break
         ok = not errors
         if ok and changed:
-            ok = self._commit(plan)
+            ok = self._commit(applied)
             if not ok:
                 errors.append("commit barrier vetoed the plan")
         if not ok and flipped:
             self._rollback(flipped)
         if changed:
             self._reregister()
+        self._clear_journal()
         REGISTRY.phase_seconds.labels(phase="agent_apply_total").observe(time.perf_counter() - t0)
         self.applied_plans += 1
-        self.shared.record_commit(ok)
-        if plan.blocked:
-            for g, reason in plan.blocked:
-                log.info("GPU %d not changed: %s", g, reason)
+        if changed or errors:
+            self.shared.record_commit(ok)
+        for g, reason in plan.blocked:
+            log.info("GPU %d not changed: %s", g, reason)
         if errors:
             return GpuError("at least one operation failed while applying the partitioning plan: " + "; ".join(errors))
+        if busy:
+            return GpuError(f"GPU(s) {busy} busy (processes on their partitions); retrying later", GpuError.BUSY)
         return None
 
-    def _commit(self, plan: XcpConfigPlan) -> bool:
-        """Verify every changed GPU, then vote through the node's commit barrier."""
-        current = self.pc.current_profiles()
-        votes = []
-        for ch in plan.changes:
-            ok = current.get(ch.gpu_index) == ch.to_profile
-            if ok and self.verify is not None:
-                ok = bool(self.verify(ch.gpu_index, ch.to_profile))
-            votes.append(ok)
+    def _gpu_busy(self, gpu: int) -> bool:
+        fn = getattr(self.pc, "gpu_busy", None)
+        if fn is None:
+            return False
+        try:
+            return bool(fn(gpu))
+        except GpuError as e:
+            log.warning("process list of GPU %d unavailable (%s): treating it as busy", gpu, e)
+            return True
+
+    def _commit(self, applied: List[Any]) -> bool:
+        """One vote per logical device of the re-enumerated node, through the commit barrier."""
+        votes = self._votes(applied)
+        self.last_votes = votes
         if self.barrier_factory is None:
             return all(votes)
         barrier = self.barrier_factory(max(1, len(votes)))
@@ -177,6 +225,31 @@ class Actuator:
             return bool(barrier.vote(all(votes)))
         finally:
             barrier.close()
+
+    def _votes(self, applied: List[Any]) -> List[bool]:
+        target = {ch.gpu_index: ch.to_profile for ch in applied}
+        dm_fn = getattr(self.pc, "device_map", None)
+        if dm_fn is None:
+            # a partition client without a device map: one vote per changed GPU
+            current = self.pc.current_profiles()
+            votes = []
+            for g, p in target.items():
+                ok = current.get(g) == p
+                if ok and self.verify is not None:
+                    ok = bool(self.verify(g, p))
+                votes.append(ok)
+            return votes
+        m = dm_fn()
+        gpu_ok: Dict[int, bool] = {}
+        for g, p in target.items():
+            parts = m.partitions_of(g)
+            ok = bool(parts) and len(parts) == parse_profile(p).partitions and \
+                all(f"{d.compute_mode}_{d.memory_mode}".lower() == p for d in parts)
+            if ok and self.verify is not None:
+                ok = bool(self.verify(g, p))
+            gpu_ok[g] = ok
+        devices = sorted(m.devices, key=lambda d: (d.hip_id, d.gpu_index, d.partition_index))
+        return [gpu_ok.get(d.gpu_index, True) for d in devices]
 
     def _rollback(self, flipped: List[Tuple[int, Optional[str]]]) -> None:
         log.info("rolling back %d GPU mode change(s)", len(flipped))
@@ -195,3 +268,64 @@ class Actuator:
             self.device_plugin.restart(self.node_name)
         except GpuError as e:
             log.error("unable to re-register the device plugin: %s", e)
+
+    # -- journal ------------------------------------------------------------------------------
+    def _write_journal(self, plan: XcpConfigPlan, plan_id: str) -> None:
+        if not self.journal:
+            return
+        entry = {"plan": plan_id, "at": round(self.clock(), 3),
+                 "from": {str(c.gpu_index): c.from_profile for c in plan.changes},
+                 "to": {str(c.gpu_index): c.to_profile for c in plan.changes}}
+        if plan.memory_partition:
+            entry["nps"] = plan.memory_partition
+        self.client.patch("Node", self.node_name, {"metadata": {"annotations": {
+            api.ANNOTATION_INFLIGHT_PLAN: json.dumps(entry, sort_keys=True, separators=(",", ":"))}}})
+
+    def _clear_journal(self) -> None:
+        if not self.journal:
+            return
+        try:
+            self.client.patch("Node", self.node_name, {"metadata": {"annotations": {api.ANNOTATION_INFLIGHT_PLAN: None}}})
+        except Exception as e:  # noqa: BLE001 - a stale journal is handled by the next start-up
+            log.warning("unable to clear the in-flight plan journal: %s", e)
+
+    # -- start-up -----------------------------------------------------------------------------
+    def startup(self) -> Dict[str, Any]:
+        """Start-up reconciliation, run once before the controllers start.
+
+        * no journal: nothing was in flight; the normal report → apply loop takes over;
+        * a journal whose plan is still the node's spec plan: the agent died between two flips of
+          that plan — roll forward now (one synchronous apply against the actual devices);
+        * a journal of a superseded plan: the spec moved on; apply the *current* spec now, which
+          also moves any GPU left in the old plan's half-applied state.
+
+        Either way the journal is cleared afterwards, and the outcome is returned (and logged)."""
+        out: Dict[str, Any] = {"journal": None, "action": "none", "modes": {}}
+        try:
+            node = self.client.get("Node", self.node_name)
+        except NotFound:
+            return out
+        anns = ko.annotations(node)
+        raw = anns.get(api.ANNOTATION_INFLIGHT_PLAN)
+        out["modes"] = dict(self.pc.current_profiles())
+        if not raw:
+            return out
+        try:
+            journal = json.loads(raw)
+        except ValueError:
+            journal = {"plan": None}
+        out["journal"] = journal
+        spec_plan = anns.get(api.ANNOTATION_PARTITIONING_PLAN, "")
+        out["action"] = "roll-forward" if journal.get("plan") == spec_plan else "superseded"
+        log.warning("found in-flight plan %s at start-up (spec plan %s, modes %s): %s",
+                    journal.get("plan"), spec_plan, out["modes"], out["action"])
+        REGISTRY.apply_errors.labels(node=self.node_name, op="startup_" + out["action"]).inc()
+        self.shared.on_report_done()  # the devices are read fresh by the plan below
+        try:
+            self.reconcile(Request(self.node_name))
+        except GpuError as e:
+            out["error"] = str(e)
+            log.error("start-up apply failed (the controllers will retry): %s", e)
+        self._clear_journal()
+        out["modes_after"] = dict(self.pc.current_profiles())
+        return out

@@ -2,7 +2,9 @@
 
 After each successful node commit (``SharedState.commit_seq`` advances) the agent runs the HIP
 probe kernels (``csrc/probe.hip``) on every logical device the node now exposes — bf16 and fp32
-MFMA throughput and HBM copy bandwidth — on a background thread, and publishes the result as the
+MFMA throughput and HBM copy bandwidth — in a spawned helper process (``cmd/gpuhelper.py``: the
+agent itself never initialises HIP, and the helper is stopped before the next flip), from a
+background thread, and publishes the result as the
 ``nos.nebuly.com/status-probe`` node annotation (through the reporter's extra-annotation hook) and
 as Prometheus gauges (``nos_probe_slice_tflops``, ``nos_probe_tflops_per_cu``,
 ``nos_probe_hbm_gbps``). This is the MI355X addition to the reference's status protocol
@@ -40,17 +42,38 @@ def hip_probe(device: int, cus: Optional[List[int]], label: str) -> Dict[str, fl
             "hbm_gbps": round(float(hbm.get("gbps", 0.0)), 0)}
 
 
-def local_device_targets() -> List[tuple]:
-    """Every HIP device of the node (after a compute-partition flip these are the partitions)."""
-    from ...ops import probe as P
-    return [(i, None, f"dev{i}") for i in range(P.device_count())]
+def device_map_targets(smi: Any) -> TargetsFn:
+    """Every logical device of the node's current device map, labelled ``gpu<i>.p<k>``; the
+    device index is the HIP ordinal a freshly spawned helper sees for it."""
+    def targets() -> List[tuple]:
+        return [(d.hip_id, None, f"gpu{d.gpu_index}.p{d.partition_index}")
+                for d in sorted(smi.logical_devices(), key=lambda d: d.hip_id) if d.hip_id >= 0]
+    return targets
+
+
+#: targets -> {label: result}; the default runs them all in one spawned helper process
+RoundFn = Callable[[List[tuple]], Dict[str, Any]]
+
+
+def spawned_round(registry: Any = None, backend: str = "hip") -> RoundFn:
+    from ...parallel.spawned import spawned_probe_round
+    return lambda targets: spawned_probe_round(targets, backend=backend, registry=registry)
 
 
 class ProbeRunner:
-    def __init__(self, shared: SharedState, node_name: str, probe_fn: ProbeFn = hip_probe,
-                 targets: TargetsFn = local_device_targets, asynchronous: bool = True):
+    """``round_fn`` (default for agents: a spawned helper, so the agent never holds a GPU context)
+    probes all targets of one commit; ``probe_fn`` is the in-process per-target alternative used
+    by the GPU tests."""
+
+    def __init__(self, shared: SharedState, node_name: str, probe_fn: Optional[ProbeFn] = None,
+                 targets: Optional[TargetsFn] = None, asynchronous: bool = True,
+                 round_fn: Optional[RoundFn] = None):
         self.shared, self.node = shared, node_name
-        self.probe_fn, self.targets = probe_fn, targets
+        if probe_fn is None and round_fn is None:
+            round_fn = spawned_round(shared.helpers)
+        if targets is None:
+            raise ValueError("ProbeRunner needs a targets function (e.g. device_map_targets(smi))")
+        self.probe_fn, self.round_fn, self.targets = probe_fn, round_fn, targets
         self.asynchronous = asynchronous
         self._seen = -1
         self._lock = threading.Lock()
@@ -73,14 +96,26 @@ class ProbeRunner:
         t0 = time.time()
         out: Dict[str, Any] = {}
         try:
-            for dev, cus, label in self.targets():
+            targets = list(self.targets())
+            batch: Dict[str, Any] = {}
+            if self.round_fn is not None:
                 try:
-                    r = self.probe_fn(dev, cus, label)
-                except Exception as e:  # noqa: BLE001 - one bad partition must not hide the others
-                    log.warning("probe of %s failed: %s", label, e)
-                    out[label] = {"error": str(e)[:200]}
-                    continue
+                    batch = self.round_fn(targets)
+                except Exception as e:  # noqa: BLE001 - a failed helper is reported, not raised
+                    log.warning("probe round failed: %s", e)
+                    batch = {label: {"error": str(e)[:200]} for _, _, label in targets}
+            for dev, cus, label in targets:
+                if self.round_fn is not None:
+                    r = batch.get(label, {"error": "no result"})
+                else:
+                    try:
+                        r = self.probe_fn(dev, cus, label)
+                    except Exception as e:  # noqa: BLE001 - one bad partition must not hide the others
+                        r = {"error": str(e)[:200]}
                 out[label] = r
+                if "error" in r:
+                    log.warning("probe of %s failed: %s", label, r["error"])
+                    continue
                 n = max(1, int(r.get("n_cus", 1)))
                 for dt in ("bf16", "fp32"):
                     if f"{dt}_tflops" in r:

@@ -15,10 +15,11 @@ def setup_partition_agent(mgr: Manager, node_name: str, partition_client: Any, d
                           barrier_factory: Optional[BarrierFactory] = None, refresh_interval: float = 10.0,
                           verify: Optional[Callable[[int, str], bool]] = None,
                           extra_annotations: Optional[Callable[[], dict]] = None,
-                          probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None):
+                          probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None,
+                          helpers: Any = None):
     """``probe``: factory taking the agent's SharedState and returning an extra-annotation hook
     (e.g. ``lambda sh: ProbeRunner(sh, node).annotations``) that measures each commit."""
-    shared = SharedState()
+    shared = SharedState(helpers)
     if probe is not None:
         hook = probe(shared)
         if extra_annotations is None:

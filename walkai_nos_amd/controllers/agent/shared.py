@@ -17,13 +17,16 @@ from typing import Optional
 
 
 class SharedState:
-    def __init__(self) -> None:
+    def __init__(self, helpers=None) -> None:
         self.lock = threading.RLock()
         self.last_parsed_plan_id: str = ""
         self.last_commit: Optional[str] = None
         self.commit_seq = 0  # bumped on every successful commit (probe-on-commit trigger)
         self._token = False
         self._token_lock = threading.Lock()
+        # spawned GPU helpers (probe, commit barrier) of this agent; stopped before every flip
+        from ...parallel.spawned import HelperRegistry
+        self.helpers = helpers if helpers is not None else HelperRegistry()
 
     def record_commit(self, ok: bool) -> None:
         with self.lock:

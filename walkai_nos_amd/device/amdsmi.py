@@ -3,106 +3,193 @@
 Two implementations of one interface:
 
 * :class:`NativeAmdSmi` — ctypes over ``libnos_amdsmi.so`` (``csrc/amdsmi_backend.cpp``), a thin C
-  ABI over ``libamd_smi``: inventory (UUID, BDF, VRAM, CU count), compute-partition get/set
-  (``amdsmi.h:5768,5799``), memory-partition get/set (``:5844,5876``), activity, VRAM usage and the
-  process list used for the "GPU busy" check.  Setters need root (``AMDSMI_STATUS_PERMISSION``,
+  ABI over ``libamd_smi``: processor enumeration (UUID, BDF + KFD location id, partition id, KFD
+  node, HIP ordinal, render node, VRAM, CU and XCD counts), compute-partition get/set
+  (``amdsmi.h:5768,5799``), memory-partition get/set (``:5844,5876``), activity, VRAM usage and
+  the process list used for the "GPU busy" check.  Setters need root (``AMDSMI_STATUS_PERMISSION``,
   ``amdsmi.h:5790``) and surface as :class:`GpuError` with code ``permission``.
 * :class:`FakeAmdSmi` — same API, in memory, with fault injection (permission denied, device
-  busy, per-GPU failures, partial success) and re-enumeration; the test and simulator backend
-  (and the only one that can flip modes on the non-root ``gpurun`` box).
+  busy, per-GPU failures, partial success) and **faithful re-enumeration**: after a flip to CPX it
+  reports eight processors per GPU with new UUIDs, HIP ordinals and render nodes, as the real
+  library does, so stale ids stop resolving.
 
-Unlike the reference NVML client, which does ``Init``/``Shutdown`` around every call,
-one session is kept per agent process.
+Both keep a :class:`~walkai_nos_amd.device.topology.DeviceMap` (physical GPU <-> logical
+partition) that is rebuilt after every ``set_*`` call — the native backend re-initialises its
+amd-smi session for that, because processor handles do not survive a partition change.  All
+public per-GPU methods take the *physical* GPU index; the partition agent never sees a stale
+handle (ref ``pkg/gpu/nvml/client.go:46-57`` gets the same effect by re-initialising NVML around
+every call).
+
+Nothing here initialises HIP: the agent process must not hold a KFD context while it flips modes
+(a held context is exactly what makes a compute-partition switch fail with "busy").
 """
 from __future__ import annotations
 
 import ctypes
 import os
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
 
 from ..models.errors import GpuError
 from ..models.xcp.known_configs import get_model_spec
 from ..models.xcp.profile import COMPUTE_MODES, MEMORY_MODES
+from .topology import NO_PARTITION, DeviceMap, GpuInfo, LogicalDevice, ProcInfo, build_device_map
+
+__all__ = ["AmdSmi", "FakeAmdSmi", "NativeAmdSmi", "GpuInfo", "LogicalDevice", "DeviceMap", "new_backend",
+           "COMPUTE_MODE_NAMES", "MEMORY_MODE_NAMES"]
 
 COMPUTE_MODE_NAMES = ("SPX", "DPX", "QPX", "CPX")
 MEMORY_MODE_NAMES = ("NPS1", "NPS2", "NPS4", "NPS8")
 
 
-@dataclass
-class GpuInfo:
-    index: int
-    uuid: str
-    bdf: str
-    model: str
-    vram_bytes: int
-    cu_count: int
-    xcds: int = 8
-
-
-@dataclass
-class LogicalDevice:
-    """One logical GPU (compute partition) as enumerated after a mode switch."""
-    gpu_index: int
-    partition_index: int
-    device_id: str
-    compute_mode: str
-    memory_mode: str
+def _nps(mode: str) -> int:
+    return MEMORY_MODES.get(mode.lower(), 1)
 
 
 class AmdSmi:
-    """Backend interface."""
+    """Backend interface.  Subclasses implement the per-processor hooks (``_processors`` …); the
+    base class owns the node's device map and re-enumerates it after every partition change."""
+
+    #: minimum seconds between re-enumerations triggered by unknown device ids (kubelet keeps
+    #: advertising the old partitions until the device plugin re-registers)
+    miss_rescan_interval = 5.0
+
+    def __init__(self) -> None:
+        self._map_lock = threading.RLock()
+        self._map: Optional[DeviceMap] = None
+        self._procs: Dict[int, ProcInfo] = {}
+        self._generation = 0
+        self._last_miss_scan = -1e9
+        self.enumerations = 0
+
+    # -- backend hooks ------------------------------------------------------------------------
+    def _processors(self, reinit: bool) -> List[ProcInfo]:
+        raise NotImplementedError
+
+    def _compute_partition(self, proc: ProcInfo) -> str:
+        raise NotImplementedError
+
+    def _memory_partition(self, proc: ProcInfo) -> str:
+        raise NotImplementedError
+
+    def _set_compute_partition(self, proc: ProcInfo, mode: str) -> None:
+        raise NotImplementedError
+
+    def _set_memory_partition(self, proc: ProcInfo, mode: str) -> None:
+        raise NotImplementedError
+
+    def _process_count(self, proc: ProcInfo) -> int:
+        raise NotImplementedError
+
+    def _activity(self, proc: ProcInfo) -> Dict[str, float]:
+        raise NotImplementedError
+
+    def _vram_usage(self, proc: ProcInfo) -> Dict[str, int]:
+        raise NotImplementedError
+
+    # -- device map -------------------------------------------------------------------------------
+    def enumerate(self, reinit: bool = True) -> DeviceMap:
+        """Re-read every processor and rebuild the physical <-> logical map."""
+        with self._map_lock:
+            procs = self._processors(reinit)
+            self._procs = {p.ordinal: p for p in procs}
+            old = self._map
+            m = build_device_map(procs, self._compute_partition, self._memory_partition, _nps, self._generation)
+            if old is None or [d.uuid for d in old.devices] != [d.uuid for d in m.devices] or \
+                    old.modes() != m.modes():
+                self._generation += 1
+                m.generation = self._generation
+            else:
+                m.generation = old.generation
+            self._map = m
+            self.enumerations += 1
+            return m
+
+    def device_map(self) -> DeviceMap:
+        with self._map_lock:
+            if self._map is None:
+                return self.enumerate(reinit=False)
+            return self._map
 
     def list_gpus(self) -> List[GpuInfo]:
-        raise NotImplementedError
+        return list(self.device_map().gpus)
 
+    def logical_devices(self) -> List[LogicalDevice]:
+        return list(self.device_map().devices)
+
+    def resolve(self, device_id: str) -> LogicalDevice:
+        """Device id (partition UUID, HIP UUID, ``renderD<n>``, BDF, ``<bdf>::s<n>``) -> partition.
+        An unknown id triggers one rate-limited re-enumeration before NOT_FOUND."""
+        m = self.device_map()
+        d = m.lookup(device_id)
+        if d is not None:
+            return d
+        with self._map_lock:
+            now = time.monotonic()
+            if now - self._last_miss_scan >= self.miss_rescan_interval:
+                self._last_miss_scan = now
+                m = self.enumerate(reinit=True)
+        return m.resolve(device_id)
+
+    def gpu_index_of(self, device_id: str) -> int:
+        return self.resolve(device_id).gpu_index
+
+    def _primary(self, gpu_index: int) -> ProcInfo:
+        d = self.device_map().primary(gpu_index)
+        return self._procs[d.proc_ordinal]
+
+    def _members(self, gpu_index: int) -> List[ProcInfo]:
+        m = self.device_map()
+        parts = m.partitions_of(gpu_index)
+        if not parts:
+            raise GpuError(f"GPU {gpu_index} not found", GpuError.NOT_FOUND)
+        return [self._procs[d.proc_ordinal] for d in parts]
+
+    # -- per physical GPU -------------------------------------------------------------------------
     def get_compute_partition(self, index: int) -> str:
-        raise NotImplementedError
-
-    def set_compute_partition(self, index: int, mode: str) -> None:
-        raise NotImplementedError
+        return self.device_map().primary(index).compute_mode
 
     def get_memory_partition(self, index: int) -> str:
-        raise NotImplementedError
+        return self.device_map().primary(index).memory_mode
+
+    def set_compute_partition(self, index: int, mode: str) -> None:
+        mode = mode.upper()
+        if mode not in COMPUTE_MODE_NAMES:
+            raise GpuError(f"invalid compute partition {mode!r}")
+        with self._map_lock:
+            proc = self._primary(index)
+            try:
+                self._set_compute_partition(proc, mode)
+            finally:
+                # the old handles are gone whether or not the switch completed
+                self.enumerate(reinit=True)
 
     def set_memory_partition(self, mode: str) -> None:
         """Node-wide: reloads the driver for every GPU (``amdsmi.h:6600-6615``)."""
-        raise NotImplementedError
+        mode = mode.upper()
+        if mode not in MEMORY_MODE_NAMES:
+            raise GpuError(f"invalid memory partition {mode!r}")
+        with self._map_lock:
+            proc = self._primary(0)
+            try:
+                self._set_memory_partition(proc, mode)
+            finally:
+                self.enumerate(reinit=True)
 
     def process_count(self, index: int) -> int:
-        raise NotImplementedError
+        """Processes holding any partition of physical GPU ``index`` (a flip destroys them all)."""
+        return sum(self._process_count(p) for p in self._members(index))
 
     def activity(self, index: int) -> Dict[str, float]:
-        raise NotImplementedError
+        acts = [self._activity(p) for p in self._members(index)]
+        return {k: sum(a[k] for a in acts) / len(acts) for k in ("gfx", "umc", "mm")}
 
     def vram_usage(self, index: int) -> Dict[str, int]:
-        raise NotImplementedError
-
-    def logical_devices(self) -> List[LogicalDevice]:
-        out: List[LogicalDevice] = []
-        for g in self.list_gpus():
-            cm = self.get_compute_partition(g.index)
-            mm = self.get_memory_partition(g.index)
-            for p in range(COMPUTE_MODES[cm.lower()]):
-                out.append(LogicalDevice(g.index, p, f"{g.bdf}/xcp{p}", cm, mm))
-        return out
-
-    def gpu_index_of(self, device_id: str) -> int:
-        """Map a device id (GPU UUID, BDF or ``<bdf>/xcp<k>``) to the physical GPU index."""
-        base = device_id.split("/xcp", 1)[0].split("::", 1)[0]
-        # the GPU set of a node is fixed for the process: index the ids once (re-scanned on a miss),
-        # the device plugin and the reporters resolve every allocated device on each pass
-        ids = getattr(self, "_gpu_ids", None)
-        if ids is None or base not in ids:
-            ids = {}
-            for g in self.list_gpus():
-                for k in (g.uuid, g.bdf, str(g.index)):
-                    ids.setdefault(k, g.index)
-            self._gpu_ids = ids
-        if base in ids:
-            return ids[base]
-        raise GpuError(f"device {device_id!r} not found", GpuError.NOT_FOUND)
+        members = self._members(index)
+        used = sum(self._vram_usage(p)["used"] for p in members)
+        return {"total": self.device_map().gpus[index].vram_bytes, "used": used}
 
     def close(self) -> None:
         return
@@ -111,44 +198,69 @@ class AmdSmi:
 # ------------------------------------------------------------------------------------------
 @dataclass
 class _FakeGpu:
-    info: GpuInfo
+    index: int
+    uuid: str
+    bdf: str
     compute: str = "SPX"
     memory: str = "NPS1"
-    processes: int = 0
+    processes: Dict[int, int] = field(default_factory=dict)  # partition -> process count
 
 
-@dataclass
 class FakeAmdSmi(AmdSmi):
-    """In-memory amd-smi with fault injection."""
-    n_gpus: int = 8
-    model: str = "MI355X"
-    is_root: bool = True
-    fail_set: Set[int] = field(default_factory=set)          # GPU indexes whose set fails
-    busy: Set[int] = field(default_factory=set)              # GPU indexes reported busy
-    fail_next: int = 0                                       # fail the next N set calls
-    memory_mode_requires_idle: bool = True
+    """In-memory amd-smi with fault injection and MI300-style re-enumeration."""
 
-    def __post_init__(self) -> None:
-        spec = get_model_spec(self.model)
-        mem = (spec.memory_gb if spec else 288) * 10**9
-        cus = spec.compute_units if spec else 256
-        xcds = spec.xcds if spec else 8
+    def __init__(self, n_gpus: int = 8, model: str = "MI355X", is_root: bool = True,
+                 fail_set: Optional[Set[int]] = None, busy: Optional[Set[int]] = None, fail_next: int = 0,
+                 memory_mode_requires_idle: bool = True):
+        super().__init__()
+        self.n_gpus, self.model, self.is_root = n_gpus, model, is_root
+        self.fail_set: Set[int] = set(fail_set or ())      # GPU indexes whose set fails
+        self.busy: Set[int] = set(busy or ())              # GPU indexes reported busy
+        self.fail_next = fail_next                         # fail the next N set calls
+        self.memory_mode_requires_idle = memory_mode_requires_idle
+        spec = get_model_spec(model)
+        self._mem = (spec.memory_gb if spec else 288) * 10**9
+        self._cus = spec.compute_units if spec else 256
+        self._xcds = spec.xcds if spec else 8
         self._lock = threading.Lock()
-        self._gpus = [_FakeGpu(GpuInfo(i, f"GPU-fake-{i:04x}", f"0000:{0x05 + i * 0x10:02x}:00.0", self.model,
-                                       mem, cus, xcds)) for i in range(self.n_gpus)]
+        self._gpus = [_FakeGpu(i, f"GPU-fake-{i:04x}", f"0000:{0x05 + i * 0x10:02x}:00.0") for i in range(n_gpus)]
         self.set_calls: List[tuple] = []
         self.reenumerations = 0
 
-    def list_gpus(self) -> List[GpuInfo]:
-        return [g.info for g in self._gpus]
+    # -- hooks ---------------------------------------------------------------------------------
+    def _processors(self, reinit: bool) -> List[ProcInfo]:
+        out: List[ProcInfo] = []
+        with self._lock:
+            for g in self._gpus:
+                n = COMPUTE_MODES[g.compute.lower()]
+                nps = _nps(g.memory)
+                for k in range(n):
+                    o = len(out)
+                    uuid = g.uuid if k == 0 else f"{g.uuid}-{g.compute.lower()}{k}"
+                    bus = int(g.bdf.split(":")[1], 16)
+                    out.append(ProcInfo(o, uuid, g.bdf, bdf_id=(k << 28) | (bus << 8), partition_id=k,
+                                        kfd_node=o + 1, hip_id=o, hip_uuid=f"GPU-{g.index:02x}{k:02x}{o:012x}",
+                                        render_minor=128 + o, market_name=self.model,
+                                        vram_bytes=self._mem // nps, cu_count=self._cus // n,
+                                        xcds=self._xcds // n))
+        return out
 
     def _gpu(self, index: int) -> _FakeGpu:
         if not 0 <= index < len(self._gpus):
             raise GpuError(f"GPU {index} not found", GpuError.NOT_FOUND)
         return self._gpus[index]
 
-    def get_compute_partition(self, index: int) -> str:
-        return self._gpu(index).compute
+    def _gpu_of(self, proc: ProcInfo) -> _FakeGpu:
+        for g in self._gpus:
+            if g.bdf == proc.bdf:
+                return g
+        raise GpuError(f"processor {proc.uuid} not found", GpuError.NOT_FOUND)
+
+    def _compute_partition(self, proc: ProcInfo) -> str:
+        return self._gpu_of(proc).compute
+
+    def _memory_partition(self, proc: ProcInfo) -> str:
+        return self._gpu_of(proc).memory
 
     def _check_set(self, index: Optional[int]) -> None:
         if not self.is_root:
@@ -158,35 +270,27 @@ class FakeAmdSmi(AmdSmi):
             raise GpuError(f"amdsmi: injected failure on GPU {index}", GpuError.GENERIC)
         if index is not None and index in self.fail_set:
             raise GpuError(f"amdsmi: injected failure on GPU {index}", GpuError.GENERIC)
-        if index is not None and (index in self.busy or self._gpu(index).processes > 0):
+        if index is not None and (index in self.busy or sum(self._gpu(index).processes.values()) > 0):
             raise GpuError(f"amdsmi: GPU {index} is busy", GpuError.BUSY)
 
-    def set_compute_partition(self, index: int, mode: str) -> None:
-        mode = mode.upper()
-        if mode not in COMPUTE_MODE_NAMES:
-            raise GpuError(f"invalid compute partition {mode!r}")
+    def _set_compute_partition(self, proc: ProcInfo, mode: str) -> None:
         with self._lock:
-            self._check_set(index)
-            g = self._gpu(index)
-            nps = MEMORY_MODES[g.memory.lower()]
-            if COMPUTE_MODES[mode.lower()] < nps:
+            g = self._gpu_of(proc)
+            self._check_set(g.index)
+            if COMPUTE_MODES[mode.lower()] < _nps(g.memory):
                 raise GpuError(f"compute partition {mode} is incompatible with memory partition {g.memory}")
             g.compute = mode
-            self.set_calls.append(("compute", index, mode))
+            g.processes.clear()
+            self.set_calls.append(("compute", g.index, mode))
             self.reenumerations += 1
 
-    def get_memory_partition(self, index: int) -> str:
-        return self._gpu(index).memory
-
-    def set_memory_partition(self, mode: str) -> None:
-        mode = mode.upper()
-        if mode not in MEMORY_MODE_NAMES:
-            raise GpuError(f"invalid memory partition {mode!r}")
+    def _set_memory_partition(self, proc: ProcInfo, mode: str) -> None:
         with self._lock:
             self._check_set(None)
-            if self.memory_mode_requires_idle and any(g.processes > 0 or g.info.index in self.busy for g in self._gpus):
+            if self.memory_mode_requires_idle and any(sum(g.processes.values()) > 0 or g.index in self.busy
+                                                      for g in self._gpus):
                 raise GpuError("amdsmi: memory partition change needs every GPU of the node idle", GpuError.BUSY)
-            nps = MEMORY_MODES[mode.lower()]
+            nps = _nps(mode)
             for g in self._gpus:
                 g.memory = mode
                 if COMPUTE_MODES[g.compute.lower()] < nps:
@@ -194,25 +298,41 @@ class FakeAmdSmi(AmdSmi):
             self.set_calls.append(("memory", None, mode))
             self.reenumerations += 1
 
-    def process_count(self, index: int) -> int:
-        return self._gpu(index).processes
+    def _process_count(self, proc: ProcInfo) -> int:
+        g = self._gpu_of(proc)
+        return g.processes.get(proc.partition_id if proc.partition_id != NO_PARTITION else 0, 0)
 
-    def set_processes(self, index: int, n: int) -> None:
-        self._gpu(index).processes = n
+    def _activity(self, proc: ProcInfo) -> Dict[str, float]:
+        return {"gfx": 100.0 if self._process_count(proc) else 0.0, "umc": 0.0, "mm": 0.0}
 
-    def activity(self, index: int) -> Dict[str, float]:
-        g = self._gpu(index)
-        return {"gfx": 100.0 if g.processes else 0.0, "umc": 0.0, "mm": 0.0}
+    def _vram_usage(self, proc: ProcInfo) -> Dict[str, int]:
+        return {"total": proc.vram_bytes, "used": 0}
 
-    def vram_usage(self, index: int) -> Dict[str, int]:
-        g = self._gpu(index)
-        return {"total": g.info.vram_bytes, "used": 0}
+    # -- test helpers -----------------------------------------------------------------------------
+    def set_processes(self, index: int, n: int, partition: int = 0) -> None:
+        """Pretend ``n`` processes hold partition ``partition`` of GPU ``index``."""
+        with self._lock:
+            g = self._gpu(index)
+            if n:
+                g.processes[partition] = n
+            else:
+                g.processes.pop(partition, None)
+
+    def attach(self, device_id: str, n: int = 1) -> None:
+        """Pretend ``n`` more processes opened the partition behind ``device_id``."""
+        d = self.resolve(device_id)
+        with self._lock:
+            g = self._gpus[d.gpu_index]
+            g.processes[d.partition_index] = g.processes.get(d.partition_index, 0) + n
 
 
 # ------------------------------------------------------------------------------------------
-class _CInfo(ctypes.Structure):
-    _fields_ = [("index", ctypes.c_uint32), ("uuid", ctypes.c_char * 64), ("bdf", ctypes.c_char * 32),
-                ("market_name", ctypes.c_char * 64), ("vram_bytes", ctypes.c_uint64), ("cu_count", ctypes.c_uint32),
+class _CProc(ctypes.Structure):
+    _fields_ = [("ordinal", ctypes.c_uint32), ("uuid", ctypes.c_char * 64), ("bdf", ctypes.c_char * 32),
+                ("market_name", ctypes.c_char * 64), ("hip_uuid", ctypes.c_char * 64),
+                ("bdf_id", ctypes.c_uint64), ("kfd_id", ctypes.c_uint64), ("vram_bytes", ctypes.c_uint64),
+                ("partition_id", ctypes.c_uint32), ("kfd_node", ctypes.c_int32), ("hip_id", ctypes.c_int32),
+                ("hsa_id", ctypes.c_int32), ("render_minor", ctypes.c_int32), ("cu_count", ctypes.c_uint32),
                 ("xcds", ctypes.c_uint32)]
 
 
@@ -222,9 +342,11 @@ def native_library_path() -> str:
 
 
 class NativeAmdSmi(AmdSmi):
-    """ctypes binding to ``libnos_amdsmi.so`` (one amd-smi session per process)."""
+    """ctypes binding to ``libnos_amdsmi.so``.  One session per process, re-initialised by every
+    re-enumeration (processor handles are invalid after a compute/memory partition change)."""
 
     def __init__(self, lib_path: Optional[str] = None):
+        super().__init__()
         path = lib_path or native_library_path()
         if not os.path.exists(path):
             raise GpuError(f"native amd-smi backend not built: {path} (run __graft_entry__.build())")
@@ -232,8 +354,8 @@ class NativeAmdSmi(AmdSmi):
         L = self._lib
         L.nos_smi_init.restype = ctypes.c_int
         L.nos_smi_last_error.restype = ctypes.c_char_p
-        L.nos_smi_gpu_count.restype = ctypes.c_int
-        L.nos_smi_gpu_info.argtypes = [ctypes.c_uint32, ctypes.POINTER(_CInfo)]
+        L.nos_smi_enumerate.argtypes = [ctypes.c_int]
+        L.nos_smi_proc_info.argtypes = [ctypes.c_uint32, ctypes.POINTER(_CProc)]
         L.nos_smi_get_compute_partition.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
         L.nos_smi_set_compute_partition.argtypes = [ctypes.c_uint32, ctypes.c_char_p]
         L.nos_smi_get_memory_partition.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
@@ -241,10 +363,10 @@ class NativeAmdSmi(AmdSmi):
         L.nos_smi_process_count.argtypes = [ctypes.c_uint32]
         L.nos_smi_activity.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.nos_smi_vram.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        self._lock = threading.Lock()
         rc = L.nos_smi_init()
         if rc != 0:
             raise GpuError(f"amdsmi init failed: {self._err()}")
-        self._lock = threading.Lock()
 
     def _err(self) -> str:
         e = self._lib.nos_smi_last_error()
@@ -253,63 +375,61 @@ class NativeAmdSmi(AmdSmi):
     def _check(self, rc: int, what: str) -> None:
         if rc == 0:
             return
-        code = GpuError.GENERIC
-        if rc == 2:
-            code = GpuError.PERMISSION
-        elif rc == 3:
-            code = GpuError.NOT_FOUND
-        elif rc == 4:
-            code = GpuError.BUSY
+        code = {2: GpuError.PERMISSION, 3: GpuError.NOT_FOUND, 4: GpuError.BUSY}.get(rc, GpuError.GENERIC)
         raise GpuError(f"{what}: {self._err()}", code)
 
-    def list_gpus(self) -> List[GpuInfo]:
+    def _processors(self, reinit: bool) -> List[ProcInfo]:
         out = []
         with self._lock:
-            n = self._lib.nos_smi_gpu_count()
-            for i in range(max(0, n)):
-                c = _CInfo()
-                self._check(self._lib.nos_smi_gpu_info(i, ctypes.byref(c)), "gpu info")
-                out.append(GpuInfo(c.index, c.uuid.decode(), c.bdf.decode(), c.market_name.decode(),
-                                   c.vram_bytes, c.cu_count, c.xcds or 8))
+            n = self._lib.nos_smi_enumerate(1 if reinit else 0)
+            if n < 0:
+                raise GpuError(f"amdsmi enumerate: {self._err()}")
+            for i in range(n):
+                c = _CProc()
+                self._check(self._lib.nos_smi_proc_info(i, ctypes.byref(c)), "processor info")
+                out.append(ProcInfo(i, c.uuid.decode(), c.bdf.decode(), c.bdf_id, c.partition_id, c.kfd_node,
+                                    c.hip_id, c.hip_uuid.decode(), c.render_minor, c.market_name.decode(),
+                                    c.vram_bytes, c.cu_count, c.xcds))
         return out
 
-    def _get_str(self, fn, index: int) -> str:
+    def _get_str(self, fn, proc: ProcInfo) -> str:
         buf = ctypes.create_string_buffer(64)
         with self._lock:
-            self._check(fn(index, buf, 64), "partition query")
+            self._check(fn(proc.ordinal, buf, 64), "partition query")
         return buf.value.decode().upper()
 
-    def get_compute_partition(self, index: int) -> str:
-        return self._get_str(self._lib.nos_smi_get_compute_partition, index)
+    def _compute_partition(self, proc: ProcInfo) -> str:
+        return self._get_str(self._lib.nos_smi_get_compute_partition, proc)
 
-    def get_memory_partition(self, index: int) -> str:
-        return self._get_str(self._lib.nos_smi_get_memory_partition, index)
+    def _memory_partition(self, proc: ProcInfo) -> str:
+        return self._get_str(self._lib.nos_smi_get_memory_partition, proc)
 
-    def set_compute_partition(self, index: int, mode: str) -> None:
+    def _set_compute_partition(self, proc: ProcInfo, mode: str) -> None:
         with self._lock:
-            self._check(self._lib.nos_smi_set_compute_partition(index, mode.upper().encode()), "set compute partition")
+            self._check(self._lib.nos_smi_set_compute_partition(proc.ordinal, mode.encode()), "set compute partition")
 
-    def set_memory_partition(self, mode: str) -> None:
+    def _set_memory_partition(self, proc: ProcInfo, mode: str) -> None:
         with self._lock:
-            self._check(self._lib.nos_smi_set_memory_partition(0, mode.upper().encode()), "set memory partition")
+            self._check(self._lib.nos_smi_set_memory_partition(proc.ordinal, mode.encode()), "set memory partition")
 
-    def process_count(self, index: int) -> int:
+    def _process_count(self, proc: ProcInfo) -> int:
         with self._lock:
-            n = self._lib.nos_smi_process_count(index)
+            n = self._lib.nos_smi_process_count(proc.ordinal)
         if n < 0:
             raise GpuError(f"process list: {self._err()}")
         return n
 
-    def activity(self, index: int) -> Dict[str, float]:
+    def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         with self._lock:
-            self._check(self._lib.nos_smi_activity(index, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "activity")
+            self._check(self._lib.nos_smi_activity(proc.ordinal, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
+                        "activity")
         return {"gfx": float(a.value), "umc": float(b.value), "mm": float(c.value)}
 
-    def vram_usage(self, index: int) -> Dict[str, int]:
+    def _vram_usage(self, proc: ProcInfo) -> Dict[str, int]:
         t, u = ctypes.c_uint64(), ctypes.c_uint64()
         with self._lock:
-            self._check(self._lib.nos_smi_vram(index, ctypes.byref(t), ctypes.byref(u)), "vram")
+            self._check(self._lib.nos_smi_vram(proc.ordinal, ctypes.byref(t), ctypes.byref(u)), "vram")
         return {"total": t.value, "used": u.value}
 
     def close(self) -> None:

@@ -2,7 +2,10 @@
 
 ``get_partition_devices`` = used devices (kubelet ``List``) ∪ (allocatable − used, marked free)
 restricted to ``amd.com/<mode>_<nps>`` resources, each resolved to its physical GPU index through
-amd-smi (a device whose GPU cannot be resolved is skipped, like the reference's NotFound path).
+the node's device map (``device/topology.py``: partition UUID, HIP UUID, render node or BDF ->
+logical partition -> physical GPU).  A device the current map does not know — typically a
+partition of the layout before a flip, still advertised until the device plugin re-registers — is
+skipped, like the reference's NotFound path (``pkg/gpu/mig/client.go:141-174``).
 
 Applying a geometry is a *mode flip* per physical GPU (``set_compute_partition``) — there are no
 per-instance create/delete calls and no placement-order search on MI355X.
@@ -55,11 +58,12 @@ class PartitionClient:
             raise
 
     def current_profiles(self) -> Dict[int, str]:
-        """Physical GPU index -> current profile name (``<mode>_<nps>``) as reported by amd-smi."""
-        out = {}
-        for g in self.smi.list_gpus():
-            out[g.index] = f"{self.smi.get_compute_partition(g.index).lower()}_{self.smi.get_memory_partition(g.index).lower()}"
-        return out
+        """Physical GPU index -> current profile name (``<mode>_<nps>``) from the device map."""
+        return self.smi.device_map().modes()
+
+    def device_map(self):
+        """The node's current physical <-> logical map (rebuilt by the backend after every flip)."""
+        return self.smi.device_map()
 
     def set_profile(self, gpu_index: int, profile: str) -> None:
         """Flip one physical GPU to ``profile``'s compute mode (its NPS must already match)."""
@@ -79,6 +83,7 @@ class PartitionClient:
         REGISTRY.phase_seconds.labels(phase="amdsmi_apply").observe(time.perf_counter() - t0)
 
     def gpu_busy(self, gpu_index: int) -> bool:
+        """Any process on any partition of the GPU (amd-smi process list)."""
         return self.smi.process_count(gpu_index) > 0
 
 

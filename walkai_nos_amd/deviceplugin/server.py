@@ -12,8 +12,11 @@ upstream plugin knows — are served by this plugin:
 * ``Allocate`` returns, for the allocated slice, ``HSA_CU_MASK`` (its XCD-symmetric CU rows, or the
   shared pool for memory-only slices), ``NOS_HBM_LIMIT_BYTES`` + ``LD_PRELOAD`` of the HBM-budget
   shim, and the ``/dev/kfd`` + render-node device specs of its GPU;
-* ``GetPreferredAllocation`` packs partition requests onto the GPU with the most partitions in use
-  (keeps whole GPUs idle so they can change mode).
+* ``GetPreferredAllocation`` keeps a request on **one GPU** (a container's ``HSA_CU_MASK`` and HBM
+  budget describe one device), choosing, among the GPUs that can serve all of it, the one with
+  the most slices already in use (packing keeps other GPUs idle so they can be re-sliced);
+* ``Allocate`` rejects a request whose slices span GPUs instead of merging CU ids of different
+  GPUs into one mask.
 """
 from __future__ import annotations
 
@@ -36,6 +39,32 @@ log = logging.getLogger("nos.deviceplugin")
 
 DEVICE_PLUGIN_DIR = "/var/lib/kubelet/device-plugins"
 KUBELET_SOCKET = os.path.join(DEVICE_PLUGIN_DIR, "kubelet.sock")
+
+
+def preferred_same_gpu(must: List[str], available: List[str], size: int, gpu_of: Dict[str, int],
+                       total: Dict[int, int]) -> List[str]:
+    """``size`` ids including ``must``, all on one GPU when any GPU can serve the request: the GPU
+    of the must-include ids if there are any, else the GPU with the most slices in use (``total``
+    advertised minus available), ties to the lower index; within it, ids in sorted order.  When no
+    single GPU has enough, fall back to sorted first-fit (``Allocate`` will then refuse)."""
+    avail_by_gpu: Dict[int, List[str]] = {}
+    for i in sorted(available):
+        avail_by_gpu.setdefault(gpu_of.get(i, -1), []).append(i)
+    must_gpus = {gpu_of.get(i, -1) for i in must}
+    cands = sorted(avail_by_gpu, key=lambda g: (-(total.get(g, 0) - len(avail_by_gpu[g])), g))
+    if must_gpus:
+        cands = [g for g in cands if g in must_gpus] if len(must_gpus) == 1 else []
+    for g in cands:
+        pick = list(must) + [i for i in avail_by_gpu[g] if i not in must]
+        if len(pick) >= size:
+            return pick[:size]
+    ids = list(must)
+    for i in sorted(available):
+        if len(ids) >= size:
+            break
+        if i not in ids:
+            ids.append(i)
+    return ids
 
 
 class SliceDevicePlugin:
@@ -81,14 +110,14 @@ class SliceDevicePlugin:
                 self._changed.wait(self.poll_interval)
 
     def GetPreferredAllocation(self, req, ctx):
+        gpu_of = {s.id: g for g, ss in self.store.load().items() for s in ss}
+        total: Dict[int, int] = {}
+        for i in self.devices():
+            total[gpu_of.get(i, -1)] = total.get(gpu_of.get(i, -1), 0) + 1
         resp = dp.PreferredAllocationResponse()
         for cr in req.container_requests:
-            ids = list(cr.must_include_deviceIDs)
-            for i in sorted(cr.available_deviceIDs):
-                if len(ids) >= cr.allocation_size:
-                    break
-                if i not in ids:
-                    ids.append(i)
+            ids = preferred_same_gpu(list(cr.must_include_deviceIDs), list(cr.available_deviceIDs),
+                                     int(cr.allocation_size), gpu_of, total)
             resp.container_responses.add(deviceIDs=ids)
         return resp
 
@@ -108,6 +137,11 @@ class SliceDevicePlugin:
                     raise KeyError(did)
                 g, s = by_id[did]
                 gpus.add(g)
+                if len(gpus) > 1:
+                    msg = f"slices {list(cr.devicesIDs)} span GPUs {sorted(gpus)}: one container's CU mask and HBM budget cover one GPU"
+                    if ctx is not None:
+                        ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, msg)
+                    raise ValueError(msg)
                 cus.extend(cus_of(s, slices[g], self.cu_count))
                 hbm += s.hbm_bytes
             car.envs[constant.ENV_HSA_CU_MASK] = hsa_cu_mask(cus, 0)

@@ -60,6 +60,12 @@ class LocalBarrier(CommitBarrier):
             while gen not in self._result:
                 rem = end - time.monotonic()
                 if rem <= 0:
+                    # close the generation: every voter of it (and any late one) sees False, and
+                    # the next round starts clean instead of being completed by a stale vote
+                    self._result[gen] = False
+                    self._votes = []
+                    self._gen += 1
+                    self._cv.notify_all()
                     return False
                 self._cv.wait(rem)
             return self._result[gen]

@@ -1,0 +1,130 @@
+"""Agent-side handles for the spawned GPU helper (``walkai_nos_amd/cmd/gpuhelper.py``).
+
+The node agents never touch the GPU through HIP themselves; they start the helper as a child
+process (``subprocess``: fork + exec of a fresh interpreter, before anything in the agent has
+initialised a GPU) and read its one JSON line.  Running helpers are registered in a
+:class:`HelperRegistry` so the actuator can stop them before a mode flip — a helper still probing
+the old partitions would hold KFD contexts and make the flip fail with "busy".
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import subprocess
+import sys
+import threading
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..utils.metrics import REGISTRY
+from .barrier import CommitBarrier
+
+log = logging.getLogger("nos.gpuhelper")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class HelperRegistry:
+    """Live helper processes of one agent."""
+
+    def __init__(self) -> None:
+        self._lock = threading.Lock()
+        self._procs: List[subprocess.Popen] = []
+
+    def add(self, p: subprocess.Popen) -> None:
+        with self._lock:
+            self._procs.append(p)
+
+    def remove(self, p: subprocess.Popen) -> None:
+        with self._lock:
+            if p in self._procs:
+                self._procs.remove(p)
+
+    def running(self) -> int:
+        with self._lock:
+            return sum(1 for p in self._procs if p.poll() is None)
+
+    def quiesce(self, grace: float = 10.0) -> int:
+        """Terminate every running helper (SIGTERM, then SIGKILL after ``grace``); returns how many."""
+        with self._lock:
+            procs = [p for p in self._procs if p.poll() is None]
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(grace)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        return len(procs)
+
+
+DEFAULT_REGISTRY = HelperRegistry()
+
+
+def run_helper(args: Sequence[str], timeout: float = 180.0, registry: Optional[HelperRegistry] = None) -> Dict[str, Any]:
+    """Run ``python -m walkai_nos_amd.cmd.gpuhelper <args>`` and return its JSON line."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    reg = registry or DEFAULT_REGISTRY
+    p = subprocess.Popen([sys.executable, "-m", "walkai_nos_amd.cmd.gpuhelper", *args], cwd=ROOT, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    reg.add(p)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, err = p.communicate()
+        raise TimeoutError(f"gpu helper {args[0]} timed out after {timeout}s")
+    finally:
+        reg.remove(p)
+    line = next((ln for ln in reversed(out.splitlines()) if ln.startswith("{")), None)
+    if p.returncode != 0 or line is None:
+        raise RuntimeError(f"gpu helper {args[0]} failed (rc={p.returncode}): {err.strip()[-500:]}")
+    return json.loads(line)
+
+
+class SpawnedNodeBarrier(CommitBarrier):
+    """Node commit barrier over every logical device, run in a fresh helper process.
+
+    One vote per logical device of the re-enumerated device map (HIP ordinal order); the helper
+    must see exactly that many HIP devices, so a partition that did not come up is a veto even if
+    every vote was 1."""
+
+    def __init__(self, n_devices: int, backend: str = "rccl", timeout: float = 180.0,
+                 registry: Optional[HelperRegistry] = None):
+        self.n = n_devices
+        self.backend = backend
+        self.timeout = timeout
+        self.registry = registry
+        self.last: Dict[str, Any] = {}
+
+    def vote_all(self, votes: Sequence[bool]) -> bool:
+        v = [1 if x else 0 for x in votes]
+        t0 = time.perf_counter()
+        try:
+            res = run_helper(["barrier", "--votes", ",".join(map(str, v)), "--expect", str(self.n),
+                              "--backend", self.backend], self.timeout, self.registry)
+        except (RuntimeError, TimeoutError) as e:
+            log.error("commit barrier helper: %s", e)
+            self.last = {"error": str(e)}
+            return False
+        REGISTRY.phase_seconds.labels(phase="commit_barrier").observe(time.perf_counter() - t0)
+        self.last = res
+        if res.get("error"):
+            log.error("commit barrier: %s", res["error"])
+            return False
+        return len(v) == self.n and int(res.get("sum", -1)) == self.n
+
+    def vote(self, ok: bool) -> bool:
+        return self.vote_all([ok] * self.n)
+
+
+def spawned_probe_round(targets: List[tuple], backend: str = "hip", timeout: float = 300.0,
+                        registry: Optional[HelperRegistry] = None) -> Dict[str, Any]:
+    """Probe every target in one helper process; label -> result (or {"error": ...})."""
+    res = run_helper(["probe", "--targets", json.dumps([list(t) for t in targets]), "--backend", backend],
+                     timeout, registry)
+    return dict(res.get("slices", {}))
