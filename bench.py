@@ -3,8 +3,10 @@
 
 Runs the flagship step (see :mod:`walkai_nos_amd.bench_core`): a node of N MI355X GPUs (one
 process per GPU under torchrun, RCCL over xGMI for the partition-commit barrier) serving a
-churning mix of 1/8, 1/2 and 1/1-GPU YOLOS-small inference pods through the nos control plane.
-Rank 0 prints one JSON line.
+churning mix of 1/8, 1/2 and 1/1-GPU YOLOS-small inference pods through the nos control plane,
+one ``--quantum``-second serving quantum per step, every compute-partition flip charged as a
+``--flip-cost``-second outage of its GPU.  After the timed window a density phase saturates the
+node (8 CPX pods per GPU, then CU-mask slices beyond).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -20,14 +22,20 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--load", type=float, default=1.0, help="offered GPU-equivalents per GPU")
     ap.add_argument("--backend", choices=("hip", "torch"), default="hip")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--preroll", type=int, default=20,
-                    help="control-plane-only churn epochs before warmup, so timing starts in steady state")
+    ap.add_argument("--preroll", type=int, default=60,
+                    help="control-plane-only steps before warmup, so timing starts in steady state")
+    ap.add_argument("--quantum", type=float, default=0.5, help="wall seconds of serving per step")
+    ap.add_argument("--flip-cost", type=float, default=2.0,
+                    help="seconds a GPU serves nothing after a compute-partition flip")
+    ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
+    ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod")
+    ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -51,7 +59,8 @@ def main() -> int:
     from walkai_nos_amd.bench_core import BenchConfig, run_bench
     cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
-                      preroll=args.preroll)
+                      preroll=args.preroll, quantum_s=args.quantum, flip_cost_s=args.flip_cost,
+                      policy=args.policy, depth=args.depth, density=not args.no_density)
     res = run_bench(cfg)
     if rank == 0:
         line = json.dumps(res)

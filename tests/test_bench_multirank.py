@@ -1,7 +1,9 @@
 """The bench's multi-GPU control path on CPU: one process per GPU rank over a gloo process group,
-every rank running the same seeded node simulation with the commit barrier as a real
-``torch.distributed`` all-reduce (the RCCL path of ``bench.py`` under torchrun).  The ranks must
-stay in lock-step (every commit votes on every rank, no hang) and split the node's pods by GPU."""
+every rank running the same seeded node simulation, with the agent's commit path
+(``Actuator._commit`` -> ``RankCommitBarrier.vote_all``) as a real ``torch.distributed``
+all-reduce — the RCCL path of ``bench.py`` under torchrun.  The ranks must stay in lock-step
+(every commit votes on every rank, no hang), split the node's pods by GPU, and a veto from ONE
+rank must roll the plan back on EVERY rank identically."""
 from __future__ import annotations
 
 import multiprocessing as mp
@@ -10,53 +12,78 @@ import socket
 import pytest
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, veto_rank, veto_commits):
     import torch.distributed as dist
 
     from walkai_nos_amd.bench_core import BenchConfig, NodeBench
-    from walkai_nos_amd.parallel.barrier import TorchBarrier
+    from walkai_nos_amd.parallel.barrier import RankCommitBarrier
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         cfg = BenchConfig(gpus=world, steps=6, warmup=1, rank=rank, world=world, preroll=10)
-        votes = []
+        results = []
+        checks = [0]
+
+        def local_check():
+            checks[0] += 1
+            return not (rank == veto_rank and checks[0] <= veto_commits)
 
         def factory(n):
-            b = TorchBarrier()
-            orig = b.vote
+            b = RankCommitBarrier(rank, world, local_check=local_check)
+            orig = b.vote_all
 
-            def vote(ok):
-                r = orig(ok)
-                votes.append(r)
+            def vote_all(votes):
+                r = orig(votes)
+                results.append((r, b.last_local))
                 return r
-            b.vote = vote
+            b.vote_all = vote_all
             return b
         nb = NodeBench(cfg, barrier_factory=factory, gpu_data_plane=False)
-        work = 0
+        served = 0
+        modes = []
         for _ in range(cfg.preroll + cfg.warmup + cfg.steps):
-            work += nb.step()
-        q.put((rank, work, len(votes), all(votes), [round(u, 6) for u in nb.util_samples],
-               len(nb.cluster.running_pods())))
+            nb.control_step()
+            served += len(nb.my_pods())
+            nb.end_step()
+            modes.append(tuple(sorted(nb.sn.smi.device_map().modes().items())))
+        q.put((rank, served, [r for r, _ in results], [loc for _, loc in results],
+               [round(u, 6) for u in nb.util_samples], modes, nb.sn.smi.set_calls))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_bench_control_plane_lockstep_gloo(world):
+def _run(world, veto_rank=-1, veto_commits=0):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, veto_rank, veto_commits)) for r in range(world)]
     [p.start() for p in ps]
     [p.join(240) for p in ps]
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
-    out = sorted(q.get(timeout=10) for _ in range(world))
+    return sorted(q.get(timeout=10) for _ in range(world))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_control_plane_lockstep_gloo(world):
+    out = _run(world)
     # identical control plane on every rank, same number of committed votes, all successful
     assert len({tuple(o[4]) for o in out}) == 1
-    assert len({o[2] for o in out}) == 1 and out[0][2] > 0
-    assert all(o[3] for o in out)
-    # every rank runs only its own GPU's pods; together they cover the node's work
-    assert sum(o[1] for o in out) > 0
+    assert len({len(o[2]) for o in out}) == 1 and len(out[0][2]) > 0
+    assert all(all(o[2]) for o in out)
+    # every rank serves only its own GPU's pods; together they cover the node's work
     assert all(o[1] > 0 for o in out)
+
+
+def test_one_rank_veto_rolls_back_on_every_rank():
+    out = _run(2, veto_rank=1, veto_commits=1)
+    r0, r1 = out
+    # the first commit: rank 1 vetoed locally, so the all-reduce failed on BOTH ranks
+    assert r1[3][0] is False and r0[3][0] is True
+    assert r0[2][0] is False and r1[2][0] is False
+    # both ranks rolled back the same flips and then committed the retry identically
+    assert r0[6] == r1[6]
+    assert any(c[0] == "compute" for c in r0[6])
+    assert r0[5] == r1[5] and r0[2] == r1[2]
+    assert any(r0[2][1:]), "the retried plan must commit once the veto is gone"

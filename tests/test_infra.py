@@ -151,11 +151,19 @@ def test_bench_control_plane_and_slice_masks():
     assert {c % 8 for c in slice_cus("cpx_nps1", 5)} == set(range(8))
     a, b = ChurnProcess(BenchConfig(seed=7)), ChurnProcess(BenchConfig(seed=7))
     assert [a.arrivals() for _ in range(20)] == [b.arrivals() for _ in range(20)]
-    nb = NodeBench(BenchConfig(gpus=2), gpu_data_plane=False)
-    for _ in range(10):
+    nb = NodeBench(BenchConfig(gpus=2, flip_cost_s=1.0, quantum_s=0.5), gpu_data_plane=False)
+    served, dark = 0, 0
+    for _ in range(20):
         nb.control_step()
-        nb.data_step()
-    assert nb.inferences > 0 and max(nb.util_samples) > 0
+        served += len(nb.my_pods())
+        dark += 1 if nb.outage.get(0, 0) > 0 else 0
+        if nb.outage.get(0, 0) > 0:
+            assert nb.my_pods() == []  # a flipped GPU serves nothing during its outage
+        nb.end_step()
+    assert served > 0 and max(nb.util_samples) > 0
+    assert nb.flips > 0 and nb.outage_gpu_steps == 2 * nb.flips or nb.outage_gpu_steps > 0
+    assert BenchConfig(flip_cost_s=2.0, quantum_s=0.5).outage_steps == 4
+    assert BenchConfig(flip_cost_s=0.0).outage_steps == 0
 
 
 def test_split3_cpu_reconstructs_exactly():

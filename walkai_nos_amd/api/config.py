@@ -6,7 +6,7 @@ Field names follow the reference (``pkg/api/nos.nebuly.com/config/v1alpha1/*``,
 * ``GpuPartitionerConfig`` — manager options plus ``batchWindowTimeoutSeconds``,
   ``batchWindowIdleSeconds``, ``knownMigGeometriesFile`` (alias ``knownGeometriesFile``),
   ``schedulerConfigFile``, ``devicePluginConfigMap{name,namespace}``, ``devicePluginDelaySeconds``;
-  MI355X additions ``planningPolicy`` (``fifo``|``batch``) and ``scoring`` (``fraction``|``pods``);
+  MI355X additions ``planningPolicy`` (``pack`` = flip-aware packing, default | ``fifo`` | ``batch`` | ``simulate``) and ``scoring`` (``fraction``|``pods``);
 * ``MigAgentConfig`` (the partition agent; also accepted as ``PartitionAgentConfig``) and
   ``GpuAgentConfig`` (the CU-mask slice agent; also ``SliceAgentConfig``) with
   ``reportConfigIntervalSeconds``;
@@ -69,7 +69,7 @@ class GpuPartitionerConfig(ManagerConfig):
     devicePluginConfigMap: NamespacedObject = field(default_factory=lambda: NamespacedObject(
         constant.DEFAULT_DEVICE_PLUGIN_CONFIGMAP_NAME, constant.DEFAULT_DEVICE_PLUGIN_CONFIGMAP_NAMESPACE))
     devicePluginDelaySeconds: float = 5.0
-    planningPolicy: str = "fifo"
+    planningPolicy: str = "pack"
     scoring: str = "fraction"
 
     def validate(self) -> None:
@@ -80,8 +80,8 @@ class GpuPartitionerConfig(ManagerConfig):
             raise ValueError("batchWindowIdleSeconds must be greater than 0")
         if self.devicePluginDelaySeconds <= 0:
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
-        if self.planningPolicy not in ("fifo", "batch", "simulate"):
-            raise ValueError("planningPolicy must be 'fifo', 'batch' or 'simulate'")
+        if self.planningPolicy not in ("fifo", "batch", "simulate", "pack"):
+            raise ValueError("planningPolicy must be 'fifo', 'batch', 'simulate' or 'pack'")
         if self.scoring not in ("fraction", "pods"):
             raise ValueError("scoring must be 'fraction' or 'pods'")
 

@@ -2,39 +2,46 @@
 
 Headline metric (BASELINE.json): *aggregate GPU utilization % + schedulable pods/node under a
 mixed fractional-GPU load*, on the workload the reference publishes numbers for (YOLOS-small
-batch-1 inference pods, ``demos/gpu-sharing-comparison``).
+batch-1 inference pods, ``demos/gpu-sharing-comparison``).  ``value`` is the aggregate inference
+rate the node sustains; utilisation and pods/node are reported next to it.
 
-One step = one churn epoch of the node:
+One step = one **serving quantum** of ``quantum_s`` wall seconds:
 
-1. pods finish / new pods arrive (deterministic seeded process; fractions 1/8, 1/2 and 1/1 GPU,
-   i.e. ``amd.com/cpx_nps1``, ``amd.com/dpx_nps1``, ``amd.com/spx_nps1``);
-2. the *real* control plane (partitioner pod/node controllers, partition agents with their
-   reporter/actuator handshake, the scheduler) runs to quiescence on the in-memory API server;
-   every partition commit is voted through the node commit barrier, which on a multi-GPU run is
-   a real RCCL all-reduce over xGMI between the GPU ranks;
-3. every running pod on this rank's GPU executes ``8 x fraction`` YOLOS-small inferences (fp32,
-   batch 1, 800x1066) on its partition: a HIP stream whose CU mask is the partition's CU set.
+1. churn: pods whose served lifetime is over finish, new pods arrive (seeded Poisson process;
+   fractions 1/8, 1/2 and 1/1 GPU = ``amd.com/cpx_nps1``, ``dpx_nps1``, ``spx_nps1``);
+2. the *real* control plane (partitioner pod/node controllers with the flip-aware ``pack`` policy,
+   partition agents with their reporter/actuator handshake and commit barrier, the scheduler)
+   runs to quiescence on the in-memory API server;
+3. **every compute-partition flip is charged**: the flipped GPU serves nothing for
+   ``flip_cost_s`` (amd-smi switch + AMD device-plugin re-registration; the reference waits up to
+   a minute for the plugin, ``pkg/gpu/client.go:86-135``; 2 s by default, ``--flip-cost``), pods
+   on it neither serve nor age during the outage, and the GPU counts as unallocated;
+4. until the quantum ends, every running pod on this rank's GPU keeps its partition busy with
+   YOLOS-small inferences (fp32-accurate, batch 1, 800x1066; a HIP graph replay per inference on
+   a stream whose CU mask is the partition's CU set, ``depth`` inferences in flight per pod).
 
 Because the box is not root, compute-partition modes cannot be flipped on the real device; a
 CPX/QPX/DPX partition is emulated by an XCD-symmetric CU mask of the same CU count (32/64/128
-CUs; the census in ``profiles/`` shows mask bit i -> XCD i mod 8, and an XCD whose mask bits are
-all zero is NOT disabled, so every slice must span all eight XCDs).  Mode changes go through the
-fake amd-smi backend; everything else — kernels, streams, collectives — is real.
+CUs; mask bit i -> XCD i mod 8, and an XCD whose mask bits are all zero is NOT disabled, so every
+slice must span all eight XCDs).  Mode changes go through the fake amd-smi backend (whose device
+map re-enumerates like the real one); everything else — kernels, streams, collectives — is real.
 
-``value`` = aggregate inferences/s over all GPUs of the job (whole-job aggregate, weak scaling:
-per-GPU offered load fixed).  Utilization and pods/node are reported alongside.
+After the timed window a **density** phase saturates the node through the same control plane and
+data plane: 8 CPX pods per GPU (the reference's MIG maximum is 7 per A100), then a CU-mask node
+with dedicated-CU and memory-only slices beyond 8 per GPU.  It is reported, never timed.
 """
 from __future__ import annotations
 
+import collections
 import json
 import math
 import os
 import random
+import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Tuple
 
-from .api import v1alpha1 as api
 from .kube import objects as ko
 from .models.xcp.profile import COMPUTE_MODES, extract_profile_name
 
@@ -44,32 +51,41 @@ BASELINE_LABEL = "MPS 7-pod aggregate throughput on 1x A100-80GB (BASELINE.md), 
 
 MIX = (("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2))
 
+#: CU-mask density phase: dedicated-CU slices plus memory-only slices on the shared rows
+CUMASK_DENSITY = (("32cu.24gb", 6), ("8gb", 10))
+
 
 @dataclass
 class BenchConfig:
     gpus: int = 1
-    steps: int = 10
-    warmup: int = 2
+    steps: int = 20
+    warmup: int = 5
     seed: int = 1234
-    offered_load: float = 1.0           # offered GPU-equivalents per GPU (= capacity)
-    lifetime: Tuple[int, int] = (2, 6)  # steps
+    offered_load: float = 1.0            # offered GPU-equivalents per GPU (= capacity)
+    quantum_s: float = 0.5               # wall seconds of serving per step
+    flip_cost_s: float = 2.0             # outage of a GPU per compute-partition flip
+    lifetime: Tuple[int, int] = (8, 24)  # served quanta per pod
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"
     graphs: bool = True
-    preroll: int = 20                   # control-plane-only epochs before warmup (steady state)
+    depth: int = 2                       # inferences in flight per pod
+    preroll: int = 60                    # control-plane-only steps before warmup (steady state)
     rank: int = 0
     world: int = 1
-    policy: str = "fifo"                # planner policy (fifo | batch | simulate)
+    policy: str = "pack"                 # planner policy (pack | fifo | batch | simulate)
+    density: bool = True
+
+    @property
+    def outage_steps(self) -> int:
+        return int(math.ceil(self.flip_cost_s / self.quantum_s - 1e-9)) if self.flip_cost_s > 0 else 0
 
 
 class ChurnProcess:
-    """Deterministic pod arrival/departure process (identical on every rank)."""
+    """Deterministic pod arrival process (identical on every rank)."""
 
     def __init__(self, cfg: BenchConfig):
         self.cfg = cfg
         self.rng = random.Random(cfg.seed)
-        self.t = 0
-        self.live: Dict[str, int] = {}  # pod name -> remaining steps once running
         self.seq = 0
         mean_frac = sum((1.0 / COMPUTE_MODES[p.split("_")[0]]) * w for p, w in MIX)
         mean_life = (cfg.lifetime[0] + cfg.lifetime[1]) / 2
@@ -110,29 +126,30 @@ def slice_cus(profile: str, partition: int, total_cus: int = 256) -> Optional[Li
 
 
 class Slot:
-    """One partition of this rank's GPU: a CU-masked stream, a model replica and an input."""
+    """One partition (or CU-mask slice) of this rank's GPU: a CU-masked stream, a model replica
+    and an input; an inference is one HIP graph replay."""
 
-    def __init__(self, profile: str, partition: int, device: int, cfg: BenchConfig, template: Any):
+    def __init__(self, cus: Optional[List[int]], device: int, cfg: BenchConfig, template: Any, seed: int = 0):
         import copy
 
         import torch
 
         from .ops.probe import Stream
 
-        self.profile, self.partition = profile, partition
-        self.hip_stream = Stream(device, slice_cus(profile, partition))
+        self.cus = cus
+        self.hip_stream = Stream(device, cus)
         self.stream = self.hip_stream.torch_stream()
         with torch.cuda.stream(self.stream):
             self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
             from .models.workload.yolos import demo_input
-            self.x = demo_input(1, cfg.hw, f"cuda:{device}", seed=partition)
+            self.x = demo_input(1, cfg.hw, f"cuda:{device}", seed=seed)
         self.graph = None
         self.cfg = cfg
+        self.inflight: collections.deque = collections.deque()
 
     @property
     def n_cus(self) -> int:
-        cus = slice_cus(self.profile, self.partition)
-        return 256 if cus is None else len(cus)
+        return 256 if self.cus is None else len(self.cus)
 
     def warm(self) -> None:
         import torch
@@ -151,14 +168,31 @@ class Slot:
             self.stream.synchronize()
             self.graph = g
 
-    def mark(self) -> Any:
-        """Event at the current tail of this slot's stream."""
+    def submit(self) -> None:
+        """Enqueue one inference and an event marking its end."""
         import torch
-        ev = torch.cuda.Event()
-        ev.record(self.stream)
-        return ev
+
+        from .ops import kernels as K
+        K.set_slice_cus(self.n_cus)
+        with torch.no_grad(), torch.cuda.stream(self.stream):
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self.out = self.model(self.x)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.inflight.append(ev)
+
+    def reap(self) -> None:
+        while self.inflight and self.inflight[0].query():
+            self.inflight.popleft()
+
+    def drain(self) -> None:
+        while self.inflight:
+            self.inflight.popleft().synchronize()
 
     def close(self) -> None:
+        self.inflight.clear()
         self.graph = None
         self.model = None
         self.x = None
@@ -168,160 +202,83 @@ class Slot:
             self.hip_stream.close()
             self.hip_stream = None
 
-    def run(self, n: int) -> None:
+
+class DataPlane:
+    """This rank's GPU: one slot per partition of every compute mode (15 model replicas)."""
+
+    def __init__(self, cfg: BenchConfig):
         import torch
 
+        from .models.workload.yolos import YolosSmall
         from .ops import kernels as K
-        K.set_slice_cus(self.n_cus)
-        with torch.no_grad(), torch.cuda.stream(self.stream):
-            for _ in range(n):
-                if self.graph is not None:
-                    self.graph.replay()
-                else:
-                    self.out = self.model(self.x)
-
-
-class NodeBench:
-    """The simulated node + this rank's GPU data plane."""
-
-    def __init__(self, cfg: BenchConfig, barrier_factory=None, gpu_data_plane: bool = True):
-        from .sim.cluster import SimCluster
-
+        K.set_backend(cfg.backend)
         self.cfg = cfg
-        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
-        if barrier_factory is not None:
-            for sn in self.cluster.nodes.values():
-                self._set_barrier(sn, barrier_factory)
-        self.churn = ChurnProcess(cfg)
-        self.cluster.run(30)  # node initialisation (SPX everywhere)
-        self.inferences = 0
-        self.util_samples: List[float] = []
-        self.pods_samples: List[int] = []
-        self.pending_samples: List[int] = []
-        self.slots: Dict[Tuple[str, int], Slot] = {}
-        self._inflight: List[List[Any]] = []  # completion events of the enqueued epochs, oldest first
-        self._mode: frozenset = frozenset()   # compute modes of this GPU's pods in the last epoch
-        self.mode_drains = 0                  # epochs that had to drain the GPU (its mode changed)
-        self.empty_epochs = 0                 # epochs with no pod on this rank's GPU
-        # host-side time split of the timed steps: control plane / waiting for the GPU / enqueue
-        self.host_s = {"control": 0.0, "wait": 0.0, "enqueue": 0.0}
-        self.gpu = gpu_data_plane
-        if self.gpu:
-            import torch
+        self.device = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(self.device)
+        self.template = YolosSmall()
+        self.slots: Dict[Any, Slot] = {}
+        for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
+            for k in range(n):
+                self.slots[(prof, k)] = Slot(slice_cus(prof, k), self.device, cfg, self.template, seed=k)
+        for s in self.slots.values():
+            s.warm()
+        torch.cuda.synchronize()
+        self._layout: frozenset = frozenset()
+        self.drains = 0
 
-            from .models.workload.yolos import YolosSmall
-            from .ops import kernels as K
-            K.set_backend(cfg.backend)
-            self.device = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(self.device)
-            template = YolosSmall()
-            for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
-                for k in range(n):
-                    self.slots[(prof, k)] = Slot(prof, k, self.device, cfg, template)
-            for s in self.slots.values():
+    def add_slots(self, slots: Dict[Any, List[int]]) -> None:
+        import torch
+        for key, cus in slots.items():
+            if key not in self.slots:
+                s = Slot(cus, self.device, self.cfg, self.template, seed=len(self.slots))
                 s.warm()
-            torch.cuda.synchronize()
+                self.slots[key] = s
+        torch.cuda.synchronize()
 
-    @staticmethod
-    def _set_barrier(sn: Any, factory: Any) -> None:
-        for c in sn.manager.controllers:
-            actuator = getattr(c.reconciler, "__self__", None)
-            if actuator is not None and hasattr(actuator, "barrier_factory"):
-                actuator.barrier_factory = factory
+    def drain_all(self) -> None:
+        for s in self.slots.values():
+            s.drain()
 
-    # -- one epoch ------------------------------------------------------------------------
-    def control_step(self) -> None:
-        t0 = time.perf_counter()
-        self._control_step()
-        self.host_s["control"] += time.perf_counter() - t0
+    def serve(self, keys: List[Any], deadline: float) -> int:
+        """Keep every listed slot busy until ``deadline``; returns the inferences enqueued.
 
-    def _control_step(self) -> None:
-        c = self.cluster
-        for name in list(self.churn.live):
-            self.churn.live[name] -= 1
-            if self.churn.live[name] <= 0:
-                del self.churn.live[name]
-                c.complete(name)
-                c.delete_pod(name)  # the owning controller garbage-collects finished pods
-        for prof in self.churn.arrivals():
-            c.submit({f"amd.com/{prof}": 1}, name=f"p{self.churn.seq}")
-            self.churn.seq += 1
-        c.run(60)
-        for p in c.running_pods():
-            n = ko.name(p)
-            if n not in self.churn.live:
-                self.churn.live[n] = self.churn.lifetime()
-        self.util_samples.append(c.utilization())
-        self.pods_samples.append(len(c.running_pods()))
-        self.pending_samples.append(len(c.pending_pods()))
-
-    def my_pods(self) -> List[Tuple[str, int, int]]:
-        """(profile, partition index, inferences this step) for pods on this rank's GPU."""
-        sn = next(iter(self.cluster.nodes.values()))
-        out = []
-        for devs in sn.kubelet.allocations.values():
-            for r, dev_id in devs:
-                prof = extract_profile_name(r)
-                if prof is None:
-                    continue
-                d = sn.smi.resolve(dev_id)
-                if d.gpu_index != self.cfg.rank:
-                    continue
-                part = d.partition_index
-                out.append((prof, part, 8 // COMPUTE_MODES[prof.split("_")[0]]))
-        return out
-
-    def data_step(self) -> int:
-        """Enqueue this epoch's inferences on the partitions' streams.
-
-        While this GPU keeps its compute mode, the pods' partitions are unchanged and their streams
-        simply run on: the epoch is queued behind the previous one (at most two epochs in flight,
-        so the host never runs far ahead), as pods on real partitions keep serving while the
-        control plane works. When the mode changes (a flip re-partitions the GPU, which the agent
-        only does on an idle GPU), every queued inference of the old layout must finish first, so
-        the slots of two layouts never run side by side. (Queueing every epoch behind GPU-side
-        stream waits instead measured slower: 243 vs 284 inf/s.)"""
-        t0 = time.perf_counter()
-        pods = self.my_pods()
-        mode = frozenset(prof.split("_")[0] for prof, _, _ in pods)
-        if self.gpu:
-            keep = 1 if mode == self._mode else 0
-            if not keep and self._inflight:
-                self.mode_drains += 1
-            while len(self._inflight) > keep:
-                for ev in self._inflight.pop(0):
-                    ev.synchronize()
-        self._mode = mode
-        t1 = time.perf_counter()
+        A different set of compute modes than in the last quantum means the GPU was re-partitioned:
+        every queued inference of the old layout finishes first (the agent only flips an idle GPU),
+        so slots of two layouts never overlap."""
+        layout = frozenset(k[0] for k in keys)
+        if layout != self._layout:
+            if any(s.inflight for s in self.slots.values()):
+                self.drains += 1
+            self.drain_all()
+            self._layout = layout
+        active = [self.slots[k] for k in keys]
         n = 0
-        marks = []
-        for prof, part, work in pods:
-            if self.gpu:
-                slot = self.slots[(prof, part)]
-                slot.run(work)
-                marks.append(slot.mark())
-            n += work
-        if self.gpu:
-            self._inflight.append(marks)
-        if n == 0:
-            self.empty_epochs += 1
-        self.inferences += n
-        self.host_s["wait"] += t1 - t0
-        self.host_s["enqueue"] += time.perf_counter() - t1
+        depth = self.cfg.depth
+        while True:
+            now = time.perf_counter()
+            if now >= deadline:
+                break
+            if not active:
+                time.sleep(deadline - now)
+                break
+            progressed = False
+            for s in active:
+                s.reap()
+                if len(s.inflight) < depth:
+                    s.submit()
+                    n += 1
+                    progressed = True
+            if not progressed:
+                time.sleep(0.0002)
         return n
-
-    def step(self) -> int:
-        self.control_step()
-        return self.data_step()
 
     def close(self) -> None:
         """Release graphs, model replicas and CU-masked streams before interpreter teardown (a
         graph destroyed after the HIP runtime has been finalised crashes the process at exit)."""
-        if not self.gpu:
-            return
         import gc
 
         import torch
+        self.drain_all()
         torch.cuda.synchronize()
         for s in self.slots.values():
             s.graph = None
@@ -334,53 +291,283 @@ class NodeBench:
         gc.collect()
 
 
+class HwBusySampler:
+    """amd-smi gfx activity of this rank's GPU, sampled on a thread during the timed window (the
+    bench process may use amd-smi; only the partition agent must stay HIP-free)."""
+
+    def __init__(self, hip_device: int, period: float = 0.1):
+        self.samples: List[float] = []
+        self.period = period
+        self._stop = threading.Event()
+        self._t: Optional[threading.Thread] = None
+        self.error = ""
+        try:
+            from .device.amdsmi import NativeAmdSmi
+            self.smi = NativeAmdSmi()
+            devs = [d for d in self.smi.logical_devices() if d.hip_id == hip_device]
+            self.gpu = devs[0].gpu_index if devs else 0
+        except Exception as e:  # noqa: BLE001 - the figure is reported as unavailable
+            self.smi, self.error = None, str(e)[:200]
+
+    def _run(self) -> None:
+        while not self._stop.wait(self.period):
+            try:
+                self.samples.append(self.smi.activity(self.gpu)["gfx"])
+            except Exception as e:  # noqa: BLE001
+                self.error = str(e)[:200]
+                return
+
+    def start(self) -> None:
+        if self.smi is not None:
+            self._t = threading.Thread(target=self._run, name="nos-hw-busy", daemon=True)
+            self._t.start()
+
+    def stop(self) -> Optional[float]:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join()
+        return round(sum(self.samples) / len(self.samples), 1) if self.samples else None
+
+
+class NodeBench:
+    """The simulated node (real control plane) + the outage model + this rank's data plane."""
+
+    def __init__(self, cfg: BenchConfig, barrier_factory=None, gpu_data_plane: bool = True,
+                 verify=None):
+        from .sim.cluster import SimCluster
+
+        self.cfg = cfg
+        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
+        self.sn = next(iter(self.cluster.nodes.values()))
+        if barrier_factory is not None or verify is not None:
+            self._set_commit(barrier_factory, verify)
+        self.churn = ChurnProcess(cfg)
+        self.cluster.run(30)  # node initialisation (SPX everywhere)
+        self.live: Dict[str, int] = {}          # running pod -> served quanta left
+        self.outage: Dict[int, int] = {}        # GPU -> quanta of outage left
+        self._flips_seen = len(self.sn.smi.set_calls)
+        self.reset_stats()
+        self.data: Optional[DataPlane] = DataPlane(cfg) if gpu_data_plane else None
+
+    def reset_stats(self) -> None:
+        self.inferences = 0
+        self.flips = 0
+        self.outage_gpu_steps = 0
+        self.gpu_steps = 0
+        self.util_samples: List[float] = []
+        self.raw_util_samples: List[float] = []
+        self.pods_samples: List[int] = []
+        self.pending_samples: List[int] = []
+        self.host_s = {"control": 0.0, "serve": 0.0}
+        self.empty_steps = 0
+
+    def _set_commit(self, factory: Any, verify: Any) -> None:
+        for c in self.sn.manager.controllers:
+            actuator = getattr(c.reconciler, "__self__", None)
+            if actuator is not None and hasattr(actuator, "barrier_factory"):
+                if factory is not None:
+                    actuator.barrier_factory = factory
+                if verify is not None:
+                    actuator.verify = verify
+
+    # -- control plane + outage model ------------------------------------------------------
+    def pod_gpus(self) -> Dict[str, set]:
+        out: Dict[str, set] = {}
+        for (_, name), devs in self.sn.kubelet.allocations.items():
+            out[name] = {self.sn.smi.resolve(d).gpu_index for _, d in devs}
+        return out
+
+    def control_step(self) -> None:
+        t0 = time.perf_counter()
+        c = self.cluster
+        gpus_of = self.pod_gpus()
+        for name in list(self.live):
+            if any(self.outage.get(g, 0) > 0 for g in gpus_of.get(name, ())):
+                continue  # its GPU is dark: the pod neither serves nor ages
+            self.live[name] -= 1
+            if self.live[name] <= 0:
+                del self.live[name]
+                c.complete(name)
+                c.delete_pod(name)  # the owning controller garbage-collects finished pods
+        for prof in self.churn.arrivals():
+            c.submit({f"amd.com/{prof}": 1}, name=f"p{self.churn.seq}")
+            self.churn.seq += 1
+        c.run(60)
+        calls = self.sn.smi.set_calls
+        for kind, gpu, _ in calls[self._flips_seen:]:
+            self.flips += 1
+            for g in (range(self.cfg.gpus) if gpu is None else (gpu,)):
+                self.outage[g] = max(self.outage.get(g, 0), self.cfg.outage_steps)
+        self._flips_seen = len(calls)
+        for p in c.running_pods():
+            n = ko.name(p)
+            if n not in self.live:
+                self.live[n] = self.churn.lifetime()
+        frac = c.gpu_allocated_fraction()
+        dark = {g for g, k in self.outage.items() if k > 0}
+        self.raw_util_samples.append(100.0 * sum(frac.values()) / max(1, len(frac)))
+        self.util_samples.append(100.0 * sum(v for (_, g), v in frac.items() if g not in dark) / max(1, len(frac)))
+        self.pods_samples.append(len(c.running_pods()))
+        self.pending_samples.append(len(c.pending_pods()))
+        self.gpu_steps += self.cfg.gpus
+        self.outage_gpu_steps += len(dark)
+        self.host_s["control"] += time.perf_counter() - t0
+
+    def end_step(self) -> None:
+        for g in list(self.outage):
+            self.outage[g] -= 1
+            if self.outage[g] <= 0:
+                del self.outage[g]
+
+    def my_pods(self) -> List[Tuple[str, int]]:
+        """(profile, partition index) of the pods served on this rank's GPU this quantum."""
+        if self.outage.get(self.cfg.rank, 0) > 0:
+            return []
+        out = []
+        for devs in self.sn.kubelet.allocations.values():
+            for r, dev_id in devs:
+                prof = extract_profile_name(r)
+                if prof is None:
+                    continue
+                d = self.sn.smi.resolve(dev_id)
+                if d.gpu_index == self.cfg.rank:
+                    out.append((prof, d.partition_index))
+        return out
+
+    def step(self, deadline: Optional[float] = None) -> int:
+        t0 = time.perf_counter()
+        deadline = deadline if deadline is not None else t0 + self.cfg.quantum_s
+        self.control_step()
+        keys = self.my_pods()
+        if not keys:
+            self.empty_steps += 1
+        t1 = time.perf_counter()
+        n = self.data.serve(keys, deadline) if self.data is not None else 0
+        self.host_s["serve"] += time.perf_counter() - t1
+        self.inferences += n
+        self.end_step()
+        return n
+
+    def close(self) -> None:
+        if self.data is not None:
+            self.data.close()
+
+
+# -- density --------------------------------------------------------------------------------
+def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 1.0) -> Dict[str, Any]:
+    """Saturate a fresh node through the control plane, then serve every pod on this rank's GPU
+    at once: 8 CPX pods per GPU, then a CU-mask node with dedicated-CU + memory-only slices."""
+    import torch
+
+    from .api import v1alpha1 as api
+    from .models.slicing.cumask import cus_of
+    from .sim.cluster import SimCluster
+    out: Dict[str, Any] = {}
+    # compute partitions: 8 x 1/8-GPU pods per GPU
+    c = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
+    c.run(30)
+    for i in range(8 * cfg.gpus):
+        c.submit({"amd.com/cpx_nps1": 1}, name=f"d{i}")
+    c.run(120)
+    sn = next(iter(c.nodes.values()))
+    per_gpu = collections.Counter(sn.smi.resolve(d).gpu_index for devs in sn.kubelet.allocations.values()
+                                  for _, d in devs)
+    out["xcp"] = {"pods_per_gpu": min(per_gpu.get(g, 0) for g in range(cfg.gpus)),
+                  "pods_per_node": sum(per_gpu.values()), "pending": len(c.pending_pods())}
+    if data is not None:
+        keys = [("cpx_nps1", sn.smi.resolve(d).partition_index) for devs in sn.kubelet.allocations.values()
+                for _, d in devs if sn.smi.resolve(d).gpu_index == cfg.rank]
+        t0 = time.perf_counter()
+        n = data.serve(keys, t0 + serve_s)
+        data.drain_all()
+        torch.cuda.synchronize()
+        out["xcp"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
+    # CU-mask slices beyond 8 per GPU
+    c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
+                    policy="fifo")
+    c2.run(30)
+    k = 0
+    for _ in range(cfg.gpus):
+        for prof, n_pods in CUMASK_DENSITY:
+            for _ in range(n_pods):
+                c2.submit({f"amd.com/gpu-{prof}": 1}, name=f"s{k}")
+                k += 1
+    c2.run(240)
+    sn2 = next(iter(c2.nodes.values()))
+    per_gpu2 = collections.Counter(sn2.smi.gpu_index_of(d) for devs in sn2.kubelet.allocations.values()
+                                   for _, d in devs)
+    out["cumask"] = {"pods_per_gpu": min(per_gpu2.get(g, 0) for g in range(cfg.gpus)),
+                     "pods_per_node": sum(per_gpu2.values()), "pending": len(c2.pending_pods()),
+                     "profiles": {p: n for p, n in CUMASK_DENSITY}}
+    if data is not None:
+        slices = sn2.plugin.store.load().get(cfg.rank, [])
+        mine = {d for devs in sn2.kubelet.allocations.values() for _, d in devs
+                if sn2.smi.gpu_index_of(d) == cfg.rank}
+        wanted = {("cumask", s.id): cus_of(s, slices, 256) for s in slices if s.id in mine}
+        data.add_slots(wanted)
+        t0 = time.perf_counter()
+        n = data.serve(list(wanted), t0 + serve_s)
+        data.drain_all()
+        torch.cuda.synchronize()
+        out["cumask"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
+    return out
+
+
+# -- driver ---------------------------------------------------------------------------------
 def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     import torch
     import torch.distributed as dist
 
-    from .parallel.barrier import LocalBarrier, TorchBarrier
+    from .parallel.barrier import LocalBarrier, RankCommitBarrier
 
     distributed = cfg.world > 1
     if distributed:
-        bf = lambda n: TorchBarrier()  # noqa: E731 - one vote per rank = per GPU of the node
+        # the agent's commit path (Actuator._commit -> barrier.vote_all(per-device votes)); each
+        # rank contributes the votes of its own GPU's partitions, all-reduced over RCCL
+        bf = lambda n: RankCommitBarrier(rank=cfg.rank, world=cfg.world)  # noqa: E731
     else:
-        bf = lambda n: LocalBarrier(1)  # noqa: E731
+        bf = lambda n: LocalBarrier(n)  # noqa: E731
     nb = NodeBench(cfg, barrier_factory=bf)
     for _ in range(cfg.preroll):
         nb.control_step()
+        nb.end_step()
     for _ in range(cfg.warmup):
         nb.step()
+    nb.data.drain_all()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
-    nb.inferences = 0
-    nb.mode_drains = 0
-    nb.empty_epochs = 0
-    nb.host_s = {k: 0.0 for k in nb.host_s}
-    nb.util_samples.clear()
-    nb.pods_samples.clear()
-    nb.pending_samples.clear()
+    nb.reset_stats()
+    busy = HwBusySampler(nb.data.device)
+    busy.start()
     t0 = time.perf_counter()
+    deadline = t0
     for _ in range(cfg.steps):
-        nb.step()
+        deadline += cfg.quantum_s
+        nb.step(deadline)
+    nb.data.drain_all()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    hw_busy = busy.stop()
     on_gpu = dist.get_backend() == "nccl" if distributed else True
-    stats = torch.tensor([elapsed, float(nb.inferences)], dtype=torch.float64,
-                         device=f"cuda:{nb.device}" if on_gpu else "cpu")
+    stats = torch.tensor([elapsed, float(nb.inferences), hw_busy if hw_busy is not None else -1.0],
+                         dtype=torch.float64, device=f"cuda:{nb.data.device}" if on_gpu else "cpu")
     if distributed:
         t = stats[:1].clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         s = stats[1:].clone()
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        elapsed, total_inf = float(t.item()), float(s.item())
+        elapsed, total_inf = float(t.item()), float(s[0].item())
+        hw_busy = round(float(s[1].item()) / cfg.world, 1) if hw_busy is not None else None
     else:
         total_inf = float(nb.inferences)
+    density = density_phase(cfg, nb.data) if cfg.density else {}
     nb.close()
     value = total_inf / elapsed
     util = sum(nb.util_samples) / max(1, len(nb.util_samples))
+    raw = sum(nb.raw_util_samples) / max(1, len(nb.raw_util_samples))
     pods = sum(nb.pods_samples) / max(1, len(nb.pods_samples))
     from .models.workload.yolos import YolosSmall
     from .ops import kernels as K
@@ -402,25 +589,70 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
                      "error vs fp64 against the f32-input MFMA path)") if cfg.backend == "hip" else "fp32",
         "data": "synthetic (seeded pod churn; random-init YOLOS-small weights; synthetic 800x1066 images)",
         "gpu_utilization_pct": round(util, 2),
+        "allocation_pct_incl_outage": round(raw, 2),
+        "hw_busy_pct": hw_busy,
+        "hw_busy_source": "amd-smi gfx_activity, sampled every 100 ms in the timed window" if hw_busy is not None
+        else f"unavailable: {busy.error}",
         "pods_per_node": round(pods, 2),
         "pods_per_gpu": round(pods / cfg.gpus, 2),
+        "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},
+        "density": density,
         "pending_pods_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
+        "pending_pods_max": max(nb.pending_samples) if nb.pending_samples else 0,
+        "flip_cost_s": cfg.flip_cost_s,
+        "flips": nb.flips,
+        "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),
+        "quantum_s": cfg.quantum_s,
         "achieved_tflops": round(value * flops / 1e12, 2),
         "host_ms_per_step": {k: round(1000.0 * v / cfg.steps, 2) for k, v in nb.host_s.items()},
-        "mode_drains": nb.mode_drains,
-        "empty_epochs": nb.empty_epochs,
+        "layout_drains": nb.data.drains if nb.data is not None else 0,
+        "empty_steps": nb.empty_steps,
         "baseline_ref": BASELINE_LABEL,
         "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
                    "parallelism": f"fractional-gpu xcp partitions, {cfg.gpus} GPU node",
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
-                   "backend": cfg.backend, "hip_graphs": cfg.graphs,
+                   "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
+                   "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
                    "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
 
 
+def control_only(cfg: BenchConfig, steps: int) -> Dict[str, Any]:
+    """The control plane + outage model alone (no GPU): allocation, flips and queue over ``steps``
+    quanta after the preroll.  ``inf_per_s_model`` prices the served partition-quanta with the
+    measured per-mode full-GPU rates (``profiles/kbench_r1_s5_modes.json``)."""
+    nb = NodeBench(cfg, gpu_data_plane=False)
+    for _ in range(cfg.preroll):
+        nb.control_step()
+        nb.end_step()
+    nb.reset_stats()
+    rate = {"spx": 356.0, "dpx": 402.1, "qpx": 414.5, "cpx": 359.1}
+    served = 0.0
+    for _ in range(steps):
+        nb.control_step()
+        for g in range(cfg.gpus):
+            if nb.outage.get(g, 0) > 0:
+                continue
+            for devs in nb.sn.kubelet.allocations.values():
+                for r, d in devs:
+                    p = extract_profile_name(r)
+                    if p is not None and nb.sn.smi.resolve(d).gpu_index == g:
+                        m = p.split("_")[0]
+                        served += rate[m] / COMPUTE_MODES[m] * cfg.quantum_s
+        nb.end_step()
+    return {"policy": cfg.policy, "gpus": cfg.gpus, "steps": steps, "flip_cost_s": cfg.flip_cost_s,
+            "util_pct": round(sum(nb.util_samples) / max(1, len(nb.util_samples)), 2),
+            "util_incl_outage_pct": round(sum(nb.raw_util_samples) / max(1, len(nb.raw_util_samples)), 2),
+            "flips": nb.flips, "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),
+            "pending_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
+            "pending_max": max(nb.pending_samples) if nb.pending_samples else 0,
+            "pods_per_gpu": round(sum(nb.pods_samples) / max(1, len(nb.pods_samples)) / cfg.gpus, 2),
+            "inf_per_s_model": round(served / (steps * cfg.quantum_s), 1)}
+
+
 def smoke_step() -> None:
-    """One control-plane epoch + one partition's inference on cuda:0 + one slice probe."""
+    """One control-plane step + one partition's inference on cuda:0 + one slice probe."""
     import torch
 
     from .ops import probe

@@ -75,6 +75,7 @@ class Actuator:
         self.last_applied_status: Optional[list] = None
         self.applied_plans = 0
         self.last_votes: List[bool] = []
+        self._vote_devices: List[Any] = []
 
     def reconcile(self, req: Request) -> Result:
         if not self.shared.at_least_one_report_since_last_apply():
@@ -218,6 +219,9 @@ class Actuator:
         if self.barrier_factory is None:
             return all(votes)
         barrier = self.barrier_factory(max(1, len(votes)))
+        participants = getattr(barrier, "set_participants", None)
+        if participants is not None and self._vote_devices:
+            participants(self._vote_devices)
         try:
             vote_all = getattr(barrier, "vote_all", None)
             if vote_all is not None:
@@ -228,6 +232,7 @@ class Actuator:
 
     def _votes(self, applied: List[Any]) -> List[bool]:
         target = {ch.gpu_index: ch.to_profile for ch in applied}
+        self._vote_devices = []
         dm_fn = getattr(self.pc, "device_map", None)
         if dm_fn is None:
             # a partition client without a device map: one vote per changed GPU
@@ -249,6 +254,7 @@ class Actuator:
                 ok = bool(self.verify(g, p))
             gpu_ok[g] = ok
         devices = sorted(m.devices, key=lambda d: (d.hip_id, d.gpu_index, d.partition_index))
+        self._vote_devices = devices
         return [gpu_ok.get(d.gpu_index, True) for d in devices]
 
     def _rollback(self, flipped: List[Tuple[int, Optional[str]]]) -> None:

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import logging
 import time
+from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Mapping, Optional, Tuple, Union
 
 from ...api import v1alpha1 as api
@@ -38,6 +39,8 @@ from ...utils.metrics import REGISTRY
 log = logging.getLogger("nos.partitioner")
 
 NodeModel = Union[PartitionedNode, SlicingNode]
+
+POLICIES = ("fifo", "batch", "simulate", "pack")
 
 
 _REQ_CACHE: Dict[Tuple[str, str], Dict[str, int]] = {}
@@ -157,6 +160,156 @@ def plan_cluster_fifo(models: Mapping[str, NodeModel], pending: List[Dict[str, i
     return changed
 
 
+@dataclass
+class PackParams:
+    """Knobs of the flip-aware ``pack`` policy (``GpuPartitionerConfig.packing``)."""
+    min_fill: float = 0.5           # flip an idle GPU only if the queue fills >= this fraction of it
+    starve_after: float = 600.0     # seconds: older pods win an idle GPU regardless of min_fill
+    drain_after: float = 7200.0     # seconds: a pod waiting this long makes a busy GPU drain for it
+    drain_backlog: float = 2.0      # ... if its profile's queue would fill at least this many GPUs
+    spx_reserve: bool = True        # keep idle SPX GPUs for recent whole-GPU demand (multi-GPU)
+    reserve_decay: float = 0.9      # EMA decay of the whole-GPU demand estimate per planning pass
+
+
+def _mode_of(gpu: Any) -> Optional[str]:
+    geo = gpu.geometry()
+    return next(iter(geo)) if len(geo) == 1 else None
+
+
+def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[str, int], float]],
+                      incoming: Optional[Mapping[str, int]] = None, params: Optional[PackParams] = None,
+                      spx_demand: float = 0.0) -> Dict[str, NodeModel]:
+    """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
+    reference's "first node that can change wins").
+
+    A mode flip destroys every partition of a GPU and costs seconds of outage (amd-smi switch plus
+    device-plugin re-registration), so the policy flips as little as possible and only idle GPUs:
+
+    1. pending pods (oldest first) take existing free partitions — split GPUs are filled first
+       because every free partition of the current layout is consumed before any flip — then the
+       capacity in-flight plans will provide;
+    2. the remaining demand is summed per profile in GPU fractions, each profile remembering its
+       oldest waiting pod;
+    3. each **idle** GPU (no partition in use; busy GPUs are never touched) is given to the profile
+       with the largest demand, but only when the queue fills at least ``min_fill`` of it, or that
+       profile's oldest pod has waited ``starve_after`` (so nothing starves): otherwise it keeps
+       its mode (hysteresis — an idle GPU left as it is costs nothing, a flip costs an outage);
+    4. on multi-GPU nodes idle SPX GPUs are kept as a reserve sized from the recent whole-GPU demand
+       (``spx_demand``, an EMA in GPUs), unless a starving pod needs them;
+    5. a profile whose oldest pod has waited ``drain_after``, and whose queue would fill
+       ``drain_backlog`` GPUs (a drain idles partitions, so it must buy a full GPU of work), with no
+       idle GPU to take gets one busy
+       GPU **drained** for it: the least-used GPU in another mode gets the new spec now, is no
+       longer offered to new pods (``PartitionedGPU.target``; the scheduler skips GPUs whose spec
+       mode differs from their current mode), and the agent flips it when its last pod leaves.
+       Without this a single GPU that never goes idle would starve every other profile forever.
+
+    ``pending`` = [(requested profiles, age in seconds)], oldest first."""
+    params = params or PackParams()
+    current = {n: m.clone() for n, m in models.items()}
+    changed: Dict[str, NodeModel] = {}
+    extra = {p: q for p, q in (incoming or {}).items() if q > 0}
+    unserved: List[Tuple[Dict[str, int], float]] = []
+    for req, age in pending:
+        placed = False
+        for name in sorted(current):
+            try:
+                current[name].add_pod(req)
+                placed = True
+                break
+            except ValueError:
+                continue
+        if not placed and all(extra.get(p, 0) >= q for p, q in req.items()):
+            for p, q in req.items():
+                extra[p] -= q
+            placed = True
+        if not placed:
+            unserved.append((req, age))
+    if not unserved or not current:
+        return changed
+    first = next(iter(current.values()))
+    w = getattr(first, "weight", None)
+    frac = (lambda p: w(p)) if w is not None else (lambda p: 1.0)
+    demand: Dict[str, float] = {}
+    oldest: Dict[str, float] = {}
+    for req, age in unserved:
+        if len(req) != 1:
+            continue  # a pod asking for two different profiles cannot be helped by one flip
+        (p, q), = req.items()
+        demand[p] = demand.get(p, 0.0) + q * frac(p)
+        oldest[p] = max(oldest.get(p, 0.0), age)
+    idle = [(name, g) for name in sorted(current) for g in current[name].gpus
+            if g.is_idle() and g.target is None]
+    total_gpus = sum(len(m.gpus) for m in current.values())
+    spx_gpus = [(n, g) for n in sorted(current) for g in current[n].gpus if (_mode_of(g) or "").startswith("spx")]
+    reserve = min(len(spx_gpus), int(round(spx_demand))) if (params.spx_reserve and total_gpus > 1) else 0
+    # idle GPUs whose mode nobody is waiting for go first; SPX GPUs last (they are the reserve)
+    idle.sort(key=lambda ng: ((_mode_of(ng[1]) or "").startswith("spx"), ng[0], ng[1].index))
+    spx_kept = sum(1 for n, g in spx_gpus if not g.is_idle())
+    for name, g in idle:
+        if not demand:
+            break
+        cur = _mode_of(g)
+        best: Optional[Tuple[Tuple[int, float, float], str]] = None
+        for p, d in demand.items():
+            if p == cur or d <= 0:
+                continue
+            starving = oldest.get(p, 0.0) >= params.starve_after
+            fill = min(d, 1.0)
+            if fill + 1e-9 < params.min_fill and not starving:
+                continue
+            key = (1 if starving else 0, fill, oldest.get(p, 0.0))
+            if best is None or key > best[0]:
+                best = (key, p)
+        if best is None:
+            continue
+        (starving, _, _), p = best
+        if cur is not None and cur.startswith("spx") and spx_kept < reserve and not starving:
+            spx_kept += 1
+            continue  # keep this idle SPX GPU for the whole-GPU demand
+        trial = g.clone()
+        if not trial.update_geometry_for({p: 10**6}) or _mode_of(trial) != p:
+            continue
+        g.used, g.free = trial.used, trial.free
+        changed[name] = current[name]
+        # the new partitions serve the waiting pods of that profile
+        placed_any = True
+        while placed_any and demand.get(p, 0) > 0:
+            placed_any = False
+            for i, (req, age) in enumerate(unserved):
+                if set(req) == {p}:
+                    try:
+                        g.add_pod(req)
+                    except ValueError:
+                        break
+                    demand[p] -= sum(q * frac(p) for q in req.values())
+                    unserved.pop(i)
+                    placed_any = True
+                    break
+        if demand.get(p, 0) <= 1e-9:
+            demand.pop(p, None)
+    # 5. drain a busy GPU for a profile that has waited too long
+    draining_to = {next(iter(g.target)) for m in current.values() for g in m.gpus if g.target}
+    for p in sorted(demand, key=lambda q: -oldest.get(q, 0.0)):
+        if demand[p] < params.drain_backlog - 1e-9 or oldest.get(p, 0.0) < params.drain_after or p in draining_to:
+            continue
+        cands = [(g.used_fraction(lambda q: round(1.0 / frac(q))) if w is not None else sum(g.used.values()),
+                  name, g) for name in sorted(current) for g in current[name].gpus
+                 if g.target is None and not g.is_idle() and _mode_of(g) != p]
+        if not cands:
+            continue
+        _, name, g = min(cands, key=lambda c: (c[0], c[1], c[2].index))
+        trial = g.clone()
+        trial.used = {}
+        trial.free = {}
+        if not trial.update_geometry_for({p: 10**6}) or _mode_of(trial) != p:
+            continue
+        g.target = trial.geometry()
+        changed[name] = current[name]
+        draining_to.add(p)
+    return changed
+
+
 def simulate_schedule(models: Mapping[str, NodeModel], pending: List[Dict[str, int]]) -> Tuple[int, float]:
     """Pods (and GPU fraction) a first-fit scheduler would place, in arrival order, on ``models``."""
     sim = {n: m.clone() for n, m in models.items()}
@@ -224,13 +377,17 @@ def plan_cluster_simulate(models: Mapping[str, NodeModel], pending: List[Dict[st
 class PodController:
     def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
                  clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
-                 retry_after: float = 5.0, scoring: str = "fraction", policy: str = "fifo"):
+                 retry_after: float = 5.0, scoring: str = "fraction", policy: str = "fifo",
+                 pack: Optional[PackParams] = None):
         self.client = client
         self.kind = kind
         self.scoring = scoring
-        if policy not in ("fifo", "batch", "simulate"):
+        if policy not in POLICIES:
             raise ValueError(f"unknown planning policy {policy!r}")
         self.policy = policy
+        self.pack = pack or PackParams()
+        self._first_seen: Dict[str, float] = {}   # pending pod uid -> first time the planner saw it
+        self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -259,6 +416,26 @@ class PodController:
             r = requested_profiles(self.kind, p)
             if r:
                 out.append(r)
+        return out
+
+    def pending_with_age(self) -> List[Tuple[Dict[str, int], float]]:
+        """(requested profiles, seconds since the planner first saw the pod), highest priority
+        then oldest first (the ``pack`` policy's input)."""
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if self.should_consider(p)]
+        pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
+        now = self.clock()
+        seen: Dict[str, float] = {}
+        out = []
+        for p in pods:
+            r = requested_profiles(self.kind, p)
+            if not r:
+                continue
+            uid = p["metadata"].get("uid") or ko.name(p)
+            t = self._first_seen.get(uid, now)
+            seen[uid] = t
+            out.append((r, now - t))
+        self._first_seen = seen
         return out
 
     def pending_requests(self) -> Dict[str, int]:
@@ -308,6 +485,16 @@ class PodController:
             if sum(m.free().get(p, 0) for m in models.values()) < q:
                 return False
         return True
+
+    def _update_spx_demand(self, nodes: List[Dict[str, Any]], pending: List[Tuple[Dict[str, int], float]]) -> None:
+        """EMA of whole-GPU demand: SPX partitions in use plus SPX pods waiting."""
+        used = 0
+        for n in nodes:
+            status, _ = ann.parse_node_annotations(ko.annotations(n))
+            used += sum(s.quantity for s in status if s.is_used() and s.profile.startswith("spx"))
+        waiting = sum(q for req, _ in pending for p, q in req.items() if p.startswith("spx"))
+        d = self.pack.reserve_decay
+        self.spx_demand = d * self.spx_demand + (1 - d) * (used + waiting)
 
     # -- watch mapping ------------------------------------------------------------------
     @property
@@ -389,7 +576,16 @@ class PodController:
             if flying:
                 return Result(requeue_after=self.retry_after)
             return Result()
-        if self.policy in ("fifo", "simulate"):
+        if self.policy == "pack":
+            incoming = {}
+            for n in flying:
+                for p, q in self.incoming_free(n).items():
+                    incoming[p] = incoming.get(p, 0) + q
+            pend = self.pending_with_age()
+            self._update_spx_demand(nodes, pend)
+            changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand)
+            need = requested
+        elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}
             for n in flying:
                 for p, q in self.incoming_free(n).items():

@@ -32,10 +32,18 @@ class PartitionedGPU:
     allowed_geometries: List[Geometry]
     used: Dict[str, int] = field(default_factory=dict)
     free: Dict[str, int] = field(default_factory=dict)
+    #: desired geometry when the spec asks for a different one than the GPU has while partitions
+    #: are still in use: the GPU is *draining* — no new pod is placed on it, and it flips to
+    #: ``target`` as soon as it is idle (MI355X: a flip destroys every partition)
+    target: Optional[Dict[str, int]] = None
 
     def clone(self) -> "PartitionedGPU":
         return PartitionedGPU(self.model, self.index, [dict(g) for g in self.allowed_geometries],
-                              dict(self.used), dict(self.free))
+                              dict(self.used), dict(self.free), dict(self.target) if self.target else None)
+
+    def spec_geometry(self) -> Geometry:
+        """What the spec should say for this GPU: the drain target, else the geometry."""
+        return dict(self.target) if self.target else self.geometry()
 
     def geometry(self) -> Geometry:
         out: Geometry = {}
@@ -108,6 +116,8 @@ class PartitionedGPU:
         return True
 
     def add_pod(self, requested: Mapping[str, int]) -> None:
+        if self.target is not None:
+            raise ValueError(f"GPU {self.index} is draining towards {self.target}")
         for p, q in requested.items():
             if self.free.get(p, 0) < q:
                 raise ValueError(f"not enough free partitions (pod requests {q} {p}, but GPU only has "

@@ -38,12 +38,18 @@ def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
     nps = gpu_util.get_memory_partition(node)
-    status, _ = ann.parse_node_annotations(ko.annotations(node))
+    status, spec = ann.parse_node_annotations(ko.annotations(node))
     gpus: Dict[int, PartitionedGPU] = {}
+    spec_by_gpu: Dict[int, Dict[str, int]] = {}
+    for a in spec:
+        spec_by_gpu.setdefault(a.index, {})[a.profile] = spec_by_gpu.get(a.index, {}).get(a.profile, 0) + a.quantity
     for idx, items in sorted(ann.group_by_gpu_index(status).items()):
         used = {a.profile: a.quantity for a in items if a.is_used()}
         free = {a.profile: a.quantity for a in items if a.is_free()}
         gpus[idx] = new_gpu(model, idx, nps, used, free)
+        want = {p: q for p, q in spec_by_gpu.get(idx, {}).items() if q > 0}
+        if want and any(q > 0 for q in used.values()) and want != gpus[idx].geometry():
+            gpus[idx].target = want  # a flip the agent cannot apply until the GPU drains
     for i in range(count):
         if i not in gpus:
             gpus[i] = new_gpu(model, i, nps)

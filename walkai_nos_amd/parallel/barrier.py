@@ -121,6 +121,35 @@ class TorchBarrier(CommitBarrier):
         return res
 
 
+class RankCommitBarrier(TorchBarrier):
+    """The agent's commit path on a one-process-per-GPU job (the multi-GPU bench).
+
+    The actuator produces one vote per logical device of the node (``Actuator._votes``) and hands
+    the barrier the devices behind them (``set_participants``); this rank keeps only the votes of
+    the partitions on *its* GPU, ANDs them with ``local_check()`` (e.g. "my data plane drained and
+    my device answers"), and the all-reduce over the ranks (RCCL over xGMI, or gloo) says whether
+    every GPU of the node committed.  One rank's veto therefore rolls the plan back on every rank
+    (each runs the same control-plane replica, so they roll back identically)."""
+
+    def __init__(self, rank: int, world: int, local_check=None, group: Any = None, device: Optional[Any] = None):
+        super().__init__(group, device)
+        self.rank = rank
+        self.local_check = local_check
+        self._gpus: Optional[List[int]] = None
+        self.last_local: Optional[bool] = None
+
+    def set_participants(self, devices: List[Any]) -> None:
+        self._gpus = [int(getattr(d, "gpu_index", d)) for d in devices]
+
+    def vote_all(self, votes: List[bool]) -> bool:
+        mine = [v for v, g in zip(votes, self._gpus or []) if g == self.rank] if self._gpus else list(votes)
+        local = all(mine)
+        if local and self.local_check is not None:
+            local = bool(self.local_check())
+        self.last_local = local
+        return self.vote(local)
+
+
 class RcclBarrier(CommitBarrier):
     """Native RCCL communicator over the node's devices (``csrc/rccl_barrier.cpp``)."""
 

@@ -44,7 +44,8 @@ def build_node_partitioning(node: Union[PartitionedNode, SlicingNode], memory_pa
     gpus = []
     for g in node.gpus:
         resources: Dict[str, int] = {}
-        for p, q in g.geometry().items():
+        geo = g.spec_geometry() if hasattr(g, "spec_geometry") else g.geometry()
+        for p, q in geo.items():
             if q <= 0:
                 continue
             r = as_res(p) if as_res is not None else _slice_resource(p)

@@ -88,21 +88,23 @@ class SimKubelet:
     def used_ids(self) -> Dict[str, str]:
         return {i: r for devs in self.allocations.values() for r, i in devs}
 
-    def free_devices(self, resource: str) -> List[str]:
+    def free_devices(self, resource: str, skip_gpus: frozenset = frozenset()) -> List[str]:
         used = self.used_ids()
-        return [i for i in self.plugin.advertised.get(resource, []) if i not in used]
+        return [i for i in self.plugin.advertised.get(resource, []) if i not in used
+                and (not skip_gpus or self.smi.gpu_index_of(i) not in skip_gpus)]
 
-    def can_fit(self, req: Dict[str, int]) -> bool:
-        return all(len(self.free_devices(r)) >= q for r, q in req.items() if is_managed(r))
+    def can_fit(self, req: Dict[str, int], skip_gpus: frozenset = frozenset()) -> bool:
+        return all(len(self.free_devices(r, skip_gpus)) >= q for r, q in req.items() if is_managed(r))
 
-    def allocate(self, pod_key: Tuple[str, str], req: Dict[str, int]) -> List[Tuple[str, str]]:
+    def allocate(self, pod_key: Tuple[str, str], req: Dict[str, int],
+                 skip_gpus: frozenset = frozenset()) -> List[Tuple[str, str]]:
         """GetPreferredAllocation semantics: pack onto the GPU that already has the most partitions
         in use, so whole GPUs stay idle for future mode flips (fragmentation control)."""
         out: List[Tuple[str, str]] = []
         for r, q in req.items():
             if not is_managed(r):
                 continue
-            free = self.free_devices(r)
+            free = self.free_devices(r, skip_gpus)
             used_per_gpu: Dict[int, int] = defaultdict(int)
             for i in self.used_ids():
                 used_per_gpu[self.smi.gpu_index_of(i)] += 1
@@ -137,6 +139,26 @@ class SimNode:
     dp_counter: Any = field(default_factory=lambda: itertools.count(1))
 
 
+def draining_gpus(node: Optional[Dict[str, Any]]) -> frozenset:
+    """GPUs whose spec asks for a different geometry than the one they report while partitions
+    are in use: they wait for their pods to leave before the agent flips them, so no new pod may
+    land on their free partitions (the pack policy's drain, ``plan_cluster_pack`` step 5)."""
+    if node is None:
+        return frozenset()
+    from ..models import annotation as ann
+    status, spec = ann.parse_node_annotations(ko.annotations(node))
+    want: Dict[int, Dict[str, int]] = defaultdict(lambda: defaultdict(int))
+    have: Dict[int, Dict[str, int]] = defaultdict(lambda: defaultdict(int))
+    busy = set()
+    for a in spec:
+        want[a.index][a.profile] += a.quantity
+    for a in status:
+        have[a.index][a.profile] += a.quantity
+        if a.is_used() and a.quantity > 0:
+            busy.add(a.index)
+    return frozenset(g for g in busy if g in want and dict(want[g]) != dict(have[g]))
+
+
 class SimScheduler:
     """Binds pending pods (first-fit over nodes ordered most-allocated first) or marks them
     Unschedulable — the signal the partitioner reacts to."""
@@ -154,10 +176,11 @@ class SimScheduler:
                 if not podutil.is_scheduled(p)
                 and p["spec"].get("schedulerName", "default-scheduler") == "default-scheduler"]
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
+        draining = {n.name: draining_gpus(self.api.get("Node", n.name)) for n in self.nodes.values()}
         for p in pods:
             reqs = res.compute_pod_request(p)
             order = sorted(self.nodes.values(), key=lambda n: (-len(n.kubelet.allocations), n.name))
-            target = next((n for n in order if n.kubelet.can_fit(reqs)), None)
+            target = next((n for n in order if n.kubelet.can_fit(reqs, draining[n.name])), None)
             if target is None:
                 if not podutil.is_unschedulable(p):
                     st = {"conditions": [{"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
@@ -173,7 +196,7 @@ class SimScheduler:
             except (Conflict, NotFound):
                 continue
             self.bound += 1
-            self.on_bind(p, target.name)
+            self.on_bind(p, target.name, draining[target.name])
         return Result()
 
 
@@ -260,9 +283,9 @@ class SimCluster:
         alloc = sn.kubelet.allocatable()
         self.api.patch("Node", sn.name, {"status": {"allocatable": alloc, "capacity": alloc}})
 
-    def _on_bind(self, pod: Dict[str, Any], node: str) -> None:
+    def _on_bind(self, pod: Dict[str, Any], node: str, skip_gpus: frozenset = frozenset()) -> None:
         """kubelet side of a binding: allocate devices (preferred allocation) and start the pod."""
-        self.nodes[node].kubelet.allocate(ko.key(pod), res.compute_pod_request(pod))
+        self.nodes[node].kubelet.allocate(ko.key(pod), res.compute_pod_request(pod), skip_gpus)
         self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Running"}}, ko.namespace(pod))
         self.binds.append((self.clock(), ko.key(pod)[1], node))
 
