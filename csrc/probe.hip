@@ -5,9 +5,9 @@
 //
 // Design (gfx950, MI355X_MICROARCH.md "Matrix cores" + "Per-instruction cycle constants"):
 //  * 256-thread workgroups = 4 waves = one wave per SIMD; default 2 workgroups per CU.
-//  * operands are staged once into LDS and re-read with ds_read_b128 every iteration (two reads
-//    per four 32x32x16 MFMAs: within the per-gap budget measured at <=3 cycles), so the loop is
-//    matrix-pipe bound, not memory bound, and the operands are random (DVFS-realistic) data.
+//  * operands are random data staged once through LDS into eight register-resident (A, B) pairs
+//    that the loop cycles through: the loop body is MFMAs only, matrix-pipe bound, and every MFMA
+//    still sees different random operands (DVFS-realistic).
 //  * four independent accumulators per wave; a 32x32x16 bf16 MFMA issues every 32 cycles per SIMD
 //    = 1024 FLOP/clk/SIMD -> 2.5 PF dense at 2.4 GHz on 256 CUs.
 //  * dtype variants: bf16 32x32x16, bf16 16x16x32, f32-input 32x32x2 (exact fp32, 1/16 rate),
@@ -44,70 +44,81 @@ template <int DTYPE>
 __global__ __launch_bounds__(kThreads) void mfma_probe(const uint4* __restrict__ src, uint32_t src_len,
                                                       float* __restrict__ out, int iters,
                                                       unsigned long long* __restrict__ clk) {
+  // Operands: random data staged through LDS once, then held in registers as kOps distinct
+  // (A, B) pairs that every iteration cycles through — each MFMA still sees different random
+  // operands (DVFS-realistic toggling), but the loop body is nothing but MFMAs: no LDS reads, no
+  // address arithmetic, one scalar loop branch per kOps MFMAs (the r1 loop re-read both operands
+  // from LDS every 4 MFMAs and reached 78-83% of the clock peak).
+  constexpr int kOps = 8;
   __shared__ uint4 lds[kLdsVec];
   const int t = threadIdx.x;
   for (int i = t; i < kLdsVec; i += kThreads) lds[i] = src[(blockIdx.x * 131u + i) % src_len];
   __syncthreads();
+  uint4 ra[kOps], rb[kOps];
+#pragma unroll
+  for (int k = 0; k < kOps; ++k) {
+    ra[k] = lds[(t * 3 + k * 97) & (kLdsVec - 1)];
+    rb[k] = lds[(t * 5 + k * 61 + 512) & (kLdsVec - 1)];
+  }
   // shader-clock cycles (s_memtime) vs the constant-rate wall clock (s_memrealtime) over the loop:
   // their ratio is the core clock the matrix pipes actually ran at under this load (DVFS).
   const unsigned long long c0 = clock64(), w0 = wall_clock64();
 
   float result = 0.f;
   if constexpr (DTYPE == 0) {  // bf16 32x32x16
-    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
+    f32x16 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = f32x16{0};
     for (int it = 0; it < iters; ++it) {
-      uint4 a = lds[(t + it * 37) & (kLdsVec - 1)];
-      uint4 b = lds[(t + it * 53 + 512) & (kLdsVec - 1)];
-      bf16x8 A = as_bf16x8(a), B = as_bf16x8(b);
-      c0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, B, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(B, A, c1, 0, 0, 0);
-      c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A, A, c2, 0, 0, 0);
-      c3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(B, B, c3, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < kOps; ++k)
+        acc[k & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(ra[k]), as_bf16x8(rb[k]), acc[k & 3], 0, 0, 0);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) result += acc[k][r];
   } else if constexpr (DTYPE == 1) {  // bf16 16x16x32
-    f32x4 c[8];
+    f32x4 acc[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = f32x4{0, 0, 0, 0};
+    for (int k = 0; k < 8; ++k) acc[k] = f32x4{0, 0, 0, 0};
     for (int it = 0; it < iters; ++it) {
-      uint4 a = lds[(t + it * 37) & (kLdsVec - 1)];
-      uint4 b = lds[(t + it * 53 + 512) & (kLdsVec - 1)];
-      bf16x8 A = as_bf16x8(a), B = as_bf16x8(b);
 #pragma unroll
-      for (int k = 0; k < 8; k += 2) {
-        c[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B, c[k], 0, 0, 0);
-        c[k + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(B, A, c[k + 1], 0, 0, 0);
+      for (int k = 0; k < 2 * kOps; ++k)
+        acc[k & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(ra[k & (kOps - 1)]), as_bf16x8(rb[(k + 3) & (kOps - 1)]),
+                                                             acc[k & 7], 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) result += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+  } else if constexpr (DTYPE == 2) {  // f32-input 32x32x2 (exact fp32)
+    f32x16 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = f32x16{0};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int k = 0; k < kOps; ++k)
+        acc[k & 3] = __builtin_amdgcn_mfma_f32_32x32x2f32(__builtin_bit_cast(float, ra[k].x),
+                                                          __builtin_bit_cast(float, rb[k].y), acc[k & 3], 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) result += acc[k][r];
+  } else {  // fp8 e4m3 32x32x16
+    f32x16 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = f32x16{0};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int k = 0; k < kOps; ++k) {
+        const long a = (long(ra[k].y) << 32) | ra[k].x, b = (long(rb[k].w) << 32) | rb[k].z;
+        acc[k & 3] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, acc[k & 3], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) result += c[k][0] + c[k][1] + c[k][2] + c[k][3];
-  } else if constexpr (DTYPE == 2) {  // f32-input 32x32x2 (exact fp32)
-    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
-    const float* ldsf = reinterpret_cast<const float*>(lds);
-    for (int it = 0; it < iters; ++it) {
-      float a = ldsf[(t + it * 37) & (4 * kLdsVec - 1)];
-      float b = ldsf[(t + it * 53 + 2048) & (4 * kLdsVec - 1)];
-      c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
-      c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c2, 0, 0, 0);
-      c3 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, b, c3, 0, 0, 0);
-    }
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
-  } else {  // fp8 e4m3 32x32x16
-    f32x16 c0 = {0}, c1 = {0}, c2 = {0}, c3 = {0};
-    const long* ldsl = reinterpret_cast<const long*>(lds);
-    for (int it = 0; it < iters; ++it) {
-      long a = ldsl[(t + it * 37) & (2 * kLdsVec - 1)];
-      long b = ldsl[(t + it * 53 + 1024) & (2 * kLdsVec - 1)];
-      c0 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(b, a, c1, 0, 0, 0);
-      c2 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, a, c2, 0, 0, 0);
-      c3 = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(b, b, c3, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) result += c0[r] + c1[r] + c2[r] + c3[r];
+      for (int r = 0; r < 16; ++r) result += acc[k][r];
   }
   out[blockIdx.x * kThreads + t] = result;
   if (clk != nullptr && t == 0) {
@@ -117,15 +128,25 @@ __global__ __launch_bounds__(kThreads) void mfma_probe(const uint4* __restrict__
 }
 
 // FLOP per loop iteration per wave for each dtype variant
-constexpr double kFlopPerIterWave[4] = {4.0 * 2 * 32 * 32 * 16, 8.0 * 2 * 16 * 16 * 32, 4.0 * 2 * 32 * 32 * 2,
-                                        4.0 * 2 * 32 * 32 * 16};
+constexpr double kFlopPerIterWave[4] = {8.0 * 2 * 32 * 32 * 16, 16.0 * 2 * 16 * 16 * 32, 8.0 * 2 * 32 * 32 * 2,
+                                        8.0 * 2 * 32 * 32 * 16};
 
 __global__ __launch_bounds__(kThreads) void hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
-  size_t i = size_t(blockIdx.x) * kThreads + threadIdx.x;
+  // Streaming copy: each lane keeps 8 x 16 B loads in flight (the guide's measured float4 copy
+  // needs ~32 KiB in flight per CU to cover an HBM miss), and the non-temporal hint keeps the
+  // once-touched lines from evicting the L2/Infinity-Cache working set of co-running partitions.
+  typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+  constexpr int U = 8;
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+  u32x4* d4 = reinterpret_cast<u32x4*>(dst);
   const size_t stride = size_t(gridDim.x) * kThreads;
-  for (; i + 3 * stride < n; i += 4 * stride) {  // 4 x 16 B in flight per lane
-    uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a; dst[i + stride] = b; dst[i + 2 * stride] = c; dst[i + 3 * stride] = d;
+  size_t i = size_t(blockIdx.x) * kThreads + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    u32x4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = __builtin_nontemporal_load(s4 + i + k * stride);
+#pragma unroll
+    for (int k = 0; k < U; ++k) __builtin_nontemporal_store(v[k], d4 + i + k * stride);
   }
   for (; i < n; i += stride) dst[i] = src[i];
 }
