@@ -9,6 +9,12 @@
 // queue the process creates, hsa_ext_amd.h:1330-1345); both variables are injected by the nos device
 // plugin at Allocate time.
 //
+// Interposed: hipMalloc, hipExtMallocWithFlags, hipMallocAsync, hipMallocFromPoolAsync,
+// hipMallocManaged, hipMallocPitch and hipMalloc3D (charged pitch x height [x depth] after the
+// runtime picked the pitch; over budget -> freed again, hipErrorOutOfMemory), and the virtual-
+// memory path PyTorch's expandable segments use: hipMemCreate charges the physical allocation,
+// hipMemRelease returns it (mapping it with hipMemMap allocates nothing more).
+//
 // Isolation is cooperative: nothing stops a process from unsetting LD_PRELOAD (documented in
 // docs/partitioning-modes.md, as the reference documents MPS's limits).
 #include <dlfcn.h>
@@ -29,6 +35,7 @@ constexpr hipErr kOutOfMemory = 2;  // hipErrorOutOfMemory
 
 std::mutex g_mu;
 std::unordered_map<void*, size_t>* g_sizes = nullptr;
+std::unordered_map<void*, size_t>* g_handles = nullptr;  // hipMemCreate handles (VMM)
 std::atomic<size_t> g_live{0};
 std::atomic<size_t> g_peak{0};
 size_t g_limit = 0;
@@ -38,6 +45,7 @@ void init_once() {
   static std::once_flag once;
   std::call_once(once, [] {
     g_sizes = new std::unordered_map<void*, size_t>();
+    g_handles = new std::unordered_map<void*, size_t>();
     if (const char* v = std::getenv("NOS_HBM_LIMIT_BYTES")) g_limit = std::strtoull(v, nullptr, 10);
     g_loaded = true;
   });
@@ -125,7 +133,32 @@ hipErr guarded(void** ptr, size_t size, Alloc&& alloc) {
   return rc;
 }
 
+// Allocations whose size the runtime decides (pitched): allocate, then charge the real size; over
+// budget -> give the memory back and fail like a real out-of-memory.
+template <typename Alloc, typename Free>
+hipErr charged_after(void* p, size_t bytes, hipErr rc, Free&& free_fn) {
+  if (rc != kSuccess || p == nullptr) return rc;
+  if (!reserve(bytes)) {
+    free_fn();
+    return kOutOfMemory;
+  }
+  track(p, bytes);
+  return rc;
+}
+
 }  // namespace
+
+struct nos_pitched_ptr {  // hipPitchedPtr (driver_types.h:385)
+  void* ptr;
+  size_t pitch;
+  size_t xsize;
+  size_t ysize;
+};
+struct nos_extent {  // hipExtent (driver_types.h:394)
+  size_t width;
+  size_t height;
+  size_t depth;
+};
 
 extern "C" {
 
@@ -147,6 +180,88 @@ hipErr hipMallocAsync(void** ptr, size_t size, void* stream) {
 hipErr hipMallocManaged(void** ptr, size_t size, unsigned int flags) {
   static auto real = next<hipErr (*)(void**, size_t, unsigned int)>("hipMallocManaged");
   return guarded(ptr, size, [&] { return real(ptr, size, flags); });
+}
+
+hipErr hipMallocFromPoolAsync(void** ptr, size_t size, void* pool, void* stream) {
+  static auto real = next<hipErr (*)(void**, size_t, void*, void*)>("hipMallocFromPoolAsync");
+  return guarded(ptr, size, [&] { return real(ptr, size, pool, stream); });
+}
+
+hipErr hipMallocPitch(void** ptr, size_t* pitch, size_t width, size_t height) {
+  static auto real = next<hipErr (*)(void**, size_t*, size_t, size_t)>("hipMallocPitch");
+  static auto real_free = next<hipErr (*)(void*)>("hipFree");
+  init_once();
+  if (!reserve(width * height)) {  // cannot fit even unpadded: fail before touching the device
+    if (ptr) *ptr = nullptr;
+    return kOutOfMemory;
+  }
+  g_live -= width * height;
+  hipErr rc = real(ptr, pitch, width, height);
+  if (rc != kSuccess || !ptr || !pitch) return rc;
+  void* p = *ptr;
+  rc = charged_after<int>(p, *pitch * height, rc, [&] { real_free(p); });
+  if (rc != kSuccess) *ptr = nullptr;
+  return rc;
+}
+
+hipErr hipMalloc3D(nos_pitched_ptr* pp, nos_extent extent) {
+  static auto real = next<hipErr (*)(nos_pitched_ptr*, nos_extent)>("hipMalloc3D");
+  static auto real_free = next<hipErr (*)(void*)>("hipFree");
+  init_once();
+  const size_t minimum = extent.width * extent.height * (extent.depth ? extent.depth : 1);
+  if (!reserve(minimum)) {
+    if (pp) pp->ptr = nullptr;
+    return kOutOfMemory;
+  }
+  g_live -= minimum;
+  hipErr rc = real(pp, extent);
+  if (rc != kSuccess || !pp) return rc;
+  void* p = pp->ptr;
+  rc = charged_after<int>(p, pp->pitch * extent.height * (extent.depth ? extent.depth : 1), rc,
+                          [&] { real_free(p); });
+  if (rc != kSuccess) pp->ptr = nullptr;
+  return rc;
+}
+
+// Virtual memory management (PyTorch PYTORCH_HIP_ALLOC_CONF=expandable_segments:True): the
+// physical backing is created by hipMemCreate and returned by hipMemRelease; hipMemMap only maps
+// an existing handle, so the handle is what carries the bytes.
+hipErr hipMemCreate(void** handle, size_t size, const void* prop, unsigned long long flags) {
+  static auto real = next<hipErr (*)(void**, size_t, const void*, unsigned long long)>("hipMemCreate");
+  init_once();
+  if (!reserve(size)) return kOutOfMemory;
+  hipErr rc = real(handle, size, prop, flags);
+  if (rc != kSuccess || !handle || !*handle) {
+    g_live -= size;
+    return rc;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  (*g_handles)[*handle] = size;
+  size_t live = g_live.load();
+  if (live > g_peak.load()) g_peak = live;
+  return rc;
+}
+
+hipErr hipMemRelease(void* handle) {
+  static auto real = next<hipErr (*)(void*)>("hipMemRelease");
+  init_once();
+  size_t n = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_handles->find(handle);
+    if (it != g_handles->end()) {
+      n = it->second;
+      g_handles->erase(it);
+    }
+  }
+  const hipErr rc = real(handle);
+  if (rc == kSuccess) {
+    g_live -= n;
+  } else if (n) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    (*g_handles)[handle] = n;
+  }
+  return rc;
 }
 
 hipErr hipFree(void* ptr) {

@@ -27,6 +27,21 @@ int hipFree(void* p) {
   return 0;
 }
 int hipFreeAsync(void* p, void*) { return hipFree(p); }
+// pitched: rows padded to 256 B, like the real runtime's texture-aligned pitch
+int hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h) {
+  *pitch = (w + 255) / 256 * 256;
+  *p = std::malloc(*pitch * h);  // not through hipMalloc: the real runtime allocates internally
+  return *p ? 0 : 2;
+}
+struct FakeHandle { size_t n; };
+int hipMemCreate(void** handle, size_t n, const void*, unsigned long long) {
+  *handle = new FakeHandle{n};
+  return 0;
+}
+int hipMemRelease(void* handle) {
+  delete static_cast<FakeHandle*>(handle);
+  return 0;
+}
 int hipMemGetInfo(size_t* free_b, size_t* total_b) {
   *total_b = kTotal;
   *free_b = kTotal / 2;

@@ -12,6 +12,9 @@ extern "C" {
 int hipMalloc(void** p, size_t n);
 int hipFree(void* p);
 int hipMemGetInfo(size_t* free_b, size_t* total_b);
+int hipMallocPitch(void** p, size_t* pitch, size_t w, size_t h);
+int hipMemCreate(void** handle, size_t n, const void* prop, unsigned long long flags);
+int hipMemRelease(void* handle);
 size_t nos_hbm_limit_bytes();
 size_t nos_hbm_live_bytes();
 size_t nos_hbm_peak_bytes();
@@ -38,6 +41,20 @@ int main() {
   CHECK(hipMemGetInfo(&fr, &tot) == 0);
   CHECK(tot == limit && fr == limit - (size_t(16) << 20));
   CHECK(hipFree(p) == 0 && nos_hbm_live_bytes() == 0);
+  // pitched allocations are charged at pitch x height (the padded size the runtime chose)
+  size_t pitch = 0;
+  CHECK(hipMallocPitch(&p, &pitch, 1000, 1024) == 0 && p && pitch == 1024);
+  CHECK(nos_hbm_live_bytes() == size_t(1024) * 1024);
+  CHECK(hipFree(p) == 0 && nos_hbm_live_bytes() == 0);
+  CHECK(hipMallocPitch(&p, &pitch, 67100, 1000) == 2 && p == nullptr);  // fits unpadded, not padded
+  CHECK(nos_hbm_live_bytes() == 0);
+  // virtual-memory handles (expandable segments) carry their physical size until released
+  void* h1 = nullptr;
+  void* h2 = nullptr;
+  CHECK(hipMemCreate(&h1, size_t(48) << 20, nullptr, 0) == 0 && h1);
+  CHECK(hipMemCreate(&h2, size_t(32) << 20, nullptr, 0) == 2);
+  CHECK(hipMemRelease(h1) == 0 && nos_hbm_live_bytes() == 0);
+  CHECK(hipMemCreate(&h2, size_t(32) << 20, nullptr, 0) == 0 && hipMemRelease(h2) == 0);
   // concurrent random alloc/free: the live total never exceeds the budget
   std::atomic<int> oom{0};
   std::vector<std::thread> ts;

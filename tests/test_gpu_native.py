@@ -193,3 +193,68 @@ def test_agent_keeps_hip_in_spawned_helpers(gpu):
     db = r["direct_barrier"]
     assert db["ok"] is True and db["veto"] is False, db
     assert db["info"]["seen"] == r["devices"] and db["info"]["sum"] == r["devices"]
+
+
+ALLOCATED_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, %(root)r)
+from walkai_nos_amd.ops import probe as P
+pl = P.census(n_wg=4096, spin=4000)
+r = P.probe_mfma("bf16", iters=1024, reps=3)
+print(json.dumps({"cus": P.distinct_cus(pl), "xcds": sorted({p["xcc"] for p in pl}), "bf16": r.tflops,
+                  "mask": os.environ.get("HSA_CU_MASK")}))
+"""
+
+
+def test_device_plugin_allocate_env_enforces_cu_set_in_a_fresh_process(gpu):
+    """Allocate()'s HSA_CU_MASK + HBM env, applied to a fresh process exactly as kubelet would:
+    the census CU set equals the slice's rows and the probe rate scales with the slice."""
+    import json
+    import tempfile
+
+    from walkai_nos_amd.device.protos import dp
+    from walkai_nos_amd.device.slicing_client import MemorySliceStore
+    from walkai_nos_amd.deviceplugin.server import SliceDevicePlugin
+    from walkai_nos_amd.models.slicing.cumask import Slice
+    store = MemorySliceStore()
+    store.save({0: [Slice("g0::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9),
+                    Slice("g0::s1", "64cu.72gb", [4, 5, 6, 7, 8, 9, 10, 11], 72 * 10**9)]})
+    out = {}
+    for res, sid in (("amd.com/gpu-32cu.36gb", "g0::s0"), ("amd.com/gpu-64cu.72gb", "g0::s1")):
+        plug = SliceDevicePlugin(res, store, {0: "/dev/dri/renderD128"}, socket_dir=tempfile.gettempdir())
+        req = dp.AllocateRequest()
+        req.container_requests.add(devicesIDs=[sid])
+        envs = dict(plug.Allocate(req, None).container_responses[0].envs)
+        env = dict(os.environ)
+        env.update(envs)
+        env["LD_PRELOAD"] = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
+        p = subprocess.run([sys.executable, "-c", ALLOCATED_CHILD % {"root": ROOT}], env=env, capture_output=True,
+                           text=True, timeout=180)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out[sid] = json.loads(p.stdout.strip().splitlines()[-1])
+    s32, s64 = out["g0::s0"], out["g0::s1"]
+    assert s32["mask"] == "0:0-31" and s64["mask"] == "0:32-95"
+    assert s32["cus"] == 32 and s64["cus"] == 64, out
+    assert s32["xcds"] == list(range(8)) and s64["xcds"] == list(range(8))
+    assert 1.6 < s64["bf16"] / s32["bf16"] < 2.4, out
+
+
+def test_hbm_limit_shim_with_expandable_segments(gpu):
+    shim = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
+    code = ("import ctypes, torch\n"
+            "a = torch.empty(2**30, dtype=torch.uint8, device='cuda')\n"
+            "try:\n"
+            "    b = torch.empty(3 * 2**30, dtype=torch.uint8, device='cuda')\n"
+            "    print('NOT_ENFORCED')\n"
+            "except RuntimeError:\n"
+            "    print('ENFORCED')\n"
+            "lib = ctypes.CDLL(None)\n"
+            "lib.nos_hbm_peak_bytes.restype = ctypes.c_size_t\n"
+            "print('PEAK', lib.nos_hbm_peak_bytes())\n")
+    env = dict(os.environ, LD_PRELOAD=shim, NOS_HBM_LIMIT_BYTES=str(2 * 2**30),
+               PYTORCH_HIP_ALLOC_CONF="expandable_segments:True")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "ENFORCED" in p.stdout and "NOT_ENFORCED" not in p.stdout, p.stdout
+    peak = int(p.stdout.split("PEAK")[1].split()[0])
+    assert 2**30 <= peak <= 2 * 2**30, peak  # the 1 GiB segment was charged through hipMemCreate

@@ -15,7 +15,8 @@ from .native import load
 
 LIB = "libnos_probe.so"
 
-DTYPES = {"bf16": 0, "bf16_16x16": 1, "fp32": 2, "fp8": 3}
+DTYPES = {"bf16": 0, "bf16_16x16": 1, "fp32": 2, "fp8": 3, "fp8_scaled": 4}
+HBM_MODES = {"stride": 0, "slab_nt": 1, "slab": 2}
 
 
 class ProbeResult(ctypes.Structure):
@@ -39,6 +40,8 @@ def _lib() -> ctypes.CDLL:
                                      ctypes.c_int, ctypes.POINTER(ProbeResult)]
         L.nos_probe_hbm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(ProbeResult)]
+        L.nos_probe_hbm_mode.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ProbeResult)]
         L.nos_probe_census.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint32)]
         L.nos_probe_cu_count.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
@@ -124,7 +127,8 @@ class SliceProbe:
     def pct_of_clock_peak(self) -> float:
         """Achieved rate over the matrix-pipe peak at the measured clock (0 if unknown)."""
         # matrix-pipe FLOP per clock per CU
-        per_clk = {"bf16": 4096, "bf16_16x16": 4096, "fp32": 256, "fp8": 8192}.get(self.dtype, 0)
+        # (non-scaled fp8 MFMAs run at the bf16 rate; the block-scaled 32x32x64 form at twice it)
+        per_clk = {"bf16": 4096, "bf16_16x16": 4096, "fp32": 256, "fp8": 4096, "fp8_scaled": 8192}.get(self.dtype, 0)
         if not self.mhz or not per_clk:
             return 0.0
         return 100.0 * self.tflops * 1e12 / (per_clk * self.n_cus * self.mhz * 1e6)
@@ -141,11 +145,11 @@ def probe_mfma(dtype: str = "bf16", device: int = 0, stream: Optional[Stream] = 
 
 
 def probe_hbm(device: int = 0, stream: Optional[Stream] = None, nbytes: int = 1 << 30, n_wg: Optional[int] = None,
-              reps: int = 5) -> Dict[str, float]:
+              reps: int = 5, mode: str = "slab_nt") -> Dict[str, float]:
     n_cus = len(stream.cus) if stream is not None and stream.cus is not None else cu_count(device)
     r = ProbeResult()
-    _check(_lib().nos_probe_hbm(device, stream.handle if stream else None, nbytes, n_wg or n_cus * 8, reps,
-                                ctypes.byref(r)))
+    _check(_lib().nos_probe_hbm_mode(device, stream.handle if stream else None, nbytes, n_wg or n_cus * 4, reps,
+                                     HBM_MODES[mode], ctypes.byref(r)))
     return {"ms": r.ms, "gbps": r.rate, "bytes": r.flops, "n_cus": n_cus}
 
 
