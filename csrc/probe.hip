@@ -177,11 +177,10 @@ __global__ __launch_bounds__(kThreads) void hbm_copy(const uint4* __restrict__ s
 
 // Slab copy: each workgroup streams one contiguous slab (DRAM page locality; the grid-stride form
 // above makes every wave-instruction of a workgroup touch a different region of the buffer).
-template <bool NT>
+template <bool NT, int U>
 __global__ __launch_bounds__(kThreads) void hbm_copy_slab(const uint4* __restrict__ src, uint4* __restrict__ dst,
                                                           size_t n) {
   typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-  constexpr int U = 8;
   const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
   u32x4* d4 = reinterpret_cast<u32x4*>(dst);
   const size_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -362,7 +361,8 @@ int nos_probe_mfma(int device, void* stream, int dtype, int n_wg, int iters, int
   return 0;
 }
 
-// mode 0: grid-stride non-temporal copy; 1: slab, non-temporal; 2: slab, default cache policy
+// mode 0: grid-stride non-temporal copy; 1: slab, non-temporal, 8 loads in flight per lane;
+// 2: slab, default cache policy; 3: slab, non-temporal, 16 in flight; 4: slab, non-temporal, 4
 int nos_probe_hbm_mode(int device, void* stream, size_t bytes, int n_wg, int reps, int mode, nos_probe_result* res);
 
 int nos_probe_hbm(int device, void* stream, size_t bytes, int n_wg, int reps, nos_probe_result* res) {
@@ -384,9 +384,13 @@ int nos_probe_hbm_mode(int device, void* stream, size_t bytes, int n_wg, int rep
     if (mode == 0)
       hipLaunchKernelGGL(hbm_copy, dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
     else if (mode == 1)
-      hipLaunchKernelGGL(hbm_copy_slab<true>, dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+      hipLaunchKernelGGL((hbm_copy_slab<true, 8>), dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+    else if (mode == 2)
+      hipLaunchKernelGGL((hbm_copy_slab<false, 8>), dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+    else if (mode == 3)
+      hipLaunchKernelGGL((hbm_copy_slab<true, 16>), dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
     else
-      hipLaunchKernelGGL(hbm_copy_slab<false>, dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
+      hipLaunchKernelGGL((hbm_copy_slab<true, 4>), dim3(n_wg), dim3(kThreads), 0, s, a, b, n);
   };
   launch();
   int rc = check(hipStreamSynchronize(s), "hbm warm-up");

@@ -109,3 +109,60 @@ def test_two_namespaces_borrow_and_reclaim_on_eight_gpus():
     assert c.nos_scheduler.preempted >= 4
     assert len([p for p in c.running_pods() if ko.namespace(p) == "team-a"]) == 12
     assert c.utilization() == 100.0
+
+
+# -- default filter plugins (ref docs/en/docs/elastic-resource-quota/configuration.md:19-42) ----
+def _node(name, labels=None, taints=None, unschedulable=False):
+    n = ko.new_node(name, labels or {}, allocatable={"cpu": "8", "memory": "8Gi", "pods": "10",
+                                                     "amd.com/cpx_nps1": "8"})
+    if taints:
+        n.setdefault("spec", {})["taints"] = taints
+    if unschedulable:
+        n.setdefault("spec", {})["unschedulable"] = True
+    return n
+
+
+def test_filters_taints_selectors_affinity():
+    from walkai_nos_amd.quota.filters import filter_node, tolerates
+    pod = ko.new_pod("p", "default", requests={"amd.com/cpx_nps1": 1})
+    gpu_taint = {"key": "amd.com/gpu", "value": "present", "effect": "NoSchedule"}
+    assert filter_node(pod, _node("a"))[0]
+    assert not filter_node(pod, _node("a", taints=[gpu_taint]))[0]
+    assert filter_node(pod, _node("a", taints=[dict(gpu_taint, effect="PreferNoSchedule")]))[0]
+    pod["spec"]["tolerations"] = [{"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}]
+    assert filter_node(pod, _node("a", taints=[gpu_taint]))[0]
+    assert tolerates({"operator": "Exists"}, gpu_taint)                          # tolerate-everything
+    assert not tolerates({"key": "amd.com/gpu", "value": "absent"}, gpu_taint)   # Equal needs the value
+    assert not filter_node(pod, _node("a", unschedulable=True))[0]
+    pod["spec"]["nodeSelector"] = {"pool": "mi355x"}
+    assert not filter_node(pod, _node("a"))[0]
+    assert filter_node(pod, _node("a", {"pool": "mi355x"}))[0]
+    del pod["spec"]["nodeSelector"]
+    pod["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+        "nodeSelectorTerms": [
+            {"matchExpressions": [{"key": "zone", "operator": "In", "values": ["z1", "z2"]},
+                                  {"key": "gpus", "operator": "Gt", "values": ["4"]}]},
+            {"matchFields": [{"key": "metadata.name", "operator": "In", "values": ["special"]}]}]}}}
+    assert filter_node(pod, _node("a", {"zone": "z2", "gpus": "8"}))[0]
+    assert not filter_node(pod, _node("a", {"zone": "z2", "gpus": "2"}))[0]
+    assert not filter_node(pod, _node("a", {"zone": "z3", "gpus": "8"}))[0]
+    assert filter_node(pod, _node("special"))[0]                                 # second term (OR)
+
+
+def test_nos_scheduler_respects_taints_and_selectors():
+    from walkai_nos_amd.quota.scheduler import SCHEDULER_NAME, NosScheduler
+    api = InMemoryAPIServer()
+    api.create(_node("tainted", {"pool": "a"}, taints=[{"key": "dedicated", "value": "x", "effect": "NoSchedule"}]))
+    api.create(_node("plain", {"pool": "b"}))
+    s = NosScheduler(api)
+    p = ko.new_pod("sel", "default", requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME)
+    p["spec"]["nodeSelector"] = {"pool": "a"}
+    api.create(p)
+    s.reconcile(NosScheduler.KEY)
+    pod = api.get("Pod", "sel", "default")
+    assert not ko.pod_node_name(pod)                      # only the tainted node matches the selector
+    assert "untolerated taint" in pod["status"]["conditions"][0]["message"]
+    api.patch("Pod", "sel", {"spec": {"tolerations": [{"key": "dedicated", "operator": "Equal", "value": "x",
+                                                       "effect": "NoSchedule"}]}}, "default")
+    s.reconcile(NosScheduler.KEY)
+    assert ko.pod_node_name(api.get("Pod", "sel", "default")) == "tainted"

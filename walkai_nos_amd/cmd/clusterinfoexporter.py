@@ -40,7 +40,7 @@ def main(argv=None) -> int:
     interval = parse_duration(args.interval)
     if interval <= 0:
         interval = 60.0
-    ex = Exporter(Collector(make_client(args.kubeconfig)), args.endpoint, args.api_token,
+    ex = Exporter(Collector(make_client(args.kubeconfig, cached=False)), args.endpoint, args.api_token,
                   parse_duration(args.http_timeout))
     stop = threading.Event()
     while not stop.is_set():

@@ -30,11 +30,16 @@ def setup_logging(level: str) -> None:
                         format='{"ts":"%(asctime)s","level":"%(levelname)s","logger":"%(name)s","msg":"%(message)s"}')
 
 
-def make_client(kubeconfig: str = "") -> Any:
+def make_client(kubeconfig: str = "", cached: Any = True) -> Any:
+    """REST client for the cluster; reconcilers read through an informer cache, like
+    controller-runtime's manager client.  ``cached``: True (the default kinds), a tuple of kinds
+    (node agents cache only Nodes), or False (periodic exporters list on demand)."""
+    from ..kube.cache import DEFAULT_CACHED, CachedClient
     from ..kube.rest import RESTClient, from_kubeconfig
-    if kubeconfig:
-        return from_kubeconfig(kubeconfig)
-    return RESTClient.in_cluster()
+    rest = from_kubeconfig(kubeconfig) if kubeconfig else RESTClient.in_cluster()
+    if not cached:
+        return rest
+    return CachedClient(rest, DEFAULT_CACHED if cached is True else tuple(cached))
 
 
 def make_manager(client: Any, cfg: ManagerConfig, component: str) -> Manager:

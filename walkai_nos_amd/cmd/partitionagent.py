@@ -40,7 +40,7 @@ def main(argv=None) -> int:
     setup_logging(args.log_level)
     cfg = load_config_file(args.config, "MigAgentConfig") if args.config else MigAgentConfig()
     node = get_env_or_panic(constant.ENV_NODE_NAME)
-    client = make_client(args.kubeconfig)
+    client = make_client(args.kubeconfig, cached=("Node",))
     smi = new_backend(cfg.amdSmiBackend)
     gpus = smi.list_gpus()
     if not gpus:

@@ -3,7 +3,11 @@
 Implements the same interface as :class:`~walkai_nos_amd.kube.memory.InMemoryAPIServer` — get,
 list (label/field selectors), create, update, merge patch, delete, bind and watch — so every
 controller runs unchanged against a real API server.  Credentials come from the in-cluster service
-account (``/var/run/secrets/kubernetes.io/serviceaccount``) or a kubeconfig token/server pair.
+account (``/var/run/secrets/kubernetes.io/serviceaccount``) or a kubeconfig: server, CA (file or
+inline ``-data``), and a bearer token (inline or ``tokenFile``) or a client certificate/key pair
+(files or inline ``-data``, the ``kind``/kubeadm default).  Reads of long-running components go
+through :class:`~walkai_nos_amd.kube.cache.CachedClient` (an informer cache in front of this
+client), as controller-runtime's reconcilers read from theirs.
 Watches are long-poll HTTP streams (``?watch=1``) consumed on a daemon thread per kind, with
 re-list on ``410 Gone``.
 
@@ -46,15 +50,18 @@ RESOURCES: Dict[str, Tuple[str, str, bool]] = {
 
 class RESTClient:
     def __init__(self, server: str, token: str = "", ca_file: Optional[str] = None, insecure: bool = False,
-                 timeout: float = 30.0):
+                 timeout: float = 30.0, cert_file: Optional[str] = None, key_file: Optional[str] = None):
         self.server = server.rstrip("/")
         self.token = token
         self.timeout = timeout
+        self.cert_file = cert_file
         if self.server.startswith("https"):
             ctx = ssl.create_default_context(cafile=ca_file) if ca_file else ssl.create_default_context()
             if insecure:
                 ctx.check_hostname = False
                 ctx.verify_mode = ssl.CERT_NONE
+            if cert_file:
+                ctx.load_cert_chain(cert_file, key_file)  # mutual TLS (client-certificate users)
             self._ctx: Optional[ssl.SSLContext] = ctx
         else:
             self._ctx = None
@@ -198,15 +205,42 @@ class RESTClient:
             s.set()
 
 
-def from_kubeconfig(path: str) -> RESTClient:
-    """Minimal kubeconfig support: current-context cluster server + CA + user token."""
+def _materialize(data_b64: Optional[str], path: Optional[str], base: str, suffix: str) -> Optional[str]:
+    """A kubeconfig credential as a file path: inline ``*-data`` (base64) is written to a private
+    temporary file (ssl only loads certificates from files); relative paths resolve against the
+    kubeconfig's directory, as kubectl does."""
+    import base64
+    import tempfile
+    if data_b64:
+        fd, name = tempfile.mkstemp(prefix="nos-kube-", suffix=suffix)
+        with os.fdopen(fd, "wb") as f:
+            f.write(base64.b64decode(data_b64))
+        os.chmod(name, 0o600)
+        return name
+    if path:
+        return path if os.path.isabs(path) else os.path.join(base, path)
+    return None
+
+
+def from_kubeconfig(path: str, context: Optional[str] = None) -> RESTClient:
+    """kubeconfig support: the (current) context's cluster server, CA (file or inline data) and
+    user credentials — bearer token (inline or ``tokenFile``) or client certificate + key (files or
+    inline data)."""
     import yaml
     with open(path) as f:
         cfg = yaml.safe_load(f)
-    ctx_name = cfg.get("current-context")
+    base = os.path.dirname(os.path.abspath(path))
+    ctx_name = context or cfg.get("current-context")
     ctx = next(c["context"] for c in cfg["contexts"] if c["name"] == ctx_name)
     cluster = next(c["cluster"] for c in cfg["clusters"] if c["name"] == ctx["cluster"])
-    user = next(u["user"] for u in cfg["users"] if u["name"] == ctx["user"])
-    return RESTClient(cluster["server"], user.get("token", ""), cluster.get("certificate-authority"),
-                      insecure=bool(cluster.get("insecure-skip-tls-verify")))
+    user = next((u["user"] for u in cfg.get("users", []) if u["name"] == ctx.get("user")), {}) or {}
+    token = user.get("token", "")
+    if not token and user.get("tokenFile"):
+        with open(_materialize(None, user["tokenFile"], base, "")) as f:
+            token = f.read().strip()
+    ca = _materialize(cluster.get("certificate-authority-data"), cluster.get("certificate-authority"), base, ".crt")
+    cert = _materialize(user.get("client-certificate-data"), user.get("client-certificate"), base, ".crt")
+    key = _materialize(user.get("client-key-data"), user.get("client-key"), base, ".key")
+    return RESTClient(cluster["server"], token, ca, insecure=bool(cluster.get("insecure-skip-tls-verify")),
+                      cert_file=cert, key_file=key)
 

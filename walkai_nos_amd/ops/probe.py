@@ -16,7 +16,7 @@ from .native import load
 LIB = "libnos_probe.so"
 
 DTYPES = {"bf16": 0, "bf16_16x16": 1, "fp32": 2, "fp8": 3, "fp8_scaled": 4}
-HBM_MODES = {"stride": 0, "slab_nt": 1, "slab": 2}
+HBM_MODES = {"stride": 0, "slab_nt": 1, "slab": 2, "slab_nt16": 3, "slab_nt4": 4}
 
 
 class ProbeResult(ctypes.Structure):
@@ -148,7 +148,9 @@ def probe_hbm(device: int = 0, stream: Optional[Stream] = None, nbytes: int = 1 
               reps: int = 5, mode: str = "slab_nt") -> Dict[str, float]:
     n_cus = len(stream.cus) if stream is not None and stream.cus is not None else cu_count(device)
     r = ProbeResult()
-    _check(_lib().nos_probe_hbm_mode(device, stream.handle if stream else None, nbytes, n_wg or n_cus * 4, reps,
+    # default: one slab-copy workgroup per CU, non-temporal (best of the tools/hbm_sweep.py sweep,
+    # profiles/hbm_sweep_r2.json: 6.1 TB/s on a 16 GiB copy; more workgroups per CU thrash DRAM pages)
+    _check(_lib().nos_probe_hbm_mode(device, stream.handle if stream else None, nbytes, n_wg or n_cus, reps,
                                      HBM_MODES[mode], ctypes.byref(r)))
     return {"ms": r.ms, "gbps": r.rate, "bytes": r.flops, "n_cus": n_cus}
 

@@ -8,8 +8,10 @@ with the same extension points:
 
 * **PreFilter** — the pod's quota (by namespace) must not exceed ``max``; above ``min`` it may only
   *borrow* while the cluster has unused guaranteed quota (sum used + req <= sum min);
-* **Filter** — NodeResourcesFit on every requested resource (allocatable minus the requests of the
-  pods bound to the node, terminal pods excluded), extended resources included;
+* **Filter** — the default kube-scheduler filters that still run next to the plugin in the
+  reference's profile (``quota/filters.py``: NodeUnschedulable, NodeSelector, NodeAffinity,
+  TaintToleration), then NodeResourcesFit on every requested resource (allocatable minus the
+  requests of the pods bound to the node, terminal pods excluded), extended resources included;
 * **Score** — most-allocated on GPU resources (bin packing keeps whole GPUs free for mode flips);
 * **PostFilter** — preemption: on each node, victims are over-quota pods of quotas the preemptor
   may reclaim from under the fair-share rule, or lower-priority pods of the same quota; the node
@@ -30,6 +32,7 @@ from ..models import resource as res
 from ..utils import pod as podutil
 from ..utils.metrics import REGISTRY
 from .elasticquota import QuotaInfo, QuotaSet, capacity_labels, compute_used
+from .filters import feasible_nodes
 from .gpu_memory import GpuMemoryCalculator
 from .operator import list_quotas
 
@@ -44,6 +47,7 @@ class CycleState:
     node_free: Dict[str, Dict[str, int]]
     node_pods: Dict[str, List[Dict[str, Any]]]
     requests: Dict[str, Dict[str, int]] = field(default_factory=dict)
+    nodes: Dict[str, Dict[str, Any]] = field(default_factory=dict)
 
 
 def _pkey(p: Dict[str, Any]) -> str:
@@ -138,15 +142,17 @@ class NosScheduler:
                                                    self.calc.pod_request).items() if r in q.resources()}
         node_free: Dict[str, Dict[str, int]] = {}
         node_pods: Dict[str, List[Dict[str, Any]]] = {}
+        nodes: Dict[str, Dict[str, Any]] = {}
         for n in self.client.list("Node"):
             node_free[ko.name(n)] = res.from_k8s(ko.node_allocatable(n))
             node_pods[ko.name(n)] = []
+            nodes[ko.name(n)] = n
         for p in pods:
             nn = ko.pod_node_name(p)
             if nn in node_free and not podutil.is_terminated(p):
                 node_free[nn] = res.subtract(node_free[nn], res.compute_pod_request(p))
                 node_pods[nn].append(p)
-        return CycleState(QuotaSet(quotas), node_free, node_pods)
+        return CycleState(QuotaSet(quotas), node_free, node_pods, nodes=nodes)
 
     @staticmethod
     def fits(req: Dict[str, int], free: Dict[str, int]) -> bool:
@@ -179,12 +185,16 @@ class NosScheduler:
                 self._mark_unschedulable(pod, why)
                 continue
             req_ = res.compute_pod_request(pod)
-            feasible = [n for n, free in state.node_free.items() if self.fits(req_, free)]
+            allowed, reasons = feasible_nodes(pod, list(state.nodes.values()))
+            allowed_names = {ko.name(n) for n in allowed}
+            feasible = [n for n, free in state.node_free.items() if n in allowed_names and self.fits(req_, free)]
             if not feasible:
-                if self._preempt(state, pod):
+                if allowed_names and self._preempt(state, pod, allowed_names):
                     retry = True
                 else:
-                    self._mark_unschedulable(pod, f"0/{len(state.node_free)} nodes are available")
+                    why = ", ".join(f"{c} {r}" for r, c in sorted(reasons.items()))
+                    self._mark_unschedulable(pod, f"0/{len(state.node_free)} nodes are available" +
+                                             (f": {why}" if why else ""))
                 continue
             node = min(feasible, key=lambda n: self.score(n, state.node_free[n], req_, state))
             self.plugin.reserve(state, pod)
@@ -199,9 +209,12 @@ class NosScheduler:
                 self.on_bind(pod, node)
         return Result(requeue_after=1.0) if retry else Result()
 
-    def _preempt(self, state: CycleState, pod: Dict[str, Any]) -> bool:
+    def _preempt(self, state: CycleState, pod: Dict[str, Any], allowed: Optional[set] = None) -> bool:
+        """Victims only on nodes the pod may run on at all (preemption cannot fix a taint)."""
         best: Optional[Tuple[int, str, List[Dict[str, Any]]]] = None
         for node in sorted(state.node_free):
+            if allowed is not None and node not in allowed:
+                continue
             victims = self.plugin.victims_on_node(state, pod, node, self.fits)
             if victims is not None and (best is None or len(victims) < best[0]):
                 best = (len(victims), node, victims)

@@ -41,6 +41,7 @@ from ..models.xcp.profile import COMPUTE_MODES, extract_profile_name, is_xcp_res
 def is_managed(r: str) -> bool:
     return is_xcp_resource(r) or is_slice_resource(r)
 from ..parallel.barrier import LocalBarrier
+from ..quota.filters import filter_node
 from ..utils import pod as podutil
 
 log = logging.getLogger("nos.sim")
@@ -176,11 +177,13 @@ class SimScheduler:
                 if not podutil.is_scheduled(p)
                 and p["spec"].get("schedulerName", "default-scheduler") == "default-scheduler"]
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
-        draining = {n.name: draining_gpus(self.api.get("Node", n.name)) for n in self.nodes.values()}
+        node_objs = {n.name: self.api.get("Node", n.name) for n in self.nodes.values()}
+        draining = {name: draining_gpus(o) for name, o in node_objs.items()}
         for p in pods:
             reqs = res.compute_pod_request(p)
             order = sorted(self.nodes.values(), key=lambda n: (-len(n.kubelet.allocations), n.name))
-            target = next((n for n in order if n.kubelet.can_fit(reqs, draining[n.name])), None)
+            target = next((n for n in order if filter_node(p, node_objs[n.name])[0]
+                           and n.kubelet.can_fit(reqs, draining[n.name])), None)
             if target is None:
                 if not podutil.is_unschedulable(p):
                     st = {"conditions": [{"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
