@@ -19,9 +19,7 @@ test-gpu: native   ## GPU test suite (MI355X)
 	$(PYTHON) -m pytest tests/ -x -q -m gpu
 
 lint:
-	$(PYTHON) -m ruff check walkai_nos_amd tests || true
-	$(PYTHON) -m compileall -q walkai_nos_amd tests
-	$(PYTHON) hack/check_headers.py
+	$(PYTHON) hack/lint.py
 
 sanitize:          ## host-code sanitizers (ASan+UBSan, TSan) over the HBM-limit shim's self-test
 	$(PYTHON) -m pytest tests/test_native_sanitizers.py -q

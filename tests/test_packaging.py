@@ -147,3 +147,55 @@ def test_every_source_file_has_a_header():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, os.path.join(root, "hack", "check_headers.py")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout
+
+
+def test_helm_install_guards_and_telemetry_identity():
+    val = open(_p("helm-charts/nos/templates/validation.yaml")).read()
+    assert 'eq .Release.Namespace "default"' in val and "fail" in val
+    inst = open(_p("helm-charts/nos/templates/telemetry/installation.yaml")).read()
+    # the UUID is looked up and reused, kept on uninstall, and nodes are looked up for the payload
+    assert 'lookup "v1" "ConfigMap"' in inst and "helm.sh/resource-policy: keep" in inst
+    assert 'lookup "v1" "Node"' in inst and "node.kubernetes.io/instance-type" in inst
+    for key in ("installationUUID", "nodes:", "chartValues:", "nosGpuPartitioner", "nosScheduler", "nosOperator"):
+        assert key in inst
+    job = open(_p("helm-charts/nos/templates/telemetry/job.yaml")).read()
+    assert "nos-telemetry-metrics" in job and "uuidv4" not in job
+
+
+def test_metrics_behind_kube_rbac_proxy_and_optional_service_monitor():
+    dep = open(_p("helm-charts/nos/templates/gpu-partitioner/deployment.yaml")).read()
+    assert "kube-rbac-proxy" in dep and "--upstream=http://127.0.0.1:8080/" in dep
+    cm = open(_p("helm-charts/nos/templates/gpu-partitioner/configmap.yaml")).read()
+    assert '"127.0.0.1:8080"' in cm
+    met = open(_p("helm-charts/nos/templates/gpu-partitioner/metrics.yaml")).read()
+    assert "tokenreviews" in met and "subjectaccessreviews" in met and "nonResourceURLs: [/metrics]" in met
+    assert "kind: ServiceMonitor" in met and ".Values.gpuPartitioner.metrics.serviceMonitor.enabled" in met
+    k = yaml.safe_load(open(_p("config/gpupartitioner/kustomization.yaml")))
+    assert "auth_proxy.yaml" in k["resources"] and k["patches"][0]["path"] == "auth_proxy_patch.yaml"
+    cfg = yaml.safe_load(open(_p("config/gpupartitioner/gpu_partitioner_config.yaml")))
+    assert cfg["metricsBindAddress"] == "127.0.0.1:8080"
+    mon = yaml.safe_load(open(_p("config/prometheus/monitor.yaml")))
+    assert mon["kind"] == "ServiceMonitor" and mon["spec"]["endpoints"][0]["port"] == "https"
+
+
+def test_lint_is_clean_and_fails_on_errors(tmp_path):
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, _p("hack/lint.py")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    bad = tmp_path / "bad.py"
+    bad.write_text("import os\n\ntry:\n    pass\nexcept:\n    pass\n")
+    sys.path.insert(0, _p("hack"))
+    import lint
+    errs = lint.check_file(str(bad))
+    assert any("unused import os" in e for e in errs) and any("bare except" in e for e in errs)
+
+
+def test_native_libraries_are_stamped_with_their_source_hash():
+    from walkai_nos_amd.ops import build as b
+    from walkai_nos_amd.ops import native
+    for t in b.TARGETS:
+        if native.available(t.name):
+            assert b.verify(t.name) == t.source_hash()
+    t = b.target("libnos_probe.so")
+    assert t.source_hash() != b.Target("x", ["probe.hip"], "hipcc", flags=["-DX"]).source_hash()

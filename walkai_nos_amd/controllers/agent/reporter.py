@@ -18,7 +18,6 @@ from ...kube import objects as ko
 from ...kube.errors import NotFound
 from ...kube.memory import create_merge_patch
 from ...kube.runtime import Request, Result
-from ...models import annotation as ann
 from ...models.xcp.profile import extract_profile_name
 from .shared import SharedState
 

@@ -350,6 +350,12 @@ class NativeAmdSmi(AmdSmi):
         path = lib_path or native_library_path()
         if not os.path.exists(path):
             raise GpuError(f"native amd-smi backend not built: {path} (run __graft_entry__.build())")
+        if lib_path is None and os.environ.get("NOS_ALLOW_STALE_NATIVE") != "1":
+            from ..ops.build import verify
+            try:
+                verify("libnos_amdsmi.so")
+            except RuntimeError as e:
+                raise GpuError(str(e)) from None
         self._lib = ctypes.CDLL(path)
         L = self._lib
         L.nos_smi_init.restype = ctypes.c_int

@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import logging
 import time
-from typing import Dict, List, Optional
+from typing import Dict, Optional
 
 from ..models.device import STATUS_FREE, DeviceList, GpuDevice
 from ..models.errors import GpuError

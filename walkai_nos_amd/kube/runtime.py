@@ -23,7 +23,7 @@ import heapq
 import logging
 import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 from ..utils.metrics import REGISTRY, Metrics

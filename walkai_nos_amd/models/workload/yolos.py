@@ -27,7 +27,7 @@ image is resized by the YOLOS processor to 800x1066 (shortest edge 800) -> 50x66
 from __future__ import annotations
 
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
 import torch

@@ -3,11 +3,19 @@
 One target per concern: the amd-smi backend (C++), the slice probe (HIP), the
 CU-mask/HBM-limit shim (C++, ``LD_PRELOAD``), the RCCL commit barrier (C++), and the fused
 workload kernels (HIP).  Outputs land in ``walkai_nos_amd/_native/`` so they travel to the GPU box
-with the ``gpurun`` snapshot.  Rebuilds only when a source is newer than its library.
+with the ``gpurun`` snapshot.
+
+Every library is **stamped** with a SHA-256 over its sources, headers, compiler command and this
+file (``<lib>.stamp``, JSON).  A library is rebuilt when the stamp is missing or differs — never by
+mtime, which a copied tree does not preserve — and :func:`walkai_nos_amd.ops.native.load` refuses
+a library whose stamp no longer matches the sources next to it, so a GPU run can never execute a
+stale build silently; ``__graft_entry__.build()`` prints the stamps it built or verified.
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -35,12 +43,35 @@ class Target:
     def out(self) -> str:
         return os.path.join(OUT, self.name)
 
+    @property
+    def stamp_path(self) -> str:
+        return self.out + ".stamp"
+
+    def source_hash(self) -> str:
+        """SHA-256 over sources + headers (+ every csrc header the sources may include) and the
+        build recipe (compiler command, this file)."""
+        h = hashlib.sha256()
+        deps = sorted(set(self.sources + self.headers + [f for f in os.listdir(CSRC) if f.endswith((".h", ".hpp"))]))
+        for d in deps:
+            path = os.path.join(CSRC, d)
+            if os.path.exists(path):
+                h.update(d.encode())
+                with open(path, "rb") as f:
+                    h.update(f.read())
+        h.update(" ".join(self.command()[1:]).encode())
+        with open(os.path.abspath(__file__), "rb") as f:
+            h.update(f.read())
+        return h.hexdigest()
+
+    def read_stamp(self) -> dict:
+        try:
+            with open(self.stamp_path) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return {}
+
     def stale(self) -> bool:
-        if not os.path.exists(self.out):
-            return True
-        t = os.path.getmtime(self.out)
-        deps = [os.path.join(CSRC, s) for s in self.sources + self.headers] + [os.path.abspath(__file__)]
-        return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+        return not os.path.exists(self.out) or self.read_stamp().get("sha256") != self.source_hash()
 
     def command(self) -> List[str]:
         srcs = [os.path.join(CSRC, s) for s in self.sources]
@@ -73,6 +104,8 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 4) -> List[str]
         p = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"building {t.name} failed:\n{' '.join(cmd)}\n{p.stderr[-4000:]}")
+        with open(t.stamp_path, "w") as f:
+            json.dump({"library": t.name, "sha256": t.source_hash(), "arch": ARCH, "sources": t.sources}, f)
         return t.name
 
     built: List[str] = []
@@ -82,6 +115,20 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 4) -> List[str]
             if verbose:
                 print(f"[nos build] {name}", file=sys.stderr)
     return built
+
+
+def target(name: str) -> Target:
+    return next(t for t in TARGETS if t.name == name)
+
+
+def verify(name: str) -> str:
+    """The stamp hash of a built library; raises if it does not match the current sources."""
+    t = target(name)
+    want, got = t.source_hash(), t.read_stamp().get("sha256")
+    if got != want:
+        raise RuntimeError(f"{name} is stale: built from {str(got)[:12]}, sources are {want[:12]} — rebuild with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'`")
+    return want
 
 
 if __name__ == "__main__":

@@ -39,6 +39,12 @@ def load(name: str) -> ctypes.CDLL:
         if not os.path.exists(p):
             raise NativeUnavailable(f"native library {name} is not built ({p}); run `python -c "
                                     f"'import __graft_entry__ as g; g.build()'` from the repo root")
+        if os.environ.get("NOS_ALLOW_STALE_NATIVE") != "1":
+            from .build import verify
+            try:
+                verify(name)  # the library must be the build of the sources next to it
+            except (RuntimeError, StopIteration) as e:
+                raise NativeUnavailable(str(e)) from None
         lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
         _libs[name] = lib
         return lib
