@@ -146,7 +146,7 @@ def modes_bench(a) -> int:
         if prof.split("_")[0] not in a.slices.split(","):
             continue
         n = min(n, a.partitions) if a.partitions else n
-        slots = [Slot(prof, k, 0, cfg, template) for k in range(n)]
+        slots = [Slot(slice_cus(prof, k), 0, cfg, template, seed=k) for k in range(n)]
         for sl in slots:
             sl.warm()
         torch.cuda.synchronize()
@@ -154,12 +154,11 @@ def modes_bench(a) -> int:
         rounds = 3
         t0 = time.perf_counter()
         for _ in range(rounds):
-            evs = []
             for sl in slots:
-                sl.run(work)
-                evs.append(sl.mark())
-            for ev in evs:
-                ev.synchronize()
+                for _ in range(work):
+                    sl.submit()
+            for sl in slots:
+                sl.drain()
         dt = time.perf_counter() - t0
         r = {"mode": prof, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
              "ms_per_round": round(1000 * dt / rounds, 2)}

@@ -58,7 +58,10 @@ class Target:
                 h.update(d.encode())
                 with open(path, "rb") as f:
                     h.update(f.read())
-        h.update(" ".join(self.command()[1:]).encode())
+        # the recipe without machine-specific paths: the tree is built here and run from another
+        # checkout path on the GPU box
+        recipe = " ".join(self.command()[1:]).replace(CSRC, "<csrc>").replace(OUT, "<out>").replace(ROOT, "<root>")
+        h.update(recipe.encode())
         with open(os.path.abspath(__file__), "rb") as f:
             h.update(f.read())
         return h.hexdigest()
