@@ -244,6 +244,29 @@ int nos_smi_activity(uint32_t idx, uint32_t* gfx, uint32_t* umc, uint32_t* mm) {
   return 0;
 }
 
+// Socket power (W), its limit (W) and the current / max GFX clock (MHz): a fully busy MI355X is
+// power-capped and clocks its matrix pipes down (profiles/clock_under_mfma_load_r2.json), which
+// is what bounds the aggregate throughput of concurrently busy partitions.
+int nos_smi_power_clock(uint32_t idx, uint32_t* watts, uint32_t* limit_w, uint32_t* gfx_mhz, uint32_t* gfx_max_mhz) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (int rc = handle(idx, &h)) return rc;
+  *watts = *limit_w = *gfx_mhz = *gfx_max_mhz = 0;
+  amdsmi_power_info_t p;
+  int rc = map_status(amdsmi_get_power_info(h, &p), "amdsmi_get_power_info");
+  if (rc == 0) {
+    *watts = p.current_socket_power != 0xFFFFFFFFu ? p.current_socket_power
+                                                    : (p.average_socket_power != 0xFFFFFFFFu ? p.average_socket_power : 0);
+    *limit_w = p.power_limit != 0xFFFFFFFFu ? p.power_limit : 0;
+  }
+  amdsmi_clk_info_t c;
+  if (amdsmi_get_clock_info(h, AMDSMI_CLK_TYPE_GFX, &c) == AMDSMI_STATUS_SUCCESS) {
+    *gfx_mhz = c.clk;
+    *gfx_max_mhz = c.max_clk;
+  }
+  return rc;
+}
+
 int nos_smi_vram(uint32_t idx, uint64_t* total, uint64_t* used) {
   std::lock_guard<std::mutex> lk(g_mu);
   amdsmi_processor_handle h;

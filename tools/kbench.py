@@ -151,7 +151,10 @@ def modes_bench(a) -> int:
             sl.warm()
         torch.cuda.synchronize()
         work = 8 // n
-        rounds = 3
+        rounds = 6
+        from walkai_nos_amd.bench_core import HwBusySampler
+        sampler = HwBusySampler(0, period=0.02)
+        sampler.start()
         t0 = time.perf_counter()
         for _ in range(rounds):
             for sl in slots:
@@ -160,8 +163,9 @@ def modes_bench(a) -> int:
             for sl in slots:
                 sl.drain()
         dt = time.perf_counter() - t0
+        busy = sampler.stop()
         r = {"mode": prof, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
-             "ms_per_round": round(1000 * dt / rounds, 2)}
+             "ms_per_round": round(1000 * dt / rounds, 2), "hw_busy_pct": busy, **sampler.power_summary()}
         print(json.dumps(r), flush=True)
         results.append(r)
         for sl in slots:

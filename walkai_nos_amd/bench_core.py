@@ -297,6 +297,7 @@ class HwBusySampler:
 
     def __init__(self, hip_device: int, period: float = 0.1):
         self.samples: List[float] = []
+        self.power: List[Dict[str, float]] = []
         self.period = period
         self._stop = threading.Event()
         self._t: Optional[threading.Thread] = None
@@ -313,6 +314,7 @@ class HwBusySampler:
         while not self._stop.wait(self.period):
             try:
                 self.samples.append(self.smi.activity(self.gpu)["gfx"])
+                self.power.append(self.smi.power_clock(self.gpu))
             except Exception as e:  # noqa: BLE001
                 self.error = str(e)[:200]
                 return
@@ -327,6 +329,12 @@ class HwBusySampler:
         if self._t is not None:
             self._t.join()
         return round(sum(self.samples) / len(self.samples), 1) if self.samples else None
+
+    def power_summary(self) -> Dict[str, float]:
+        if not self.power:
+            return {}
+        keys = self.power[0].keys()
+        return {f"mean_{k}": round(sum(p[k] for p in self.power) / len(self.power), 1) for k in keys}
 
 
 class NodeBench:
@@ -593,6 +601,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "hw_busy_pct": hw_busy,
         "hw_busy_source": "amd-smi gfx_activity, sampled every 100 ms in the timed window" if hw_busy is not None
         else f"unavailable: {busy.error}",
+        "hw_power_clock": busy.power_summary(),
         "pods_per_node": round(pods, 2),
         "pods_per_gpu": round(pods / cfg.gpus, 2),
         "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},

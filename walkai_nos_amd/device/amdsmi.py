@@ -89,6 +89,9 @@ class AmdSmi:
     def _vram_usage(self, proc: ProcInfo) -> Dict[str, int]:
         raise NotImplementedError
 
+    def _power_clock(self, proc: ProcInfo) -> Dict[str, float]:
+        return {}
+
     # -- device map -------------------------------------------------------------------------------
     def enumerate(self, reinit: bool = True) -> DeviceMap:
         """Re-read every processor and rebuild the physical <-> logical map."""
@@ -190,6 +193,10 @@ class AmdSmi:
         members = self._members(index)
         used = sum(self._vram_usage(p)["used"] for p in members)
         return {"total": self.device_map().gpus[index].vram_bytes, "used": used}
+
+    def power_clock(self, index: int) -> Dict[str, float]:
+        """Socket power / limit (W) and GFX clock / max (MHz) of physical GPU ``index``."""
+        return self._power_clock(self._primary(index))
 
     def close(self) -> None:
         return
@@ -308,6 +315,11 @@ class FakeAmdSmi(AmdSmi):
     def _vram_usage(self, proc: ProcInfo) -> Dict[str, int]:
         return {"total": proc.vram_bytes, "used": 0}
 
+    def _power_clock(self, proc: ProcInfo) -> Dict[str, float]:
+        busy = self._process_count(proc) > 0
+        return {"power_w": 1000.0 if busy else 150.0, "power_limit_w": 1400.0, "gfx_mhz": 2000.0 if busy else 100.0,
+                "gfx_max_mhz": 2400.0}
+
     # -- test helpers -----------------------------------------------------------------------------
     def set_processes(self, index: int, n: int, partition: int = 0) -> None:
         """Pretend ``n`` processes hold partition ``partition`` of GPU ``index``."""
@@ -369,6 +381,7 @@ class NativeAmdSmi(AmdSmi):
         L.nos_smi_process_count.argtypes = [ctypes.c_uint32]
         L.nos_smi_activity.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.nos_smi_vram.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.nos_smi_power_clock.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 4
         self._lock = threading.Lock()
         rc = L.nos_smi_init()
         if rc != 0:
@@ -437,6 +450,13 @@ class NativeAmdSmi(AmdSmi):
         with self._lock:
             self._check(self._lib.nos_smi_vram(proc.ordinal, ctypes.byref(t), ctypes.byref(u)), "vram")
         return {"total": t.value, "used": u.value}
+
+    def _power_clock(self, proc: ProcInfo) -> Dict[str, float]:
+        v = [ctypes.c_uint32() for _ in range(4)]
+        with self._lock:
+            self._check(self._lib.nos_smi_power_clock(proc.ordinal, *[ctypes.byref(x) for x in v]), "power/clock")
+        return {"power_w": float(v[0].value), "power_limit_w": float(v[1].value), "gfx_mhz": float(v[2].value),
+                "gfx_max_mhz": float(v[3].value)}
 
     def close(self) -> None:
         self._lib.nos_smi_shutdown()
