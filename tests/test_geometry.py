@@ -14,7 +14,13 @@ from walkai_nos_amd.models.xcp.profile import XcpProfile, extract_profile_name, 
 
 from walkai_nos_amd.models import mig  # noqa: E402
 
-A100_80 = mig.KNOWN_GEOMETRIES[mig.A100_PCIE_80GB]
+A100_80_BUILTIN = mig.KNOWN_GEOMETRIES[mig.A100_PCIE_80GB]
+# the table TestGPU__UpdateGeometryFor installs with SetKnownGeometries before its cases
+# (ref pkg/gpu/mig/gpu_test.go:297-317)
+A100_80 = [{"1g.10gb": 7}, {"1g.10gb": 5, "2g.20gb": 1}, {"1g.10gb": 3, "2g.20gb": 2}, {"1g.10gb": 1, "2g.20gb": 3},
+           {"1g.10gb": 2, "2g.20gb": 1, "3g.40gb": 1}, {"2g.20gb": 2, "3g.40gb": 1}, {"1g.10gb": 3, "3g.40gb": 1},
+           {"1g.10gb": 1, "2g.20gb": 1, "3g.40gb": 1}, {"3g.40gb": 2}, {"1g.10gb": 3, "4g.40gb": 1},
+           {"1g.10gb": 1, "2g.20gb": 1, "4g.40gb": 1}, {"7g.79gb": 1}]
 A100_40 = mig.KNOWN_GEOMETRIES[mig.A100_SXM4_40GB]
 A30 = mig.KNOWN_GEOMETRIES[mig.A30]
 
@@ -45,6 +51,14 @@ def g(table, used=None, free=None, model="m"):
 def test_update_geometry_for_reference_vectors(gpu, required, expected, updated):
     assert gpu.update_geometry_for(required) is updated
     assert gpu.geometry() == expected
+
+
+def test_builtin_mig_tables_match_the_reference():
+    # pkg/gpu/mig/known_configs.go:26-140: 4 A30 and 12 geometries per A100 model
+    assert len(A30) == 4 and len(A100_40) == 12 and len(A100_80_BUILTIN) == 12
+    assert {"1g.5gb": 7} in A100_40 and {"2g.10gb": 1, "1g.5gb": 5} in A100_40
+    assert {"7g.79gb": 1} in A100_80_BUILTIN and {"4g.40gb": 1, "1g.10gb": 3} in A100_80_BUILTIN
+    assert max(sum(geo.values()) for geo in A100_40) == 7  # the 7-pods-per-GPU density anchor
 
 
 def test_apply_geometry_sets_free_and_drops_missing():

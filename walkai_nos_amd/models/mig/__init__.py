@@ -21,15 +21,22 @@ A30 = "A30"
 A100_SXM4_40GB = "NVIDIA-A100-40GB-SXM4"
 A100_PCIE_80GB = "NVIDIA-A100-80GB-PCIe"
 
+# the reference's tables entry for entry (``pkg/gpu/mig/known_configs.go:26-140``), including its
+# A100-80GB rows that mix 20 GB and 40 GB profiles: they are parity data, not a statement about
+# what an A100 accepts
 KNOWN_GEOMETRIES: Dict[str, List[Dict[str, int]]] = {
     A30: [{"4g.24gb": 1}, {"2g.12gb": 2}, {"2g.12gb": 1, "1g.6gb": 2}, {"1g.6gb": 4}],
-    A100_SXM4_40GB: [{"7g.40gb": 1}, {"4g.20gb": 1, "2g.10gb": 1, "1g.5gb": 1}, {"3g.20gb": 2},
-                     {"1g.5gb": 7}],
+    A100_SXM4_40GB: [
+        {"7g.40gb": 1}, {"4g.20gb": 1, "2g.10gb": 1, "1g.5gb": 1}, {"4g.20gb": 1, "1g.5gb": 3},
+        {"3g.20gb": 2}, {"3g.20gb": 1, "2g.10gb": 1, "1g.5gb": 1}, {"3g.20gb": 1, "1g.5gb": 3},
+        {"2g.10gb": 2, "3g.20gb": 1}, {"2g.10gb": 1, "1g.5gb": 2, "3g.20gb": 1}, {"2g.10gb": 3, "1g.5gb": 1},
+        {"2g.10gb": 2, "1g.5gb": 3}, {"2g.10gb": 1, "1g.5gb": 5}, {"1g.5gb": 7},
+    ],
     A100_PCIE_80GB: [
-        {"1g.10gb": 7}, {"1g.10gb": 5, "2g.20gb": 1}, {"1g.10gb": 3, "2g.20gb": 2}, {"1g.10gb": 1, "2g.20gb": 3},
-        {"1g.10gb": 2, "2g.20gb": 1, "3g.40gb": 1}, {"2g.20gb": 2, "3g.40gb": 1}, {"1g.10gb": 3, "3g.40gb": 1},
-        {"1g.10gb": 1, "2g.20gb": 1, "3g.40gb": 1}, {"3g.40gb": 2}, {"1g.10gb": 3, "4g.40gb": 1},
-        {"1g.10gb": 1, "2g.20gb": 1, "4g.40gb": 1}, {"7g.79gb": 1},
+        {"7g.79gb": 1}, {"4g.40gb": 1, "2g.20gb": 1, "1g.10gb": 1}, {"4g.40gb": 1, "1g.10gb": 3},
+        {"3g.40gb": 2}, {"3g.40gb": 1, "2g.20gb": 1, "1g.10gb": 1}, {"3g.40gb": 1, "1g.10gb": 3},
+        {"2g.20gb": 2, "3g.20gb": 1}, {"2g.10gb": 1, "1g.10gb": 2, "3g.40gb": 1}, {"2g.20gb": 3, "1g.10gb": 1},
+        {"2g.20gb": 2, "1g.10gb": 3}, {"2g.20gb": 1, "1g.10gb": 5}, {"1g.10gb": 7},
     ],
 }
 
