@@ -1,5 +1,6 @@
 """Packaging: kustomize manifests, Helm chart, CRDs, ComponentConfigs, console scripts, demo."""
 import glob
+import json
 import importlib
 import os
 import re
@@ -199,3 +200,83 @@ def test_native_libraries_are_stamped_with_their_source_hash():
             assert b.verify(t.name) == t.source_hash()
     t = b.target("libnos_probe.so")
     assert t.source_hash() != b.Target("x", ["probe.hip"], "hipcc", flags=["-DX"]).source_hash()
+
+
+# -- the chart rendered (hack/helmlite.py: a Go-template subset interpreter; no helm binary here) --
+def _chart(values=None, namespace="nos-system", lookup=None):
+    import sys
+    sys.path.insert(0, _p("hack"))
+    import helmlite
+    return helmlite, helmlite.Chart(_p("helm-charts/nos"), values or {}, namespace=namespace, lookup=lookup)
+
+
+def test_helm_chart_renders_to_valid_objects():
+    from walkai_nos_amd.api.config import load_config
+    _, chart = _chart()
+    objs = chart.objects()
+    kinds = {o["kind"] for o in objs}
+    assert {"Deployment", "DaemonSet", "ConfigMap", "ClusterRole", "ClusterRoleBinding", "ServiceAccount",
+            "Service", "Job"} <= kinds
+    for o in objs:
+        assert o.get("apiVersion") and o["metadata"].get("name"), o
+        if o["kind"] not in ("ClusterRole", "ClusterRoleBinding"):
+            assert o["metadata"]["namespace"] == "nos-system", o["metadata"]
+    deps = {o["metadata"]["name"]: o for o in objs if o["kind"] in ("Deployment", "DaemonSet")}
+    gp = deps["nos-gpu-partitioner"]["spec"]["template"]["spec"]
+    assert [c["name"] for c in gp["containers"]] == ["gpu-partitioner", "kube-rbac-proxy"]
+    for d in deps.values():
+        for c in d["spec"]["template"]["spec"]["containers"]:
+            assert c["image"] and "<no value>" not in json.dumps(c)
+    cms = {o["metadata"]["name"]: o for o in objs if o["kind"] == "ConfigMap"}
+    cfg = load_config(cms["nos-gpu-partitioner-config"]["data"]["gpu_partitioner_config.yaml"])
+    assert cfg.planningPolicy == "pack" and cfg.metricsBindAddress == "127.0.0.1:8080"
+    assert "known_geometries.yaml" in cms["nos-gpu-partitioner-config"]["data"]
+
+
+def test_helm_chart_refuses_the_default_namespace():
+    helmlite, chart = _chart(namespace="default")
+    with pytest.raises(helmlite.Fail):
+        chart.render()
+
+
+def test_helm_telemetry_reuses_the_installation_uuid_and_reports_nodes():
+    from walkai_nos_amd.exporters.telemetry import Metrics
+    node = {"metadata": {"name": "gpu-1", "labels": {"amd.com/gpu.product-name": "MI355X", "kubernetes.io/os": "linux",
+                                                     "node.kubernetes.io/instance-type": "mi355x-8"}},
+            "status": {"capacity": {"amd.com/gpu": "8"}, "nodeInfo": {"kubeletVersion": "v1.30.0"}}}
+
+    def lookup(api, kind, ns, name):
+        if kind == "ConfigMap" and name == "nos-installation-info":
+            return {"data": {"installationUUID": "11111111-2222-3333-4444-555555555555"}}
+        if kind == "Node":
+            return {"items": [node]}
+        return {}
+    _, chart = _chart(lookup=lookup)
+    cms = {o["metadata"]["name"]: o for o in chart.objects() if o["kind"] == "ConfigMap"}
+    assert cms["nos-installation-info"]["data"]["installationUUID"] == "11111111-2222-3333-4444-555555555555"
+    assert cms["nos-installation-info"]["metadata"]["annotations"]["helm.sh/resource-policy"] == "keep"
+    m = Metrics.from_yaml(cms["nos-telemetry-metrics"]["data"]["metrics.yaml"])
+    assert m.installationUUID == "11111111-2222-3333-4444-555555555555"
+    assert m.nodes[0].name == "gpu-1" and "kubernetes.io/os" not in m.nodes[0].labels
+    assert m.nodes[0].labels["node.kubernetes.io/instance-type"] == "mi355x-8"
+    assert m.components.nosGpuPartitioner is True
+    # a first install generates a fresh UUID
+    _, fresh = _chart()
+    u = {o["metadata"]["name"]: o for o in fresh.objects()}["nos-installation-info"]["data"]["installationUUID"]
+    assert len(u) == 36 and u != "11111111-2222-3333-4444-555555555555"
+
+
+def test_helm_metrics_exposure_toggles():
+    _, plain = _chart({"gpuPartitioner": {"metrics": {"authProxy": {"enabled": False},
+                                                      "serviceMonitor": {"enabled": True}}}})
+    objs = plain.objects()
+    dep = next(o for o in objs if o["kind"] == "Deployment" and o["metadata"]["name"] == "nos-gpu-partitioner")
+    assert [c["name"] for c in dep["spec"]["template"]["spec"]["containers"]] == ["gpu-partitioner"]
+    svc = next(o for o in objs if o["kind"] == "Service" and o["metadata"]["name"] == "nos-gpu-partitioner-metrics")
+    assert svc["spec"]["ports"][0]["port"] == 8080
+    sm = next(o for o in objs if o["kind"] == "ServiceMonitor")
+    assert sm["spec"]["endpoints"][0]["port"] == "metrics"
+    assert not any(o["kind"] == "ClusterRole" and o["metadata"]["name"] == "nos-metrics-reader" for o in objs)
+    _, off = _chart({"shareTelemetry": False, "operator": {"enabled": False}})
+    names = {o["metadata"]["name"] for o in off.objects()}
+    assert "nos-telemetry" not in names and "nos-installation-info" not in names
