@@ -455,7 +455,10 @@ class NativeAmdSmi(AmdSmi):
         v = [ctypes.c_uint32() for _ in range(4)]
         with self._lock:
             self._check(self._lib.nos_smi_power_clock(proc.ordinal, *[ctypes.byref(x) for x in v]), "power/clock")
-        return {"power_w": float(v[0].value), "power_limit_w": float(v[1].value), "gfx_mhz": float(v[2].value),
+        limit = float(v[1].value)
+        if limit > 1e5:  # some drivers report the limit in microwatts
+            limit /= 1e6
+        return {"power_w": float(v[0].value), "power_limit_w": limit, "gfx_mhz": float(v[2].value),
                 "gfx_max_mhz": float(v[3].value)}
 
     def close(self) -> None:
