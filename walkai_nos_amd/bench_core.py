@@ -51,8 +51,9 @@ BASELINE_LABEL = "MPS 7-pod aggregate throughput on 1x A100-80GB (BASELINE.md), 
 
 MIX = (("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2))
 
-#: CU-mask density phase: dedicated-CU slices plus memory-only slices on the shared rows
-CUMASK_DENSITY = (("32cu.24gb", 6), ("8gb", 10))
+#: CU-mask density phases: dedicated-CU slices plus memory-only slices on the shared rows, and
+#: memory-only slices alone (the reference's MPS semantics: HBM budgets, compute shared by all)
+CUMASK_DENSITY = {"cumask": (("32cu.24gb", 6), ("8gb", 10)), "cumask_shared": (("16gb", 16),)}
 
 
 @dataclass
@@ -491,33 +492,34 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
         torch.cuda.synchronize()
         out["xcp"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
     # CU-mask slices beyond 8 per GPU
-    c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
-                    policy="fifo")
-    c2.run(30)
-    k = 0
-    for _ in range(cfg.gpus):
-        for prof, n_pods in CUMASK_DENSITY:
-            for _ in range(n_pods):
-                c2.submit({f"amd.com/gpu-{prof}": 1}, name=f"s{k}")
-                k += 1
-    c2.run(240)
-    sn2 = next(iter(c2.nodes.values()))
-    per_gpu2 = collections.Counter(sn2.smi.gpu_index_of(d) for devs in sn2.kubelet.allocations.values()
-                                   for _, d in devs)
-    out["cumask"] = {"pods_per_gpu": min(per_gpu2.get(g, 0) for g in range(cfg.gpus)),
-                     "pods_per_node": sum(per_gpu2.values()), "pending": len(c2.pending_pods()),
-                     "profiles": {p: n for p, n in CUMASK_DENSITY}}
-    if data is not None:
-        slices = sn2.plugin.store.load().get(cfg.rank, [])
-        mine = {d for devs in sn2.kubelet.allocations.values() for _, d in devs
-                if sn2.smi.gpu_index_of(d) == cfg.rank}
-        wanted = {("cumask", s.id): cus_of(s, slices, 256) for s in slices if s.id in mine}
-        data.add_slots(wanted)
-        t0 = time.perf_counter()
-        n = data.serve(list(wanted), t0 + serve_s)
-        data.drain_all()
-        torch.cuda.synchronize()
-        out["cumask"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
+    for variant, mix in CUMASK_DENSITY.items():
+        c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
+                        policy="fifo")
+        c2.run(30)
+        k = 0
+        for _ in range(cfg.gpus):
+            for prof, n_pods in mix:
+                for _ in range(n_pods):
+                    c2.submit({f"amd.com/gpu-{prof}": 1}, name=f"s{k}")
+                    k += 1
+        c2.run(240)
+        sn2 = next(iter(c2.nodes.values()))
+        per_gpu2 = collections.Counter(sn2.smi.gpu_index_of(d) for devs in sn2.kubelet.allocations.values()
+                                       for _, d in devs)
+        out[variant] = {"pods_per_gpu": min(per_gpu2.get(g, 0) for g in range(cfg.gpus)),
+                        "pods_per_node": sum(per_gpu2.values()), "pending": len(c2.pending_pods()),
+                        "profiles": {p: n for p, n in mix}}
+        if data is not None:
+            slices = sn2.plugin.store.load().get(cfg.rank, [])
+            mine = {d for devs in sn2.kubelet.allocations.values() for _, d in devs
+                    if sn2.smi.gpu_index_of(d) == cfg.rank}
+            wanted = {(variant, s.id): cus_of(s, slices, 256) for s in slices if s.id in mine}
+            data.add_slots(wanted)
+            t0 = time.perf_counter()
+            n = data.serve(list(wanted), t0 + serve_s)
+            data.drain_all()
+            torch.cuda.synchronize()
+            out[variant]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
     return out
 
 
