@@ -81,8 +81,11 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
   static_assert(NPL % 2 == 0, "hidden size must be a multiple of 128");
   constexpr int D = NPL * 64, NP = NPL / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + wave;
-  if (row >= rows) return;
+  const float2* w2 = reinterpret_cast<const float2*>(w);
+  const float2* b2 = reinterpret_cast<const float2*>(b);
+  // grid-stride over rows: a slice sharing the GPU launches a few workgroups per CU instead of one
+  // per 4 rows (workgroup dispatch is what concurrent partitions contend for)
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
   const float2* xr = reinterpret_cast<const float2*>(x + size_t(row) * D);
   float2 v[NP];
   float s = 0.f;
@@ -100,8 +103,6 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
     q += v[i].x * v[i].x + v[i].y * v[i].y;
   }
   const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
-  const float2* w2 = reinterpret_cast<const float2*>(w);
-  const float2* b2 = reinterpret_cast<const float2*>(b);
   if (yp) {
     const size_t plane2 = size_t(rows) * D / 2;  // plane stride in bf16 pairs
     uint32_t* dst = reinterpret_cast<uint32_t*>(yp) + size_t(row) * (D / 2);
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
       dst[plane2 + c2] = __builtin_bit_cast(uint32_t, h1);
       dst[2 * plane2 + c2] = __builtin_bit_cast(uint32_t, h2);
     }
-    return;
+    continue;
   }
   float2* yr = reinterpret_cast<float2*>(y + size_t(row) * D);
 #pragma unroll
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
     const int c2 = i * 64 + lane;
     const float2 ww = w2[c2], bb = b2[c2];
     yr[c2] = make_float2(v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y);
+  }
   }
 }
 
@@ -572,7 +574,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_sk_lds(const float* __restric
 template <int G>
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
-                                                         int B, int T, int H, int P, __bf16* __restrict__ outp) {
+                                                         int B, int T, int H, int P, __bf16* __restrict__ outp,
+                                                         int h0, int Ht) {
   __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
@@ -585,9 +588,9 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   const long long w_lo = ((t0 + 1) * P + U - 1) / U - 1;
   const long long w_hi = (t1 * P + U - 1) / U - 1;
   if (w_lo == w_hi) return;
-  const int head = int((grp / QG) % H);
+  const int head = h0 + int((grp / QG) % H);
   const int b = int(grp / ((long long)QG * H));
-  const int D = H * HD;
+  const int D = Ht * HD;
   const int tid = threadIdx.x;
   auto slot_of = [&](long long w) -> long long {
     const long long s = w * U / P;
@@ -915,7 +918,8 @@ template <int G>
 __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
-                                                             int B, int T, int H, float scale_log2e, int P) {
+                                                             int B, int T, int H, int h0, int Ht, float scale_log2e,
+                                                             int P) {
   static_assert(G == 4 || G == 8, "4 or 8 query tiles per workgroup");
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
@@ -924,7 +928,7 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
   const long long U = (long long)B * H * QG * NK;
   long long u = sk_begin(w, U, P);
   const long long u1 = sk_begin(w + 1, U, P);
-  const int D = H * HD, ld = 3 * D;
+  const int D = Ht * HD, ld = 3 * D;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int j = lane & 31, hf = lane >> 5;
   const int lrow = (tid & 255) >> 3, lch = tid & 7;
@@ -939,7 +943,7 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
     const int nb = kb1 - kb0;
     const int qg = int(grp % QG);
-    const int head = int((grp / QG) % H);
+    const int head = h0 + int((grp / QG) % H);
     const int b = int(grp / ((long long)QG * H));
     const __bf16* base = qkv3 + size_t(b) * T * ld;
     const int qt = qg * G + wv;
@@ -1255,10 +1259,12 @@ int nos_attention_x3_wg_per_cu() {
 
 // Stream-K attention over x3 planes of a packed [B, T, 3*H*64] QKV tensor (plane stride
 // `plane_stride` elements); output fp32 [B, T, H*64] (out) or its x3 planes [3][B*T*H*64] (outp),
-// exactly one non-null. Workspace: nos_attention_ws_bytes of the LDS variant (variant 0 layout),
-// merged by the same fixup kernel.
-int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B, int T,
-                        int H, int head_dim, float scale, int waves, void* stream) {
+// exactly one non-null. Heads h0 .. h0+hn-1 only: a slice of few CUs runs the heads in blocks so its
+// workgroups share one block's K/V in L2 (with every head in flight at once, the K/V planes of all
+// heads are the L2 working set — the traffic concurrent partitions contend for). Workspace:
+// nos_attention_ws_bytes of the LDS variant (variant 0 layout), merged by the same fixup kernel.
+int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
+                              int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream) {
   if ((out == nullptr) == (outp == nullptr)) {
     g_err = "attention x3: exactly one of out / outp";
     return -1;
@@ -1275,6 +1281,14 @@ int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void*
     g_err = "attention x3: plane stride must be a multiple of 8 elements (16-B aligned planes)";
     return -1;
   }
+  if (h0 < 0 || hn <= 0 || h0 + hn > H) {
+    g_err = "attention x3: head block out of range";
+    return -1;
+  }
+  if (!g_x3_pipelined && (h0 != 0 || hn != H)) {
+    g_err = "attention x3: head blocks need the pipelined kernel";
+    return -1;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int G = nos_attention_x3_group();
   const int NK = (T + 31) / 32, QG = (NK + G - 1) / G;
@@ -1288,29 +1302,37 @@ int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void*
                        sl2, waves);
   else if (G == 8)
     hipLaunchKernelGGL(attn_fwd_x3p<8>, dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
-                       T, H, sl2, waves);
+                       T, hn, h0, H, sl2, waves);
   else
     hipLaunchKernelGGL(attn_fwd_x3p<4>, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
-                       T, H, sl2, waves);
+                       T, hn, h0, H, sl2, waves);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (G == 8)
-    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(B * H * QG * 8), dim3(256), 0, s, part_o, part_ml, out, B, T, H,
-                       waves, op);
+    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(B * hn * QG * 8), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
+                       waves, op, h0, H);
   else
-    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H,
-                       waves, op);
+    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * hn * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
+                       waves, op, h0, H);
   return check_launch("attn_sk_lds_fixup");
 }
 
-// y (fp32) or yp (x3 planes [3][rows][D]) — exactly one of them non-null
-int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,
-                      float eps, void* stream) {
+int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B, int T,
+                        int H, int head_dim, float scale, int waves, void* stream) {
+  return nos_attention_x3_sk_heads(qkv3, plane_stride, out, outp, ws, B, T, H, 0, H, head_dim, scale, waves, stream);
+}
+
+// y (fp32) or yp (x3 planes [3][rows][D]) — exactly one of them non-null; `wgs` workgroups of 4
+// rows each (grid-stride), 0 = one per 4 rows
+int nos_layernorm_f32_grid(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,
+                           float eps, int wgs, void* stream) {
   if ((y == nullptr) == (yp == nullptr)) {
     g_err = "layernorm: exactly one of y / yp";
     return -1;
   }
+  if (rows <= 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((rows + 3) / 4), block(256);
+  const int full = (rows + 3) / 4;
+  const dim3 grid(wgs > 0 ? std::min(wgs, full) : full), block(256);
   __bf16* p = reinterpret_cast<__bf16*>(yp);
   switch (D) {
     case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
@@ -1323,6 +1345,11 @@ int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, 
       return -1;
   }
   return check_launch("layernorm_f32");
+}
+
+int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,
+                      float eps, void* stream) {
+  return nos_layernorm_f32_grid(x, w, b, y, yp, rows, D, eps, 0, stream);
 }
 
 int nos_bias_gelu_f32(float* y, const float* b, int rows, int N, void* stream) {
@@ -1390,7 +1417,7 @@ int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, 
                        scale_log2e, waves);
     if (int rc = check_launch("attn_fwd_sk_lds")) return rc;
     hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
-                       static_cast<__bf16*>(nullptr));
+                       static_cast<__bf16*>(nullptr), 0, H);
     return check_launch("attn_sk_lds_fixup");
   }
   float* part_o = ws;

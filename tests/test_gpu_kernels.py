@@ -245,6 +245,26 @@ def test_attention_x3_fp32_accurate_any_grid(K, T, H, B):
         K.set_attention_x3_group(8)
 
 
+@pytest.mark.parametrize("group", [4, 8])
+def test_attention_x3_head_blocks_match_one_launch(K, group):
+    # heads in blocks (one launch per block, x3 planes out) must equal the all-heads launch and fp64
+    T, H, B = 1000, 6, 2
+    torch.manual_seed(3)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    planes = K.split3(qkv)
+    K.set_attention_x3_group(group)
+    try:
+        for hb, waves in ((1, 32), (2, 7), (4, 64), (6, 256)):
+            o3 = torch.full((3, B, T, H * 64), float("nan"), dtype=torch.bfloat16, device="cuda")
+            K.attention_x3(planes, o3, H, 64, 0.125, waves, head_block=hb)
+            torch.cuda.synchronize()
+            out = o3[0].float() + o3[1].float() + o3[2].float()
+            assert (out - ref).abs().max().item() < 2e-6, (hb, waves)
+    finally:
+        K.set_attention_x3_group(8)
+
+
 def test_attention_x3_asymmetric_values(K):
     T, H = 96, 1
     qkv = torch.zeros(1, T, 3 * 64, device="cuda")

@@ -233,6 +233,15 @@ def test_helm_chart_renders_to_valid_objects():
     assert "known_geometries.yaml" in cms["nos-gpu-partitioner-config"]["data"]
 
 
+def test_helm_chart_passes_pack_knobs_to_the_partitioner_config():
+    from walkai_nos_amd.api.config import load_config
+    _, chart = _chart({"gpuPartitioner": {"packing": {"minFill": 0.25, "drainGainAfterSeconds": 120}}})
+    cms = {o["metadata"]["name"]: o for o in chart.objects() if o["kind"] == "ConfigMap"}
+    cfg = load_config(cms["nos-gpu-partitioner-config"]["data"]["gpu_partitioner_config.yaml"])
+    p = cfg.pack_params()
+    assert (p.min_fill, p.drain_gain_after) == (0.25, 120.0)
+
+
 def test_helm_chart_refuses_the_default_namespace():
     helmlite, chart = _chart(namespace="default")
     with pytest.raises(helmlite.Fail):

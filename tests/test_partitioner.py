@@ -1,4 +1,6 @@
 """Cluster-side partitioner: pod controller (B1), node initialiser (B2), spec writer (C4)."""
+import pytest
+
 from walkai_nos_amd import constant
 from walkai_nos_amd.api import v1alpha1 as api
 from walkai_nos_amd.controllers.partitioner.node_controller import NodeController
@@ -233,3 +235,30 @@ def test_pod_controller_plan_memo_skips_replanning_until_the_api_changes():
         assert len(calls) == n + 1                   # a node write forces a re-plan
     finally:
         pcm.plan_cluster_fifo = orig
+
+
+def test_packing_config_maps_to_pack_params():
+    from walkai_nos_amd.api.config import GpuPartitionerConfig
+    cfg = GpuPartitionerConfig(packing={"minFill": 0.25, "drainGainAfterSeconds": 120, "spxReserve": False})
+    cfg.validate()
+    p = cfg.pack_params()
+    assert (p.min_fill, p.drain_gain_after, p.spx_reserve) == (0.25, 120.0, False)
+    assert p.drain_gain == 0.625  # untouched knobs keep their defaults
+    with pytest.raises(ValueError):
+        GpuPartitionerConfig(packing={"minFil": 0.2}).validate()
+    with pytest.raises(ValueError):
+        GpuPartitionerConfig(packing={"drainGain": -1}).validate()
+
+
+def test_pack_gain_drain_rotates_an_underused_gpu():
+    # one GPU in CPX mode holding a single 1/8 pod, SPX pods waiting past drain_gain_after: the GPU
+    # is drained for SPX (target set, no new CPX pods), which it would never be by the backlog rule
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, new_node_model, plan_cluster_pack
+    node = xnode("n0", gpus=1, anns={"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "1",
+                                     "nos.nebuly.com/status-gpu-0-cpx_nps1-free": "7"})
+    models = {"n0": new_node_model("xcp", node)}
+    pending = [({"spx_nps1": 1}, 700.0)]
+    changed = plan_cluster_pack(models, pending, params=PackParams())
+    assert changed["n0"].gpus[0].target == {"spx_nps1": 1}
+    assert plan_cluster_pack(models, pending, params=PackParams(drain_gain_after=0)) == {}
+    assert plan_cluster_pack(models, [({"spx_nps1": 1}, 100.0)], params=PackParams()) == {}

@@ -71,9 +71,27 @@ class GpuPartitionerConfig(ManagerConfig):
     devicePluginDelaySeconds: float = 5.0
     planningPolicy: str = "pack"
     scoring: str = "fraction"
+    #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
+    #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds
+    packing: Dict[str, Any] = field(default_factory=dict)
+
+    PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
+                    "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
+                    "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after"}
+
+    def pack_params(self) -> Any:
+        from ..controllers.partitioner.pod_controller import PackParams
+        return PackParams(**{self.PACKING_KEYS[k]: (bool(v) if k == "spxReserve" else float(v))
+                             for k, v in self.packing.items()})
 
     def validate(self) -> None:
         super().validate()
+        unknown = set(self.packing) - set(self.PACKING_KEYS)
+        if unknown:
+            raise ValueError(f"packing: unknown keys {sorted(unknown)}")
+        for k, v in self.packing.items():
+            if k != "spxReserve" and (not isinstance(v, (int, float)) or v < 0):
+                raise ValueError(f"packing.{k} must be a non-negative number")
         if self.batchWindowTimeoutSeconds <= 0:
             raise ValueError("batchWindowTimeoutSeconds must be greater than 0")
         if self.batchWindowIdleSeconds <= 0:

@@ -27,7 +27,7 @@ def main(argv=None) -> int:
     client = make_client(args.kubeconfig)
     mgr = make_manager(client, cfg, "gpupartitioner")
     setup_partitioner(mgr, batch_timeout=cfg.batchWindowTimeoutSeconds, batch_idle=cfg.batchWindowIdleSeconds,
-                      scoring=cfg.scoring, policy=cfg.planningPolicy)
+                      scoring=cfg.scoring, policy=cfg.planningPolicy, pack=cfg.pack_params())
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr)
 

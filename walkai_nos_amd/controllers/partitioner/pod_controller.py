@@ -169,6 +169,8 @@ class PackParams:
     drain_backlog: float = 2.0      # ... if its profile's queue would fill at least this many GPUs
     spx_reserve: bool = True        # keep idle SPX GPUs for recent whole-GPU demand (multi-GPU)
     reserve_decay: float = 0.9      # EMA decay of the whole-GPU demand estimate per planning pass
+    drain_gain: float = 0.625       # drain a busy GPU whose used fraction is this much below the
+    drain_gain_after: float = 600.0  # ... fill a profile waiting this long would give it (0 = off)
 
 
 def _mode_of(gpu: Any) -> Optional[str]:
@@ -197,8 +199,10 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
     4. on multi-GPU nodes idle SPX GPUs are kept as a reserve sized from the recent whole-GPU demand
        (``spx_demand``, an EMA in GPUs), unless a starving pod needs them;
     5. a profile whose oldest pod has waited ``drain_after``, and whose queue would fill
-       ``drain_backlog`` GPUs (a drain idles partitions, so it must buy a full GPU of work), with no
-       idle GPU to take gets one busy
+       ``drain_backlog`` GPUs (a drain idles partitions, so it must buy a full GPU of work), or whose
+       oldest pod has waited ``drain_gain_after`` and whose queue would fill a GPU at least
+       ``drain_gain`` more than the pods now holding one (a single-GPU node otherwise serves one
+       profile for as long as its pods keep arriving), with no idle GPU to take gets one busy
        GPU **drained** for it: the least-used GPU in another mode gets the new spec now, is no
        longer offered to new pods (``PartitionedGPU.target``; the scheduler skips GPUs whose spec
        mode differs from their current mode), and the agent flips it when its last pod leaves.
@@ -288,14 +292,23 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
                     break
         if demand.get(p, 0) <= 1e-9:
             demand.pop(p, None)
-    # 5. drain a busy GPU for a profile that has waited too long
+    # 5. drain a busy GPU for a profile that has waited too long (backlog rule), or whose waiting
+    #    demand would use the GPU much better than the few pods holding it now (gain rule)
     draining_to = {next(iter(g.target)) for m in current.values() for g in m.gpus if g.target}
+    used_of = (lambda g: g.used_fraction(lambda q: round(1.0 / frac(q)))) if w is not None else \
+        (lambda g: float(sum(g.used.values())))
     for p in sorted(demand, key=lambda q: -oldest.get(q, 0.0)):
-        if demand[p] < params.drain_backlog - 1e-9 or oldest.get(p, 0.0) < params.drain_after or p in draining_to:
+        if p in draining_to:
             continue
-        cands = [(g.used_fraction(lambda q: round(1.0 / frac(q))) if w is not None else sum(g.used.values()),
-                  name, g) for name in sorted(current) for g in current[name].gpus
+        backlog = demand[p] >= params.drain_backlog - 1e-9 and oldest.get(p, 0.0) >= params.drain_after
+        gain_ok = params.drain_gain_after > 0 and oldest.get(p, 0.0) >= params.drain_gain_after
+        if not backlog and not gain_ok:
+            continue
+        fill = min(demand[p], 1.0)
+        cands = [(used_of(g), name, g) for name in sorted(current) for g in current[name].gpus
                  if g.target is None and not g.is_idle() and _mode_of(g) != p]
+        if not backlog:
+            cands = [c for c in cands if w is not None and fill - c[0] >= params.drain_gain - 1e-9]
         if not cands:
             continue
         _, name, g = min(cands, key=lambda c: (c[0], c[1], c[2].index))

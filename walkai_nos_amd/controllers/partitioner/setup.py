@@ -15,13 +15,13 @@ from .pod_controller import PodController
 def setup_partitioner(mgr: Manager, kinds=(api.PARTITIONING_KIND_XCP, api.PARTITIONING_KIND_CUMASK),
                       batch_timeout: float = 0.0, batch_idle: float = 0.0, retry_after: float = 5.0,
                       partitioner: Optional[Partitioner] = None, scoring: str = "fraction",
-                      policy: str = "fifo"):
+                      policy: str = "fifo", pack=None):
     partitioner = partitioner or Partitioner(mgr.client)
     pod_ctrls = []
     for kind in kinds:
         pc = PodController(mgr.client, kind, partitioner, clock=mgr.clock, batch_timeout=batch_timeout,
                            batch_idle=batch_idle, retry_after=retry_after, scoring=scoring,
-                           policy=policy)
+                           policy=policy, pack=pack)
         # MaxConcurrentReconciles = 1: one writer per kind (mig_controller.go:204)
         mgr.new_controller(f"{constant.CLUSTER_PARTITIONER_CONTROLLER}-{kind}", pc.reconcile,
                            [Watch("Pod", mapper=pc.map_pod)], 1)

@@ -288,6 +288,25 @@ def shared_slice_tiles(cands: list, cus: int) -> list:
     return big or cands
 
 
+_TUNED_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "x3_tuned.json")
+_tuned: Optional[Dict[str, int]] = None
+
+
+def tuned_table() -> Dict[str, int]:
+    """Tiles measured on CONCURRENT sibling partitions (``tools/contention.py --emit-table``): the
+    isolated autotuner cannot see what a slice's neighbours cost it, so where the table has the
+    exact (shape, epilogue, outputs, slice size) key its tile wins. ``NOS_X3_TUNED=0`` ignores it."""
+    global _tuned
+    if _tuned is None:
+        table: Dict[str, int] = {}
+        if os.environ.get("NOS_X3_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+            import json
+            with open(_TUNED_PATH) as f:
+                table = {k: int(v["tile"]) for k, v in json.load(f).items() if int(v["tile"]) in X3_TILES}
+        _tuned = table
+    return _tuned
+
+
 def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
     best, best_key = cands[0], None
     for c in cands:
@@ -356,6 +375,13 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
         key = (M, N, Kd, epi, int(out_f32) | 2 * int(out_x3), cus)
         with _lock:
             tile = _x3_cache.get(key)
+        if tile is None:
+            tile = tuned_table().get(f"M{M}_N{N}_K{Kd}_epi{epi}_out{key[4]}_cus{cus}")
+            if tile is not None and N % X3_TILES[tile][1] == 0:
+                with _lock:
+                    _x3_cache[key] = tile
+            else:
+                tile = None
         if tile is None:
             cands = x3_eligible(N, Kd)
             if not cands:

@@ -165,16 +165,39 @@ def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
     return per_cu * cus
 
 
+_head_block: Optional[int] = None
+
+
+def set_attention_head_block(n: Optional[int]) -> None:
+    """Heads per x3 attention launch (None = the slice-size rule of :func:`attention_head_block`)."""
+    global _head_block
+    _head_block = n
+
+
+def attention_head_block(cus: int, heads: int) -> int:
+    """Heads per x3 attention launch on a slice of ``cus`` CUs. All heads in one launch puts every
+    head's K/V planes in the L2 working set at once; on a small slice the heads run in blocks so
+    its workgroups share one block's K/V (``NOS_ATTN_HEAD_BLOCK`` / :func:`set_attention_head_block`
+    override the rule for A/B runs)."""
+    env = os.environ.get("NOS_ATTN_HEAD_BLOCK")
+    n = _head_block if _head_block is not None else (int(env) if env else heads)
+    return max(1, min(heads, n))
+
+
 def attention_x3(planes: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float,
-                 waves: int) -> torch.Tensor:
+                 waves: int, head_block: Optional[int] = None) -> torch.Tensor:
     """Stream-K attention over the x3 planes ``[3, B, T, 3*H*64]`` of a packed QKV tensor. ``out`` is
-    fp32 ``[B, T, H*64]`` or bf16 ``[3, B, T, H*64]`` (the output leaves as x3 planes)."""
+    fp32 ``[B, T, H*64]`` or bf16 ``[3, B, T, H*64]`` (the output leaves as x3 planes); the heads run
+    ``head_block`` at a time (default: all)."""
     _, B, T, _ = planes.shape
     ws = torch.empty(waves * 2 * (64 * 32 + 64) * attention_x3_group(), dtype=torch.float32, device=planes.device)
     x3_out = out.dtype == torch.bfloat16
-    _check(_L().nos_attention_x3_sk(planes.data_ptr(), planes[0].numel(), None if x3_out else out.data_ptr(),
-                                    out.data_ptr() if x3_out else None, ws.data_ptr(), B, T, heads, head_dim, scale,
-                                    waves, _stream()))
+    hb = heads if head_block is None else max(1, min(heads, int(head_block)))
+    for h0 in range(0, heads, hb):
+        _check(_L().nos_attention_x3_sk_heads(planes.data_ptr(), planes[0].numel(),
+                                              None if x3_out else out.data_ptr(), out.data_ptr() if x3_out else None,
+                                              ws.data_ptr(), B, T, heads, h0, min(hb, heads - h0), head_dim, scale,
+                                              waves, _stream()))
     return out
 
 
@@ -185,7 +208,9 @@ def attention_qkv_x3(planes: torch.Tensor, heads: int, head_dim: int, scale: flo
         qkv = (planes[0].double() + planes[1].double() + planes[2].double()).float()
         return split3(attention_ref(qkv, heads, head_dim, scale))
     out = torch.empty(3, B, T, heads * head_dim, dtype=torch.bfloat16, device=planes.device)
-    return attention_x3(planes, out, heads, head_dim, scale, attention_x3_waves(slice_cus(), B, T, heads))
+    cus = slice_cus()
+    hb = attention_head_block(cus, heads)
+    return attention_x3(planes, out, heads, head_dim, scale, attention_x3_waves(cus, B, T, hb), head_block=hb)
 
 
 def set_backend(name: str) -> None:
@@ -210,6 +235,7 @@ def _L() -> ctypes.CDLL:
             L = load(LIB)
             vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
             L.nos_layernorm_f32.argtypes = [vp, vp, vp, vp, vp, i32, i32, f32, vp]
+            L.nos_layernorm_f32_grid.argtypes = [vp, vp, vp, vp, vp, i32, i32, f32, i32, vp]
             L.nos_bias_gelu_f32.argtypes = [vp, vp, i32, i32, vp]
             L.nos_attention_f32.argtypes = [vp, vp, i32, i32, i32, i32, f32, vp]
             L.nos_attention_f32_sk.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
@@ -220,6 +246,8 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
             L.nos_attention_x3_set_group.argtypes = [i32]
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
+                                                    i32, vp]
             group = os.environ.get("NOS_ATTN_X3_GROUP")  # A/B switch for whole-model runs
             if group and L.nos_attention_x3_set_group(int(group)) != 0:
                 raise RuntimeError(f"NOS_ATTN_X3_GROUP={group}: {L.nos_kernels_last_error().decode()}")
@@ -246,6 +274,15 @@ def _check(rc: int) -> None:
         raise RuntimeError(f"nos kernel failed: {_L().nos_kernels_last_error().decode()} (rc={rc})")
 
 
+def layernorm_wgs(rows: int) -> int:
+    """LayerNorm workgroups (4 rows each, grid-stride): one per 4 rows on the whole GPU; a slice that
+    shares the GPU launches ``NOS_LN_WG_PER_CU`` (default 4) per CU of the slice."""
+    cus = slice_cus()
+    if cus >= total_cus():
+        return 0
+    return cus * int(os.environ.get("NOS_LN_WG_PER_CU", "4"))
+
+
 def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
     if not _use_hip(x) or x.dtype != torch.float32:
         return F.layer_norm(x, (x.shape[-1],), w, b, eps)
@@ -255,8 +292,8 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> 
     if D % 4 != 0 or D > 64 * 4 * 8:
         return F.layer_norm(x, (D,), w, b, eps)
     out = torch.empty_like(x)
-    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), None, rows, D, eps,
-                                  _stream()))
+    _check(_L().nos_layernorm_f32_grid(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), None, rows, D, eps,
+                                       layernorm_wgs(rows), _stream()))
     return out
 
 
@@ -268,8 +305,8 @@ def layernorm_x3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) 
     D = x.shape[-1]
     rows = x.numel() // D
     out = torch.empty((3,) + tuple(x.shape), dtype=torch.bfloat16, device=x.device)
-    _check(_L().nos_layernorm_f32(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, out.data_ptr(), rows, D, eps,
-                                  _stream()))
+    _check(_L().nos_layernorm_f32_grid(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, out.data_ptr(), rows, D, eps,
+                                       layernorm_wgs(rows), _stream()))
     return out
 
 
@@ -375,7 +412,10 @@ def attention_qkv(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) ->
     B, T, _ = qkv.shape
     out = torch.empty(B, T, heads * head_dim, dtype=qkv.dtype, device=qkv.device)
     if get_fp32_matmul() == "x3":
-        return attention_x3(split3(qkv), out, heads, head_dim, scale, attention_x3_waves(slice_cus(), B, T, heads))
+        cus = slice_cus()
+        hb = attention_head_block(cus, heads)
+        return attention_x3(split3(qkv), out, heads, head_dim, scale, attention_x3_waves(cus, B, T, hb),
+                            head_block=hb)
     return attention_sk(qkv, out, heads, head_dim, scale, attention_waves(slice_cus(), B, T, heads))
 
 
