@@ -765,17 +765,20 @@ const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
 // S3/S2; 15-17 = 2-wave 32x64 S3/S2, 64x32 S2; 18-22 = 64-deep stages (128-byte row segments):
 // 64x64 S2/S3, 64x32 S2, 32x64 S2, 64x32 S3; 23/24 = 64-deep on 8 waves: 128x64 S2, 64x128 S2;
 // 25/26 = 128x64 S4, 64x128 S4 (three stages in flight); 27-31 = v_mfma 16x16x32: 64x64 S2,
-// 64x64 S3, 128x128 S2 (8 waves), 32x64 S2 (2 waves), 64x32 S2 (2 waves).
-static const int kCfgX3[32][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// 64x64 S3, 128x128 S2 (8 waves), 32x64 S2 (2 waves), 64x32 S2 (2 waves); 32-34 = 96/192-wide
+// tiles (three 32-column blocks per wave), so N = 384 / 1536 split into 216 tiles at M = 3401 — one
+// round on 256 CUs instead of 1.3-2.5: 128x192 S2, 64x96 S2 (2 waves), 64x192 S2 (2 waves).
+static const int kCfgX3[35][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
                                   {32, 64, 3}, {32, 64, 2}, {64, 32, 2},
                                   {64, 64, 2}, {64, 64, 3}, {64, 32, 2}, {32, 64, 2}, {64, 32, 3},
                                   {128, 64, 2}, {64, 128, 2}, {128, 64, 4}, {64, 128, 4},
-                                  {64, 64, 2}, {64, 64, 3}, {128, 128, 2}, {32, 64, 2}, {64, 32, 2}};
+                                  {64, 64, 2}, {64, 64, 3}, {128, 128, 2}, {32, 64, 2}, {64, 32, 2},
+                                  {128, 192, 2}, {64, 96, 2}, {64, 192, 2}};
 
-int nos_gemm_x3_num_configs() { return 32; }
+int nos_gemm_x3_num_configs() { return 35; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
@@ -814,7 +817,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 31) return -1;
+  if (cfg < 0 || cfg > 34) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];
@@ -877,6 +880,9 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
     case 29: return launch_d<128, 128, 2, 4, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 30: return launch_d<32, 64, 1, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 31: return launch_d<64, 32, 2, 1, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 32: return launch_d<128, 192, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 33: return launch_d<64, 96, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 34: return launch_d<64, 192, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;

@@ -151,18 +151,28 @@ def attention_x3_group() -> int:
 
 
 def attention_x3_waves(cus: int, B: int = 0, T: int = 0, H: int = 0) -> int:
-    """Persistent grid of the x3 attention kernel (same sizing rule as the f32 LDS kernel)."""
+    """Persistent grid of the x3 attention kernel (same sizing rule as the f32 LDS kernel), trimmed
+    to the largest multiple of half the query-group count when that keeps >= 90% of the slots: then
+    stream-K segment boundaries fall on (or halfway through) query groups, so each workgroup runs
+    one or two whole key ranges with one prologue each. Measured on the whole GPU (T = 3401, 84
+    groups): 252 workgroups 100 us vs 256 120 us (`profiles/attn_grid_r2.json`); DPX 126 vs 128:
+    145 vs 153 us; smaller slices keep every slot."""
     global _x3_wg
     if _x3_wg is None:
         _x3_wg = int(_L().nos_attention_x3_wg_per_cu())
     per_cu = _x3_wg
-    if T:
-        nk = (T + 31) // 32
-        g = attention_x3_group()
-        units = B * H * ((nk + g - 1) // g) * nk
-        while per_cu > 1 and units / (per_cu * cus) < 30:
-            per_cu -= 1
-    return per_cu * cus
+    if not T:
+        return per_cu * cus
+    nk = (T + 31) // 32
+    g = attention_x3_group()
+    groups = B * H * ((nk + g - 1) // g)
+    units = groups * nk
+    while per_cu > 1 and units / (per_cu * cus) < 30:
+        per_cu -= 1
+    slots = per_cu * cus
+    half = max(1, groups // 2) if groups % 2 == 0 else groups
+    aligned = (slots // half) * half
+    return aligned if aligned >= 0.9 * slots else slots
 
 
 _head_block: Optional[int] = None
