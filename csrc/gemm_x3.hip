@@ -56,6 +56,19 @@ __device__ __forceinline__ void xcd_band(int w, int P, int tiles, int& base, int
   base = x * q + min(x, r) + li, stride = px, count = li < n ? (n - li + px - 1) / px : 0;
 }
 
+// Grouped tile order: logical tile t walks GROUP tile rows down a column before moving right, so
+// the tiles an XCD runs at once cover GROUP rows x (its workgroups / GROUP) columns — A and W
+// slices that fit its 4 MB L2 together — instead of one row of tiles sweeping all of W. GROUP
+// rides in bits 8-15 of the epilogue word (1 = plain row-major order).
+__device__ __forceinline__ void tile_rc(int t, int tiles_m, int tiles_n, int group, int& mt, int& nt) {
+  if (group <= 1) {
+    mt = t / tiles_n, nt = t % tiles_n;
+    return;
+  }
+  const int per = group * tiles_n, g = t / per, r0 = g * group, gs = min(tiles_m - r0, group), o = t - g * per;
+  mt = r0 + o % gs, nt = o / gs;
+}
+
 __device__ __forceinline__ f32x16 mfma_x3(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
                                           const bf16x8& b1, const bf16x8& b2, f32x16 d) {
   d = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, d, 0, 0, 0);
@@ -202,11 +215,15 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
   __shared__ __attribute__((aligned(16))) __bf16 As[NBUF][3 * BM * LSTR];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NBUF][3 * BN * LSTR];
 
-  const int tiles_n = N / BN;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int group = (epi >> 8) & 0xff;
+  epi &= 0xff;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int tiles = tiles_m * tiles_n;
   const int t = xcd_major(blockIdx.x, gridDim.x);
   if (t >= tiles) return;
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int mt, nt;
+  tile_rc(t, tiles_m, tiles_n, group, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -518,11 +535,15 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS], B2[S > 2 ? 3 * BN * BKS : 8],
       B3[S > 3 ? 3 * BN * BKS : 8];
 
-  const int tiles_n = N / BN;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int group = (epi >> 8) & 0xff;
+  epi &= 0xff;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int tiles = tiles_m * tiles_n;
   const int t = xcd_major(blockIdx.x, gridDim.x);
   if (t >= tiles) return;
-  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  int mt, nt;
+  tile_rc(t, tiles_m, tiles_n, group, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS bases stay scalar
@@ -653,8 +674,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
   __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS],
       B2[S > 2 ? 3 * BN * BKS : 8], B3[S > 3 ? 3 * BN * BKS : 8];
 
-  const int tiles_n = N / BN;
-  const int tiles = ((M + BM - 1) / BM) * tiles_n;
+  const int group = (epi >> 8) & 0xff;
+  epi &= 0xff;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int tiles = tiles_m * tiles_n;
   int tb, ts, tcount;
   xcd_band(blockIdx.x, gridDim.x, tiles, tb, ts, tcount);
   if (tcount <= 0) return;
@@ -679,9 +702,11 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
   {                                                                                       \
     const int h_ = (H);                                                                   \
     const int ti_ = h_ / nk, ks_ = h_ - ti_ * nk, t_ = tb + ti_ * ts;                     \
+    int mt_, nt_;                                                                         \
+    tile_rc(t_, tiles_m, tiles_n, group, mt_, nt_);                                       \
     uint32_t va_[BM / RPI / NW], vb_[BN / RPI / NW];                                      \
-    dma_offsets<BM, NW, BKS>(va_, (t_ / tiles_n) * BM, M - 1, K, wave, lane);             \
-    dma_offsets<BN, NW, BKS>(vb_, (t_ % tiles_n) * BN, N - 1, K, wave, lane);             \
+    dma_offsets<BM, NW, BKS>(va_, mt_ * BM, M - 1, K, wave, lane);                        \
+    dma_offsets<BN, NW, BKS>(vb_, nt_ * BN, N - 1, K, wave, lane);                        \
     dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3S_A(BUF), wave);                 \
     dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3S_B(BUF), wave);                 \
   }
@@ -690,7 +715,9 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
     compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3S_A(BUF), X3S_B(BUF), wm, wn, j, hf);    \
     if (((G) + 1) % nk == 0) {                                                            \
       const int t_ = tb + ((G) / nk) * ts;                                                \
-      store_tile<TM, TN>(acc, (t_ / tiles_n) * BM + wm * WM, (t_ % tiles_n) * BN + wn * WN, j, hf, bias, R, R2, \
+      int mt_, nt_;                                                                       \
+      tile_rc(t_, tiles_m, tiles_n, group, mt_, nt_);                                     \
+      store_tile<TM, TN>(acc, mt_ * BM + wm * WM, nt_ * BN + wn * WN, j, hf, bias, R, R2,   \
                          r2_rows, C, Cp, c_plane, M, N, epi);                             \
       _Pragma("unroll") for (int a = 0; a < TM; ++a)                                      \
         _Pragma("unroll") for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};             \
@@ -754,9 +781,21 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
 }
 }  // namespace
 
+static int g_group_m = 1;
+
 extern "C" {
 
 const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
+
+// grouped tile order (tile rows per group, 1..255; 1 = row-major): see tile_rc
+int nos_gemm_x3_set_group(int g) {
+  if (g < 1 || g > 255) {
+    g_err = "gemm_x3: group must be 1..255";
+    return -1;
+  }
+  g_group_m = g;
+  return 0;
+}
 
 // Tile configurations (BM x BN, LDS buffers, load stages in flight): 0 = 64x64, 1 = 128x64,
 // 2 = 64x128, 3 = 128x128 (double-buffered LDS); 4 = 64x64, 5 = 128x64, 6 = 64x128 (single-buffered:
@@ -799,6 +838,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  epi |= g_group_m << 8;
   switch (cfg) {
     case 0: return launch_s<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 1: return launch_s<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
@@ -847,6 +887,7 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  epi |= g_group_m << 8;
   switch (cfg) {
     case 0: return launch<32, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 1: return launch<64, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);

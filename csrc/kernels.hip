@@ -304,8 +304,12 @@ __global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ 
 // 4 MB L2 holds at most two heads' K/V (1.7 MB each at T=3401) instead of all of them.
 __device__ __forceinline__ long long sk_begin(long long w, long long U, long long P) { return w * U / P; }
 
+// any P: XCD x (= phys % 8) owns the contiguous logical run of its P/8 (+1 for the first P % 8
+// XCDs) workgroups — a bijection, so a grid trimmed to query-group boundaries (252 on 256 CUs)
+// keeps each XCD on about one head's K/V
 __device__ __forceinline__ int sk_logical(int phys, int P) {
-  return (P % 8 == 0) ? (phys % 8) * (P / 8) + phys / 8 : phys;
+  const int x = phys % 8, q = P / 8, r = P % 8;
+  return x * q + min(x, r) + phys / 8;
 }
 
 template <int WPE>

@@ -241,8 +241,23 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3_persistent.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32,
                                              i32, vp]
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
+        L.nos_gemm_x3_set_group.argtypes = [i32]
+        g = int(os.environ.get("NOS_X3_GROUP_M", str(X3_GROUP_M)))
+        if L.nos_gemm_x3_set_group(g) != 0:
+            raise RuntimeError(f"NOS_X3_GROUP_M={g}: {L.nos_gemm_x3_last_error().decode()}")
         _x3_bound = True
     return L
+
+
+#: tile rows per group of the x3 GEMMs' grouped tile order (1 = row-major); NOS_X3_GROUP_M overrides
+X3_GROUP_M = 1
+
+
+def set_group_m(g: int) -> None:
+    """Grouped tile order of the x3 GEMMs: ``g`` tile rows walked per column step (1 = row-major)."""
+    L = _lib_x3()
+    if L.nos_gemm_x3_set_group(int(g)) != 0:
+        raise ValueError(L.nos_gemm_x3_last_error().decode())
 
 
 def weight_planes(w: torch.Tensor) -> torch.Tensor:
