@@ -918,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
 // G = query tiles (waves) per workgroup sharing each K/V block: 4 (two workgroups per CU) or 8 (one
 // 512-thread workgroup per CU: half the K/V bytes per query, the L2/Infinity-Cache traffic that
 // concurrent partitions share; the K and V loads are split between the two halves of the group).
-template <int G>
+template <int G, bool QW = false>
 __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -1016,6 +1016,11 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     }
     __syncthreads();
 
+    // the Q fragments (and the first K/V blocks) have landed: say so explicitly, or the waitcnt
+    // pass, merging the loop's back edge with this entry, keeps a vmcnt wait on the Q loads in
+    // front of every block's score MFMAs — which in steady state waits for the K/V prefetch
+    // issued at the top of that same iteration (its global-load latency on the critical path)
+    if constexpr (QW) __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0)
     f32x16 o0 = {0}, o1 = {0}, scur = {0};
     float m = -INFINITY, l = 0.f;
     if (active) X3P_QK(scur, 0)
@@ -1230,6 +1235,12 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
 }
 
 static int g_x3_pipelined = 1;
+static int g_x3_flags = 0;  // bit 0: explicit vmcnt(0) after a segment's Q/K/V prologue (A/B switch)
+
+int nos_attention_x3_set_flags(int f) {
+  g_x3_flags = f;
+  return 0;
+}
 static int g_x3_group = 8;  // query tiles per workgroup of the pipelined x3 kernel (4 or 8; 8 measured faster)
 
 // 4 = two 256-thread workgroups per CU, 8 = one 512-thread workgroup sharing K/V (default)
@@ -1304,6 +1315,9 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
                        sl2, waves);
+  else if (G == 8 && (g_x3_flags & 1))
+    hipLaunchKernelGGL((attn_fwd_x3p<8, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
+                       part_ml, B, T, hn, h0, H, sl2, waves);
   else if (G == 8)
     hipLaunchKernelGGL(attn_fwd_x3p<8>, dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
                        T, hn, h0, H, sl2, waves);

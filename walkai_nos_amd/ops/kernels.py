@@ -258,6 +258,8 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                                                     i32, vp]
+            L.nos_attention_x3_set_flags.argtypes = [i32]
+            L.nos_attention_x3_set_flags(int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))
             group = os.environ.get("NOS_ATTN_X3_GROUP")  # A/B switch for whole-model runs
             if group and L.nos_attention_x3_set_group(int(group)) != 0:
                 raise RuntimeError(f"NOS_ATTN_X3_GROUP={group}: {L.nos_kernels_last_error().decode()}")
