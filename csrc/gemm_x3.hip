@@ -535,7 +535,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS], B2[S > 2 ? 3 * BN * BKS : 8],
       B3[S > 3 ? 3 * BN * BKS : 8];
 
-  const int group = (epi >> 8) & 0xff;
+  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7;
   epi &= 0xff;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
@@ -581,8 +581,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
     const int k0_ = (STAGE) * BKS;                                                 \
-    dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave);            \
-    dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave);            \
+    if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave); \
+    if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave); \
   }
 #define X3D_ITER(KS, BUF)                                                          \
   {                                                                                \
@@ -615,16 +615,18 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #undef X3D_B
 #undef X3D_A
   vm_wait<0>();  // no DMA may still target this workgroup's LDS when it retires
-  // direct stores: each instruction writes whole 64/128-byte row segments of two rows. Re-shaping
-  // the tile for wider per-lane vectors was measured: through lane-quad DPP transposes it was
-  // slower; through an LDS scratch in the freed stage buffers it was faster but produced
-  // run-to-run differences whenever several workgroups shared a CU (tools/x3_gemm_stress.py),
-  // cause not pinned down, so it is not used.
+  // direct stores: each instruction writes whole 64/128-byte row segments of two rows. Wider
+  // per-lane vectors were measured: through lane-quad DPP transposes slower; through a dedicated
+  // wave-private LDS scratch (16-byte row chunks, 8x fewer store instructions for x3 planes)
+  // correct run to run but no faster (qkv 27.6 vs 27.6 us, fc1 47.4 vs 46.3 on the whole GPU):
+  // the plane bytes, not the instruction count, set the epilogue's time. (A scratch in the freed
+  // stage buffers had given run-to-run differences with several workgroups per CU.)
   if constexpr (M16)
     store_tile16<TM16, TN16>(acc16, m0 + wm * WM, n0 + wn * WN, lane, bias, R, R2, r2_rows, C, Cp, c_plane, M, N,
                              epi);
   else
-    store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
+    if (!(ablate & 4))
+      store_tile<TM, TN>(acc, m0 + wm * WM, n0 + wn * WN, j, hf, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
 }
 
 template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32, bool M16 = false>
@@ -674,7 +676,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
   __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS],
       B2[S > 2 ? 3 * BN * BKS : 8], B3[S > 3 ? 3 * BN * BKS : 8];
 
-  const int group = (epi >> 8) & 0xff;
+  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7;
   epi &= 0xff;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
@@ -707,8 +709,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
     uint32_t va_[BM / RPI / NW], vb_[BN / RPI / NW];                                      \
     dma_offsets<BM, NW, BKS>(va_, mt_ * BM, M - 1, K, wave, lane);                        \
     dma_offsets<BN, NW, BKS>(vb_, nt_ * BN, N - 1, K, wave, lane);                        \
-    dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3S_A(BUF), wave);                 \
-    dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3S_B(BUF), wave);                 \
+    if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3S_A(BUF), wave); \
+    if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3S_B(BUF), wave); \
   }
 #define X3S_BODY(G, BUF)                                                                  \
   {                                                                                       \
@@ -717,7 +719,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
       const int t_ = tb + ((G) / nk) * ts;                                                \
       int mt_, nt_;                                                                       \
       tile_rc(t_, tiles_m, tiles_n, group, mt_, nt_);                                     \
-      store_tile<TM, TN>(acc, mt_ * BM + wm * WM, nt_ * BN + wn * WN, j, hf, bias, R, R2,   \
+      if (!(ablate & 4)) store_tile<TM, TN>(acc, mt_ * BM + wm * WM, nt_ * BN + wn * WN, j, hf, bias, R, R2, \
                          r2_rows, C, Cp, c_plane, M, N, epi);                             \
       _Pragma("unroll") for (int a = 0; a < TM; ++a)                                      \
         _Pragma("unroll") for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};             \
@@ -782,10 +784,16 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
 }  // namespace
 
 static int g_group_m = 1;
+static int g_ablate = 0;  // timing studies only: 1 = skip the A operand loads, 2 = skip W (results invalid)
 
 extern "C" {
 
 const char* nos_gemm_x3_last_error() { return g_err.c_str(); }
+
+int nos_gemm_x3_set_ablate(int a) {
+  g_ablate = a & 7;
+  return 0;
+}
 
 // grouped tile order (tile rows per group, 1..255; 1 = row-major): see tile_rc
 int nos_gemm_x3_set_group(int g) {
@@ -838,7 +846,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  epi |= g_group_m << 8;
+  epi |= (g_group_m << 8) | (g_ablate << 16);
   switch (cfg) {
     case 0: return launch_s<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 1: return launch_s<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
@@ -887,7 +895,7 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  epi |= g_group_m << 8;
+  epi |= (g_group_m << 8) | (g_ablate << 16);
   switch (cfg) {
     case 0: return launch<32, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 1: return launch<64, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);

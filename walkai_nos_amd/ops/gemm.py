@@ -242,6 +242,8 @@ def _lib_x3() -> ctypes.CDLL:
                                              i32, vp]
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         L.nos_gemm_x3_set_group.argtypes = [i32]
+        L.nos_gemm_x3_set_ablate.argtypes = [i32]
+        L.nos_gemm_x3_set_ablate(int(os.environ.get("NOS_X3_ABLATE", "0")))  # timing studies only
         g = int(os.environ.get("NOS_X3_GROUP_M", str(X3_GROUP_M)))
         if L.nos_gemm_x3_set_group(g) != 0:
             raise RuntimeError(f"NOS_X3_GROUP_M={g}: {L.nos_gemm_x3_last_error().decode()}")
