@@ -189,3 +189,42 @@ def test_weight_planes_cached_on_tensor_and_invalidated_by_writes():
     assert torch.equal(p2[0].float() + p2[1].float() + p2[2].float(), w.detach().reshape(8, -1))
     other = torch.randn(8, 12)                             # a different tensor never hits w's cache
     assert torch.equal(G.weight_planes(other)[0], other.to(torch.bfloat16))
+
+
+def test_attention_x3_grid_trimmed_to_query_group_boundaries(monkeypatch):
+    # 84 query groups (T = 3401, 6 heads, 8 query tiles per workgroup): 256 CUs -> 252 = 84 x 3,
+    # DPX 128 -> 126 = 84 x 1.5; slices with fewer slots than groups keep every slot
+    from walkai_nos_amd.ops import kernels as K
+    monkeypatch.setattr(K, "_x3_wg", 1)
+    monkeypatch.setattr(K, "attention_x3_group", lambda: 8)
+    assert [K.attention_x3_waves(c, 1, 3401, 6) for c in (256, 128, 64, 32)] == [252, 126, 64, 32]
+    assert K.attention_x3_waves(256) == 256  # no shape: every slot
+
+
+def test_x3_tuned_table_lookup(monkeypatch, tmp_path):
+    import json
+    from walkai_nos_amd.ops import gemm as G
+    p = tmp_path / "x3_tuned.json"
+    p.write_text(json.dumps({"M3401_N1152_K384_epi1_out2_cus32": {"tile": 102, "concurrent_us": 1.0},
+                             "M1_N1_K32_epi0_out1_cus32": {"tile": 999}}))
+    monkeypatch.setattr(G, "_TUNED_PATH", str(p))
+    monkeypatch.setattr(G, "_tuned", None)
+    t = G.tuned_table()
+    assert t == {"M3401_N1152_K384_epi1_out2_cus32": 102}  # unknown tile ids are dropped
+    monkeypatch.setattr(G, "_tuned", None)
+    monkeypatch.setenv("NOS_X3_TUNED", "0")
+    assert G.tuned_table() == {}
+    monkeypatch.setattr(G, "_tuned", None)
+
+
+def test_shipped_x3_tuned_table_names_known_tiles():
+    import json
+    import os
+    from walkai_nos_amd.ops import gemm as G
+    with open(G._TUNED_PATH) as f:
+        table = json.load(f)
+    for key, v in table.items():
+        assert v["tile"] in G.X3_TILES, key
+        n = int(key.split("_")[1][1:])
+        assert n % G.X3_TILES[v["tile"]][1] == 0, key
+    assert os.path.basename(G._TUNED_PATH) == "x3_tuned.json"
