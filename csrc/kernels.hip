@@ -918,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
 // G = query tiles (waves) per workgroup sharing each K/V block: 4 (two workgroups per CU) or 8 (one
 // 512-thread workgroup per CU: half the K/V bytes per query, the L2/Infinity-Cache traffic that
 // concurrent partitions share; the K and V loads are split between the two halves of the group).
-template <int G, bool QW = false>
+template <int G, bool QW = false, bool F32IN = false>
 __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -950,6 +950,10 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     const int head = h0 + int((grp / QG) % H);
     const int b = int(grp / ((long long)QG * H));
     const __bf16* base = qkv3 + size_t(b) * T * ld;
+    // F32IN: qkv arrives as fp32 [B][T][3D] (4 B per element instead of three 2-B planes) and is
+    // split here — Q once per segment, each K/V chunk as it is stashed (the same RNE split the
+    // producers use, so the planes are bit-identical to a planes-in run)
+    const float* basef = reinterpret_cast<const float*>(qkv3) + size_t(b) * T * ld;
     const int qt = qg * G + wv;
     const bool active = qt < QT;
     const int q0 = qt * 32;
@@ -957,34 +961,66 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     bf16x8 qf[3][4];
     {
       const int qrow = min(q0 + j, T - 1);
-      const __bf16* qp = base + size_t(qrow) * ld + head * HD + 8 * hf;
+      if constexpr (F32IN) {
+        const float* qp = basef + size_t(qrow) * ld + head * HD + 8 * hf;
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+        for (int s = 0; s < 4; ++s) {
+          const f32x4 lo = *reinterpret_cast<const f32x4*>(qp + 16 * s);
+          const f32x4 hi = *reinterpret_cast<const f32x4*>(qp + 16 * s + 4);
+          const f32x8 x = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          split3(x, qf[0][s], qf[1][s], qf[2][s]);
+        }
+      } else {
+        const __bf16* qp = base + size_t(qrow) * ld + head * HD + 8 * hf;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) qf[p][s] = *reinterpret_cast<const bf16x8*>(qp + p * plane + 16 * s);
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) qf[p][s] = *reinterpret_cast<const bf16x8*>(qp + p * plane + 16 * s);
+      }
     }
     const __bf16* kg = base + D + head * HD + 8 * lch;
     const __bf16* vg = base + 2 * D + head * HD + 8 * lch;
+    const float* kgf = basef + D + head * HD + 8 * lch;
+    const float* vgf = basef + 2 * D + head * HD + 8 * lch;
     uint4 pk0, pk1, pk2, pv0, pv1, pv2;
+    f32x4 fk0, fk1, fv0, fv1;  // F32IN staging: the chunk's 8 fp32 values
     auto fetch_k = [&](int blk) {
       const size_t r = size_t(min(blk * 32 + lrow, T - 1)) * ld;
-      pk0 = *reinterpret_cast<const uint4*>(kg + r);
-      pk1 = *reinterpret_cast<const uint4*>(kg + plane + r);
-      pk2 = *reinterpret_cast<const uint4*>(kg + 2 * plane + r);
+      if constexpr (F32IN) {
+        fk0 = *reinterpret_cast<const f32x4*>(kgf + r);
+        fk1 = *reinterpret_cast<const f32x4*>(kgf + r + 4);
+      } else {
+        pk0 = *reinterpret_cast<const uint4*>(kg + r);
+        pk1 = *reinterpret_cast<const uint4*>(kg + plane + r);
+        pk2 = *reinterpret_cast<const uint4*>(kg + 2 * plane + r);
+      }
     };
     auto fetch_v = [&](int blk) {
       const size_t r = size_t(min(blk * 32 + lrow, T - 1)) * ld;
-      pv0 = *reinterpret_cast<const uint4*>(vg + r);
-      pv1 = *reinterpret_cast<const uint4*>(vg + plane + r);
-      pv2 = *reinterpret_cast<const uint4*>(vg + 2 * plane + r);
+      if constexpr (F32IN) {
+        fv0 = *reinterpret_cast<const f32x4*>(vgf + r);
+        fv1 = *reinterpret_cast<const f32x4*>(vgf + r + 4);
+      } else {
+        pv0 = *reinterpret_cast<const uint4*>(vg + r);
+        pv1 = *reinterpret_cast<const uint4*>(vg + plane + r);
+        pv2 = *reinterpret_cast<const uint4*>(vg + 2 * plane + r);
+      }
+    };
+    auto split_chunk = [](const f32x4& lo, const f32x4& hi, uint4& c0, uint4& c1, uint4& c2) {
+      const f32x8 x = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      bf16x8 a0, a1, a2;
+      split3(x, a0, a1, a2);
+      c0 = __builtin_bit_cast(uint4, a0), c1 = __builtin_bit_cast(uint4, a1), c2 = __builtin_bit_cast(uint4, a2);
     };
     auto stash_k = [&](int buf) {
+      if constexpr (F32IN) split_chunk(fk0, fk1, pk0, pk1, pk2);
       __bf16* kd = &lds_k[buf * 3 * XK_PLANE + lrow * XK_STR + 8 * lch];
       *reinterpret_cast<uint4*>(kd) = pk0;
       *reinterpret_cast<uint4*>(kd + XK_PLANE) = pk1;
       *reinterpret_cast<uint4*>(kd + 2 * XK_PLANE) = pk2;
     };
     auto stash_v = [&](int buf) {
+      if constexpr (F32IN) split_chunk(fv0, fv1, pv0, pv1, pv2);
       __bf16* vd = &lds_v[buf * 3 * XV_PLANE + lrow * XV_STR + 8 * lch];
       *reinterpret_cast<uint4*>(vd) = pv0;
       *reinterpret_cast<uint4*>(vd + XV_PLANE) = pv1;
@@ -1278,8 +1314,9 @@ int nos_attention_x3_wg_per_cu() {
 // workgroups share one block's K/V in L2 (with every head in flight at once, the K/V planes of all
 // heads are the L2 working set — the traffic concurrent partitions contend for). Workspace:
 // nos_attention_ws_bytes of the LDS variant (variant 0 layout), merged by the same fixup kernel.
-int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
-                              int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream) {
+static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
+                               int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream,
+                               bool f32in) {
   if ((out == nullptr) == (outp == nullptr)) {
     g_err = "attention x3: exactly one of out / outp";
     return -1;
@@ -1304,6 +1341,10 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
     g_err = "attention x3: head blocks need the pipelined kernel";
     return -1;
   }
+  if (f32in && (!g_x3_pipelined || nos_attention_x3_group() != 8)) {
+    g_err = "attention x3: fp32 input needs the pipelined 8-tile kernel";
+    return -1;
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int G = nos_attention_x3_group();
   const int NK = (T + 31) / 32, QG = (NK + G - 1) / G;
@@ -1315,6 +1356,9 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
                        sl2, waves);
+  else if (G == 8 && f32in)
+    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
+                       part_ml, B, T, hn, h0, H, sl2, waves);
   else if (G == 8 && (g_x3_flags & 1))
     hipLaunchKernelGGL((attn_fwd_x3p<8, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
                        part_ml, B, T, hn, h0, H, sl2, waves);
@@ -1332,6 +1376,17 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
     hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * hn * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
                        waves, op, h0, H);
   return check_launch("attn_sk_lds_fixup");
+}
+
+int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
+                              int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream) {
+  return attention_x3_launch(qkv3, plane_stride, out, outp, ws, B, T, H, h0, hn, head_dim, scale, waves, stream, false);
+}
+
+// the same from an fp32 packed QKV tensor [B, T, 3*H*64] (split to planes inside the kernel)
+int nos_attention_x3f_sk_heads(const float* qkv, float* out, void* outp, float* ws, int B, int T, int H, int h0,
+                               int hn, int head_dim, float scale, int waves, void* stream) {
+  return attention_x3_launch(qkv, 8, out, outp, ws, B, T, H, h0, hn, head_dim, scale, waves, stream, true);
 }
 
 int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B, int T,

@@ -357,3 +357,20 @@ def test_yolos_x3_matches_f32_mode(K):
     e3, e32 = (l3 - lt).abs().max().item(), (l32 - lt).abs().max().item()
     assert e3 < 1e-3 and e32 < 1e-3, (e3, e32)
     assert (b3 - bt).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("T,H,B", [(1000, 2, 1), (3401, 6, 1), (77, 1, 2)])
+def test_attention_x3_fp32_input_equals_planes_input(K, T, H, B):
+    # the fp32-input kernel splits Q/K/V in-kernel exactly as split3 does: bit-identical planes out
+    torch.manual_seed(4)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    for waves, hb in ((7, None), (252, None), (64, 1)):
+        a = torch.empty(3, B, T, H * 64, dtype=torch.bfloat16, device="cuda")
+        b = torch.empty_like(a)
+        K.attention_x3(K.split3(qkv), a, H, 64, 0.125, waves, head_block=hb)
+        K.attention_x3f(qkv, b, H, 64, 0.125, waves, head_block=hb)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b), (waves, hb)
+        out = b[0].float() + b[1].float() + b[2].float()
+        assert (out - ref).abs().max().item() < 2e-6

@@ -48,6 +48,11 @@ class SliceOps:
         from walkai_nos_amd.ops.gemm import gemm_x3
         if name == "qkv":
             return lambda: gemm_x3(self.h3, self.w["qkv"], self.b["qkv"], out_f32=False, out_x3=True, tile=tile)
+        if name == "qkv_f32":  # the same GEMM with an fp32 output (4 B per element instead of 6)
+            return lambda: gemm_x3(self.h3, self.w["qkv"], self.b["qkv"], out_f32=True, out_x3=False, tile=tile)
+        if name == "fc1_f32":
+            return lambda: gemm_x3(self.h3, self.w["fc1"], self.b["fc1"], gelu=True, out_f32=True, out_x3=False,
+                                   tile=tile)
         if name == "proj":
             return lambda: gemm_x3(self.h3, self.w["proj"], self.b["proj"], residual=self.x, tile=tile)
         if name == "fc1":
@@ -144,7 +149,7 @@ def main() -> int:
             cases += [("ln", ("ln", int(v))) for v in a.ln_wg_per_cu.split(",")]
         elif a.tiles == "all":
             from walkai_nos_amd.ops.gemm import x3_eligible
-            w = slices[0].w[name]
+            w = slices[0].w[name.replace("_f32", "")]
             cases += [(name, ("tile", c)) for c in x3_eligible(w.shape[0], w.shape[1])]
         elif a.tiles:
             cases += [(name, ("tile", int(t))) for t in a.tiles.split(",")]

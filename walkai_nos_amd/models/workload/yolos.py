@@ -79,8 +79,13 @@ class _Block(nn.Module):
             # every fp32 product on the bf16 matrix cores in x3 form: activations leave their
             # producer as three exact bf16 planes; the residual stream stays fp32
             h3 = K.layernorm_x3(x, self.ln1.weight, self.ln1.bias, self.c.layer_norm_eps)
-            qkv3 = K.linear_x3(h3, self.qkv.weight, self.qkv.bias, out_x3=True)
-            o3 = K.attention_qkv_x3(qkv3, H, Dh, 1.0 / math.sqrt(Dh))
+            if K.attention_input_f32():
+                # QKV leaves the GEMM as fp32 (4 B per element); attention splits it in-kernel
+                qkv = K.linear_x3(h3, self.qkv.weight, self.qkv.bias)
+                o3 = K.attention_qkv_x3f(qkv, H, Dh, 1.0 / math.sqrt(Dh))
+            else:
+                qkv3 = K.linear_x3(h3, self.qkv.weight, self.qkv.bias, out_x3=True)
+                o3 = K.attention_qkv_x3(qkv3, H, Dh, 1.0 / math.sqrt(Dh))
             x = K.linear_x3(o3, self.proj.weight, self.proj.bias, residual=x)
             h3 = K.layernorm_x3(x, self.ln2.weight, self.ln2.bias, self.c.layer_norm_eps)
             f3 = K.linear_x3(h3, self.fc1.weight, self.fc1.bias, gelu=True, out_x3=True)

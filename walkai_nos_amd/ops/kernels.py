@@ -211,6 +211,38 @@ def attention_x3(planes: torch.Tensor, out: torch.Tensor, heads: int, head_dim: 
     return out
 
 
+def attention_input_f32() -> bool:
+    """True: the model hands attention an fp32 QKV tensor (the QKV GEMM writes 4 B per element instead
+    of three bf16 planes; the kernel splits Q, K and V itself). ``NOS_ATTN_F32IN=0`` keeps planes."""
+    return os.environ.get("NOS_ATTN_F32IN", "1") != "0" and attention_x3_group() == 8
+
+
+def attention_x3f(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float, waves: int,
+                  head_block: Optional[int] = None) -> torch.Tensor:
+    """:func:`attention_x3` from an fp32 packed QKV tensor ``[B, T, 3*H*64]`` (split in-kernel)."""
+    B, T, _ = qkv.shape
+    qkv = qkv.contiguous()
+    ws = torch.empty(waves * 2 * (64 * 32 + 64) * attention_x3_group(), dtype=torch.float32, device=qkv.device)
+    x3_out = out.dtype == torch.bfloat16
+    hb = heads if head_block is None else max(1, min(heads, int(head_block)))
+    for h0 in range(0, heads, hb):
+        _check(_L().nos_attention_x3f_sk_heads(qkv.data_ptr(), None if x3_out else out.data_ptr(),
+                                               out.data_ptr() if x3_out else None, ws.data_ptr(), B, T, heads, h0,
+                                               min(hb, heads - h0), head_dim, scale, waves, _stream()))
+    return out
+
+
+def attention_qkv_x3f(qkv: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
+    """fp32 packed QKV in, x3 planes ``[3, B, T, H*64]`` of the attention output out."""
+    B, T, _ = qkv.shape
+    if not _use_hip(qkv):
+        return split3(attention_ref(qkv, heads, head_dim, scale))
+    out = torch.empty(3, B, T, heads * head_dim, dtype=torch.bfloat16, device=qkv.device)
+    cus = slice_cus()
+    hb = attention_head_block(cus, heads)
+    return attention_x3f(qkv, out, heads, head_dim, scale, attention_x3_waves(cus, B, T, hb), head_block=hb)
+
+
 def attention_qkv_x3(planes: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
     """x3 planes of packed QKV in, x3 planes ``[3, B, T, H*64]`` of the attention output out."""
     _, B, T, _ = planes.shape
@@ -258,6 +290,7 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                                                     i32, vp]
+            L.nos_attention_x3f_sk_heads.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp]
             L.nos_attention_x3_set_flags.argtypes = [i32]
             L.nos_attention_x3_set_flags(int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))
             group = os.environ.get("NOS_ATTN_X3_GROUP")  # A/B switch for whole-model runs
