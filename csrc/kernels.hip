@@ -918,7 +918,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
 // G = query tiles (waves) per workgroup sharing each K/V block: 4 (two workgroups per CU) or 8 (one
 // 512-thread workgroup per CU: half the K/V bytes per query, the L2/Infinity-Cache traffic that
 // concurrent partitions share; the K and V loads are split between the two halves of the group).
-template <int G, bool QW = false, bool F32IN = false>
+template <int G, bool QW = false, bool F32IN = false, bool PRIO = false>
 __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -1187,6 +1187,11 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
     // VALU phases together; their P planes wait in registers and the V block stays in its buffer
     // (its next refill is staged by these same waves, after the deferred P.V)
     bf16x8 pa0, pa1, pa2, pb0, pb1, pb2;
+    // PRIO: the second-dispatched half (waves 4-7) loses every VALU arbitration against its SIMD
+    // partner at equal priority; one static s_setprio 1 for that half (A/B switch)
+    if constexpr (PRIO) {
+      if (G == 8 && wv >= 4) __builtin_amdgcn_s_setprio(1);
+    }
     if (G == 8 && wv >= 4) {
       for (int i = 0; i < nb;) {
         X3P_ITER_LATE(scur, snext)
@@ -1271,7 +1276,8 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
 }
 
 static int g_x3_pipelined = 1;
-static int g_x3_flags = 0;  // bit 0: explicit vmcnt(0) after a segment's Q/K/V prologue (A/B switch)
+static int g_x3_flags = 0;  // A/B switches: bit 0 explicit vmcnt(0) after a segment's prologue (planes input),
+                            // bit 1 static s_setprio 1 for waves 4-7 (fp32 input)
 
 int nos_attention_x3_set_flags(int f) {
   g_x3_flags = f;
@@ -1356,6 +1362,9 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
                        sl2, waves);
+  else if (G == 8 && f32in && (g_x3_flags & 2))
+    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op,
+                       part_o, part_ml, B, T, hn, h0, H, sl2, waves);
   else if (G == 8 && f32in)
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
                        part_ml, B, T, hn, h0, H, sl2, waves);
