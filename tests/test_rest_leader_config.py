@@ -151,3 +151,57 @@ devicePluginDelaySeconds: 5
     args = load_config("apiVersion: kubescheduler.config.k8s.io/v1beta3\nkind: CapacitySchedulingArgs\n"
                        "amdGpuResourceMemoryGB: 288\n")
     assert isinstance(args, CapacitySchedulingArgs) and args.nvidiaGpuResourceMemoryGB == 288
+
+
+class _RelistStub(BaseHTTPRequestHandler):
+    lists = 0
+
+    def _send(self, code, body):
+        data = json.dumps(body).encode()
+        self.send_response(code)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def do_GET(self):  # noqa: N802
+        if "watch=1" in self.path:
+            self.send_response(200)
+            self.send_header("Content-Type", "application/json")
+            self.end_headers()
+            if _RelistStub.lists == 1:  # the first watch expires: 410 Gone -> re-list
+                self.wfile.write((json.dumps({"type": "ERROR", "object": {"code": 410}}) + "\n").encode())
+            self.wfile.flush()
+            time.sleep(0.3)
+            return None
+        _RelistStub.lists += 1
+        names = ["a", "b"] if _RelistStub.lists == 1 else ["a"]  # "b" was deleted while the watch was down
+        return self._send(200, {"metadata": {"resourceVersion": str(10 + _RelistStub.lists)},
+                                "items": [{"metadata": {"name": n, "resourceVersion": "1"}} for n in names]})
+
+    def log_message(self, *a):
+        return
+
+
+def test_rest_watch_relist_drops_objects_deleted_during_the_gap():
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), _RelistStub)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    _RelistStub.lists = 0
+    try:
+        c = RESTClient(f"http://127.0.0.1:{srv.server_address[1]}")
+        events = []
+        done = threading.Event()
+
+        def h(t, o, old):
+            events.append((t, o["metadata"]["name"]))
+            if t == "DELETED":
+                done.set()
+
+        cancel = c.watch("Node", h)
+        assert done.wait(10)
+        cancel()
+        c.close()
+        assert ("ADDED", "a") in events and ("ADDED", "b") in events
+        assert ("DELETED", "b") in events and ("DELETED", "a") not in events
+    finally:
+        srv.shutdown()

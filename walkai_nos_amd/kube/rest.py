@@ -163,13 +163,20 @@ class RESTClient:
                     if not rv:
                         doc = self._req("GET", self._path(kind))
                         rv = doc.get("metadata", {}).get("resourceVersion", "")
+                        seen = set()
                         for o in doc.get("items", []):
                             o = self._with_kind(o, kind)
                             k = (o["metadata"].get("namespace", ""), o["metadata"]["name"])
+                            seen.add(k)
                             old = cache.get(k)
                             cache[k] = o
                             if replay or old is not None:
                                 handler("ADDED" if old is None else "MODIFIED", o, old)
+                        # a re-list after 410 Gone replaces the mirror: objects deleted while the watch
+                        # was down get their DELETED now (an informer's Replace)
+                        for k in [k for k in cache if k not in seen]:
+                            gone = cache.pop(k)
+                            handler("DELETED", gone, gone)
                     resp = self._req("GET", self._path(kind), query={"watch": "1", "resourceVersion": rv,
                                                                      "allowWatchBookmarks": "true"},
                                      stream=True, timeout=300)
