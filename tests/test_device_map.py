@@ -160,6 +160,45 @@ def test_actuator_stops_gpu_helpers_before_flipping():
     assert p.poll() is not None and e.smi.get_compute_partition(0) == "CPX"
 
 
+def test_no_helper_starts_while_a_flip_holds_the_gate():
+    import threading
+    import time
+    from walkai_nos_amd.parallel.spawned import HelperRegistry
+    reg = HelperRegistry()
+    started = []
+
+    def spawn():
+        p = reg.spawn([sys.executable, "-c", "pass"], timeout=10.0)
+        started.append(time.monotonic())
+        p.wait()
+    with reg.held():
+        t = threading.Thread(target=spawn)
+        t.start()
+        time.sleep(0.3)
+        assert not started  # held back while the flip runs
+        released = time.monotonic()
+    t.join(10)
+    assert started and started[0] >= released
+    with reg.held():
+        with pytest.raises(TimeoutError):
+            reg.spawn([sys.executable, "-c", "pass"], timeout=0.1)
+
+
+def test_actuator_holds_helpers_back_during_the_switch():
+    e = Env(n_gpus=1)
+    seen = []
+    real = e.smi.set_compute_partition
+
+    def switch(gpu, mode):
+        seen.append(e.shared.helpers._held)
+        return real(gpu, mode)
+    e.smi.set_compute_partition = switch
+    e.spec({"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", api.ANNOTATION_PARTITIONING_PLAN: "1"})
+    e.reporter.reconcile(Request("node-a"))
+    e.actuator.reconcile(Request("node-a"))
+    assert seen == [1] and e.shared.helpers._held == 0
+
+
 def test_veto_from_a_missing_partition_rolls_back():
     e = Env(n_gpus=2)
 

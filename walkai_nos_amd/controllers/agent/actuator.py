@@ -35,6 +35,8 @@ Fixes vs the reference: a deleted node (NotFound) is ignored instead of retried 
 """
 from __future__ import annotations
 
+import contextlib
+
 import json
 import logging
 import time
@@ -149,44 +151,50 @@ class Actuator:
         except Exception as e:  # noqa: BLE001 - no durable record, no flip
             REGISTRY.apply_errors.labels(node=self.node_name, op="journal").inc()
             return GpuError(f"unable to journal plan {plan_id!r} before applying it: {e}")
-        stopped = self.shared.helpers.quiesce()
-        if stopped:
-            log.info("stopped %d GPU helper process(es) before flipping", stopped)
-        if plan.memory_partition:
-            try:
-                self.pc.set_memory_partition(plan.memory_partition)
-                changed = True
-            except GpuError as e:
-                REGISTRY.apply_errors.labels(node=self.node_name, op="memory_partition").inc()
-                self._clear_journal()
-                return e
-            # the driver reload re-derived every GPU's compute mode; re-read before flipping
-            current = self.pc.current_profiles()
-            plan.changes = [c.__class__(c.gpu_index, current.get(c.gpu_index), c.to_profile)
-                            for c in plan.changes if current.get(c.gpu_index) != c.to_profile]
-        applied = []
-        for ch in plan.changes:
-            if self._gpu_busy(ch.gpu_index):
-                busy.append(ch.gpu_index)
-                REGISTRY.apply_errors.labels(node=self.node_name, op="gpu_busy").inc()
-                log.info("GPU %d has processes on its partitions: not flipping it to %s", ch.gpu_index, ch.to_profile)
-                continue
-            try:
-                self.pc.set_profile(ch.gpu_index, ch.to_profile)
-                flipped.append((ch.gpu_index, ch.from_profile))
-                applied.append(ch)
-                changed = True
-            except GpuError as e:
-                REGISTRY.apply_errors.labels(node=self.node_name, op="compute_partition").inc()
-                errors.append(f"GPU {ch.gpu_index} -> {ch.to_profile}: {e}")
-                break
+        helpers = self.shared.helpers
+        gate = helpers.held() if hasattr(helpers, "held") else contextlib.nullcontext()
+        with gate:  # no helper may start between the quiesce and the last switch
+            stopped = self.shared.helpers.quiesce()
+            if stopped:
+                log.info("stopped %d GPU helper process(es) before flipping", stopped)
+            if plan.memory_partition:
+                try:
+                    self.pc.set_memory_partition(plan.memory_partition)
+                    changed = True
+                except GpuError as e:
+                    REGISTRY.apply_errors.labels(node=self.node_name, op="memory_partition").inc()
+                    self._clear_journal()
+                    return e
+                # the driver reload re-derived every GPU's compute mode; re-read before flipping
+                current = self.pc.current_profiles()
+                plan.changes = [c.__class__(c.gpu_index, current.get(c.gpu_index), c.to_profile)
+                                for c in plan.changes if current.get(c.gpu_index) != c.to_profile]
+            applied = []
+            for ch in plan.changes:
+                if self._gpu_busy(ch.gpu_index):
+                    busy.append(ch.gpu_index)
+                    REGISTRY.apply_errors.labels(node=self.node_name, op="gpu_busy").inc()
+                    log.info("GPU %d has processes on its partitions: not flipping it to %s", ch.gpu_index, ch.to_profile)
+                    continue
+                try:
+                    self.pc.set_profile(ch.gpu_index, ch.to_profile)
+                    flipped.append((ch.gpu_index, ch.from_profile))
+                    applied.append(ch)
+                    changed = True
+                except GpuError as e:
+                    REGISTRY.apply_errors.labels(node=self.node_name, op="compute_partition").inc()
+                    errors.append(f"GPU {ch.gpu_index} -> {ch.to_profile}: {e}")
+                    break
         ok = not errors
         if ok and changed:
             ok = self._commit(applied)
             if not ok:
                 errors.append("commit barrier vetoed the plan")
         if not ok and flipped:
-            self._rollback(flipped)
+            gate = helpers.held() if hasattr(helpers, "held") else contextlib.nullcontext()
+            with gate:
+                helpers.quiesce()  # e.g. a barrier helper left behind by a timeout
+                self._rollback(flipped)
         if changed:
             self._reregister()
         self._clear_journal()

@@ -8,6 +8,7 @@ the old partitions would hold KFD contexts and make the flip fail with "busy".
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import logging
 import os
@@ -26,11 +27,35 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 class HelperRegistry:
-    """Live helper processes of one agent."""
+    """Live helper processes of one agent, and the gate that keeps new ones out during a flip."""
 
     def __init__(self) -> None:
         self._lock = threading.Lock()
+        self._cond = threading.Condition(self._lock)
+        self._held = 0
         self._procs: List[subprocess.Popen] = []
+
+    @contextlib.contextmanager
+    def held(self):
+        """No helper starts while held: a probe round that begins between :meth:`quiesce` and the
+        amd-smi switch would open KFD contexts on the partitions being destroyed."""
+        with self._cond:
+            self._held += 1
+        try:
+            yield self
+        finally:
+            with self._cond:
+                self._held -= 1
+                self._cond.notify_all()
+
+    def spawn(self, cmd: Sequence[str], timeout: float, **kw: Any) -> subprocess.Popen:
+        """Start and register a helper once the gate is open (atomically: quiesce never misses it)."""
+        with self._cond:
+            if not self._cond.wait_for(lambda: self._held == 0, timeout):
+                raise TimeoutError(f"gpu helper {list(cmd)[-1:]} held back for {timeout}s by a partition flip")
+            p = subprocess.Popen(list(cmd), **kw)
+            self._procs.append(p)
+            return p
 
     def add(self, p: subprocess.Popen) -> None:
         with self._lock:
@@ -69,9 +94,8 @@ def run_helper(args: Sequence[str], timeout: float = 180.0, registry: Optional[H
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     reg = registry or DEFAULT_REGISTRY
-    p = subprocess.Popen([sys.executable, "-m", "walkai_nos_amd.cmd.gpuhelper", *args], cwd=ROOT, env=env,
-                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    reg.add(p)
+    p = reg.spawn([sys.executable, "-m", "walkai_nos_amd.cmd.gpuhelper", *args], timeout, cwd=ROOT, env=env,
+                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
         out, err = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
