@@ -15,8 +15,9 @@
 // memory path PyTorch's expandable segments use: hipMemCreate charges the physical allocation,
 // hipMemRelease returns it (mapping it with hipMemMap allocates nothing more).
 //
-// Isolation is cooperative: nothing stops a process from unsetting LD_PRELOAD (documented in
-// docs/partitioning-modes.md, as the reference documents MPS's limits).
+// Isolation is cooperative: nothing stops a process from unsetting LD_PRELOAD, or from allocating
+// through entry points not listed above (texture arrays: hipMallocArray / hipArray3DCreate), as
+// docs/partitioning.md ("Caveats") says — the reference documents MPS's limits the same way.
 #include <dlfcn.h>
 
 #include <atomic>
