@@ -13,11 +13,13 @@ DETR-style MLP heads) built for the MI355X inference path:
 * the interpolated position embeddings are computed once per input resolution and cached (the
   upstream implementation re-interpolates on every forward);
 * the hot ops dispatch to hand-written HIP kernels (:mod:`walkai_nos_amd.ops.kernels`) on the GPU:
-  fused LayerNorm, fused bias+GELU, fused residual adds and an f32-MFMA flash attention; plain
-  GEMMs go to hipBLASLt through ``torch.nn.functional.linear``;
+  LayerNorm that emits x3 planes, x3 GEMMs with bias / exact GELU / residuals fused into the store
+  (the QKV projection leaves as fp32, which the x3 flash attention splits in-kernel), and the
+  stream-K x3 flash attention; the detection heads (100 tokens) stay on ``torch`` / hipBLASLt;
 * ``load_hf_state_dict`` maps a ``transformers`` ``YolosForObjectDetection`` state dict onto this
-  module, which is how numerical parity is tested (``tests/test_workload_yolos.py``) — there is
-  no network, so weights are random-init of the same architecture.
+  module, which is how numerical parity is tested
+  (``tests/test_infra.py::test_yolos_matches_transformers_reference``) — there is no network, so
+  weights are random-init of the same architecture.
 
 Config (hustvl/yolos-small): hidden 384, 12 layers, 6 heads, MLP 1536, patch 16, 100 detection
 tokens, pre-training image size 800x1333, 91 COCO labels (+1 "no object").  The demo's 640x480
