@@ -923,11 +923,13 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
                                                              int B, int T, int H, int h0, int Ht, float scale_log2e,
-                                                             int P) {
+                                                             int Pk) {
   static_assert(G == 4 || G == 8, "4 or 8 query tiles per workgroup");
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
-  const int w = sk_logical(blockIdx.x, P);
+  // bit 30 of the grid word: logical workgroup = physical (no XCD-major remap; A/B switch)
+  const int P = Pk & 0x3fffffff;
+  const int w = (Pk >> 30) ? int(blockIdx.x) : sk_logical(blockIdx.x, P);
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
   long long u = sk_begin(w, U, P);
@@ -1359,24 +1361,25 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   __bf16* op = reinterpret_cast<__bf16*>(outp);
   const float sl2 = scale * 1.4426950408889634f;
   const __bf16* q3 = reinterpret_cast<const __bf16*>(qkv3);
+  const int pk = waves | ((g_x3_flags & 4) ? (1 << 30) : 0);
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
                        sl2, waves);
   else if (G == 8 && f32in && (g_x3_flags & 2))
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op,
-                       part_o, part_ml, B, T, hn, h0, H, sl2, waves);
+                       part_o, part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8 && f32in)
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
-                       part_ml, B, T, hn, h0, H, sl2, waves);
+                       part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8 && (g_x3_flags & 1))
     hipLaunchKernelGGL((attn_fwd_x3p<8, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
-                       part_ml, B, T, hn, h0, H, sl2, waves);
+                       part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8)
     hipLaunchKernelGGL(attn_fwd_x3p<8>, dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
-                       T, hn, h0, H, sl2, waves);
+                       T, hn, h0, H, sl2, pk);
   else
     hipLaunchKernelGGL(attn_fwd_x3p<4>, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
-                       T, hn, h0, H, sl2, waves);
+                       T, hn, h0, H, sl2, pk);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (G == 8)
     hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(B * hn * QG * 8), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
