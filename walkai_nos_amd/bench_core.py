@@ -528,6 +528,9 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     import torch
     import torch.distributed as dist
 
+    if os.environ.get("NOS_X3_ABLATE", "0") != "0":
+        raise SystemExit("NOS_X3_ABLATE skips GEMM work (a timing-study switch): the bench refuses to run with it")
+
     from .parallel.barrier import LocalBarrier, RankCommitBarrier
 
     distributed = cfg.world > 1

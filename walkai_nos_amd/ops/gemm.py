@@ -243,7 +243,12 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         L.nos_gemm_x3_set_group.argtypes = [i32]
         L.nos_gemm_x3_set_ablate.argtypes = [i32]
-        L.nos_gemm_x3_set_ablate(int(os.environ.get("NOS_X3_ABLATE", "0")))  # timing studies only
+        ablate = int(os.environ.get("NOS_X3_ABLATE", "0"))  # timing studies only: results are invalid
+        if ablate:
+            import logging
+            logging.getLogger("nos.gemm").warning("NOS_X3_ABLATE=%d: x3 GEMM operand loads / stores skipped, "
+                                                  "results are INVALID (timing study)", ablate)
+        L.nos_gemm_x3_set_ablate(ablate)
         g = int(os.environ.get("NOS_X3_GROUP_M", str(X3_GROUP_M)))
         if L.nos_gemm_x3_set_group(g) != 0:
             raise RuntimeError(f"NOS_X3_GROUP_M={g}: {L.nos_gemm_x3_last_error().decode()}")
