@@ -674,7 +674,9 @@ def smoke_step() -> None:
     assert r.tflops > 0
     cfg = BenchConfig(gpus=1, steps=1, warmup=0, graphs=False)
     nb = NodeBench(cfg, barrier_factory=None, gpu_data_plane=False)
-    nb.control_step()
+    for _ in range(8):  # a few quanta of churn, so pods are scheduled and running
+        nb.control_step()
+        nb.end_step()
     from .models.workload.yolos import YolosSmall, demo_input
     m = YolosSmall().cuda().eval()
     with torch.no_grad():
