@@ -374,3 +374,31 @@ def test_attention_x3_fp32_input_equals_planes_input(K, T, H, B):
         assert torch.equal(a, b), (waves, hb)
         out = b[0].float() + b[1].float() + b[2].float()
         assert (out - ref).abs().max().item() < 2e-6
+
+
+def test_gemm_x3_split_k_reproducible_concurrent_and_counters_reset(K):
+    # split-K: the last-arriving split sums the partials in split order, so repeated launches are
+    # bit-identical; two streams (own workspaces) run concurrently; every launch re-zeroes counters
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(5)
+    M, N, Kd = 3401, 384, 1536
+    x3 = K.split3(torch.randn(M, Kd, device="cuda"))
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda")
+    ref = x3.double().sum(0) @ w.double().t() + b.double() + r.double()
+    cfgs = [c for c in G.x3_eligible(N, Kd) if c in G.X3_SPLIT]
+    assert cfgs
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    for cfg in cfgs:
+        outs = []
+        for s in (s1, s2, s1):
+            with torch.cuda.stream(s):
+                outs.append(G.gemm_x3(x3, w, b, residual=r, tile=cfg))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), cfg
+        assert (outs[0].double() - ref).abs().max().item() < 2e-4, cfg
+    for ws in G._split_ws.values():
+        if ws.ctr is not None:
+            assert int(ws.ctr.abs().sum().item()) == 0
