@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
     ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
+    ap.add_argument("--emulation", default=None, choices=("pinned", "spread"),
+                    help="compute-partition emulation on the SPX device (default: pinned; bench_core.EMULATION)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -61,6 +63,8 @@ def main() -> int:
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
                       preroll=args.preroll, quantum_s=args.quantum, flip_cost_s=args.flip_cost,
                       policy=args.policy, depth=args.depth, density=not args.no_density)
+    if args.emulation:
+        cfg.emulation = args.emulation
     res = run_bench(cfg)
     if rank == 0:
         line = json.dumps(res)

@@ -23,6 +23,8 @@
 #include <cstdint>
 #include <string>
 
+#include "pin.h"
+
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -35,23 +37,19 @@ constexpr int BK = 32, LSTR = 40;
 
 __device__ __forceinline__ int acc_row(int r, int hf) { return (r & 3) + 8 * (r >> 2) + 4 * hf; }
 
-// Logical tile of physical workgroup `phys` in a grid of n: workgroups are dealt round-robin over the
-// 8 XCDs (phys % 8 = XCD, observed placement — speed only, never correctness), so XCD x gets the
-// contiguous logical range starting at x*(n/8) + min(x, n%8): a band of whole tile rows whose A
-// rows stay in that XCD's L2 while it sweeps the weight columns. A bijection for every n.
-__device__ __forceinline__ int xcd_major(int phys, int n) {
-  const int x = phys % 8, q = n / 8, r = n % 8;
-  return x * q + min(x, r) + phys / 8;
-}
+// Logical tile order: xcd_major_n (pin.h) deals workgroups round-robin over the XCDs (phys % nx =
+// XCD, observed placement — speed only, never correctness), so XCD x gets a contiguous logical range:
+// a band of whole tile rows whose A rows stay in that XCD's L2 while it sweeps the weight columns.
 
 // Persistent grids: workgroup w's tiles are base + i*stride, i < count — the XCD's band again, dealt
-// over the XCD's P/8 workgroups (P % 8 == 0; otherwise a plain w + i*P sweep).
-__device__ __forceinline__ void xcd_band(int w, int P, int tiles, int& base, int& stride, int& count) {
-  if (P % 8) {
+// over the XCD's P/nx workgroups (nx XCDs: 8, or the pinned partition's; P % nx == 0, otherwise a
+// plain w + i*P sweep).
+__device__ __forceinline__ void xcd_band(int w, int P, int nx, int tiles, int& base, int& stride, int& count) {
+  if (P % nx) {
     base = w, stride = P, count = w < tiles ? (tiles - w + P - 1) / P : 0;
     return;
   }
-  const int x = w % 8, li = w / 8, px = P / 8, q = tiles / 8, r = tiles % 8;
+  const int x = w % nx, li = w / nx, px = P / nx, q = tiles / nx, r = tiles % nx;
   const int n = q + (x < r ? 1 : 0);
   base = x * q + min(x, r) + li, stride = px, count = li < n ? (n - li + px - 1) / px : 0;
 }
@@ -216,10 +214,12 @@ __global__ __launch_bounds__(256, 2) void gemm_x3(const __bf16* __restrict__ A, 
   __shared__ __attribute__((aligned(16))) __bf16 Bs[NBUF][3 * BN * LSTR];
 
   const int group = (epi >> 8) & 0xff;
+  const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
   epi &= 0xff;
+  if (pb.id < 0) return;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
-  const int t = xcd_major(blockIdx.x, gridDim.x);
+  const int t = xcd_major_n(pb.id, pb.n, pb.nx);
   if (t >= tiles) return;
   int mt, nt;
   tile_rc(t, tiles_m, tiles_n, group, mt, nt);
@@ -284,7 +284,7 @@ int launch(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* 
     return -1;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3<WM, WN, NBUF>), dim3(tiles), dim3(256), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
+  hipLaunchKernelGGL((gemm_x3<WM, WN, NBUF>), dim3(pinned_grid(tiles, unsigned(epi >> 20) & 0xffu)), dim3(256), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp,
                      cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -613,11 +613,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
       B3[S > 3 ? 3 * BN * BKS : 8];
 
   const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7;
+  const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
   epi &= 0xff;
+  if (pb.id < 0) return;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
   // logical unit = (tile, split), a tile's splits adjacent so they share an XCD (and its L2)
-  const int u = xcd_major(blockIdx.x, gridDim.x);
+  const int u = xcd_major_n(pb.id, pb.n, pb.nx);
   if (u >= tiles * splits) return;
   const int t = u / splits, sp = u - t * splits;
   int mt, nt;
@@ -733,7 +735,8 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     return -1;
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(tiles * splits), dim3(64 * WGM * WGN), 0, s, A,
+  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(pinned_grid(tiles * splits, unsigned(epi >> 20) & 0xffu)),
+                     dim3(64 * WGM * WGN), 0, s, A,
                      ap, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi, splits, ws, ctr);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -768,11 +771,13 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3s(const __bf16* __re
       B2[S > 2 ? 3 * BN * BKS : 8], B3[S > 3 ? 3 * BN * BKS : 8];
 
   const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7;
+  const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
   epi &= 0xff;
+  if (pb.id < 0) return;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
   int tb, ts, tcount;
-  xcd_band(blockIdx.x, gridDim.x, tiles, tb, ts, tcount);
+  xcd_band(pb.id, pb.n, pb.nx, tiles, tb, ts, tcount);
   if (tcount <= 0) return;
   const int nk = K / BKS;
   const int total = tcount * nk;  // this workgroup's stages
@@ -863,7 +868,8 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
   }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
   const int g = std::max(1, std::min(grid, tiles));
-  hipLaunchKernelGGL((gemm_x3s<BM, BN, WGM, WGN, S, BKS>), dim3(g), dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2,
+  hipLaunchKernelGGL((gemm_x3s<BM, BN, WGM, WGN, S, BKS>), dim3(pinned_grid(g, unsigned(epi >> 20) & 0xffu)),
+                     dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2,
                      r2_rows, C, Cp, cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -990,7 +996,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  epi |= (g_group_m << 8) | (g_ablate << 16);
+  epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
   switch (cfg) {
     case 0: return launch_s<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 1: return launch_s<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
@@ -1039,7 +1045,7 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
   const __bf16* w = reinterpret_cast<const __bf16*>(W);
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  epi |= (g_group_m << 8) | (g_ablate << 16);
+  epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
   return dispatch(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, cfg, s, 1, nullptr, nullptr);
 }
 
@@ -1062,7 +1068,7 @@ int nos_gemm_x3_split(const void* A, size_t ap, const void* W, size_t wp, const 
     g_err = "gemm_x3: split-K needs an LDS-DMA 32x32-MFMA tile (config 7..26, 32..34)";
     return -1;
   }
-  epi |= (g_group_m << 8) | (g_ablate << 16);
+  epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
   return dispatch(reinterpret_cast<const __bf16*>(A), ap, reinterpret_cast<const __bf16*>(W), wp, bias, R, R2,
                   r2_rows, C, reinterpret_cast<__bf16*>(Cp), cp, M, N, K, epi, cfg,
                   reinterpret_cast<hipStream_t>(stream), splits, reinterpret_cast<float*>(ws),

@@ -20,6 +20,8 @@
 //  * bias_gelu_f32: in-place exact (erf) GELU(y + b) epilogue, dwordx4 vectorised.
 #include <hip/hip_runtime.h>
 
+#include "pin.h"
+
 #include <cmath>
 #include <cstdint>
 #include <string>
@@ -77,15 +79,17 @@ __device__ __forceinline__ void store_x3(__bf16* __restrict__ y, size_t plane, s
 template <int NPL>
 __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, float* __restrict__ y,
-                                                     __bf16* __restrict__ yp, int rows, float eps) {
+                                                     __bf16* __restrict__ yp, int rows, float eps, unsigned pin) {
   static_assert(NPL % 2 == 0, "hidden size must be a multiple of 128");
+  const PinnedBlock pb = pinned_block(pin);
+  if (pb.id < 0) return;
   constexpr int D = NPL * 64, NP = NPL / 2;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float2* w2 = reinterpret_cast<const float2*>(w);
   const float2* b2 = reinterpret_cast<const float2*>(b);
   // grid-stride over rows: a slice sharing the GPU launches a few workgroups per CU instead of one
   // per 4 rows (workgroup dispatch is what concurrent partitions contend for)
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  for (int row = pb.id * 4 + wave; row < rows; row += pb.n * 4) {
   const float2* xr = reinterpret_cast<const float2*>(x + size_t(row) * D);
   float2 v[NP];
   float s = 0.f;
@@ -579,19 +583,23 @@ template <int G>
 __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict__ part_o,
                                                          const float* __restrict__ part_ml, float* __restrict__ out,
                                                          int B, int T, int H, int P, __bf16* __restrict__ outp,
-                                                         int h0, int Ht) {
+                                                         int h0, int Ht, unsigned pin) {
   __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
-  const int wv = blockIdx.x % G;
-  const long long grp = blockIdx.x / G;
+  const PinnedBlock pb = pinned_block(pin);
+  if (pb.id < 0) return;
+  // grid-stride over the (group, query tile) units: a pinned launch runs a few workgroups per CU
+  for (int id = pb.id; id < B * H * QG * G; id += pb.n) {
+  const int wv = id % G;
+  const long long grp = id / G;
   const int qg = int(grp % QG);
   const int qt = qg * G + wv;
-  if (qt >= QT) return;
+  if (qt >= QT) continue;
   const long long t0 = grp * NK, t1 = t0 + NK;
   const long long w_lo = ((t0 + 1) * P + U - 1) / U - 1;
   const long long w_hi = (t1 * P + U - 1) / U - 1;
-  if (w_lo == w_hi) return;
+  if (w_lo == w_hi) continue;
   const int head = h0 + int((grp / QG) % H);
   const int b = int(grp / ((long long)QG * H));
   const int D = Ht * HD;
@@ -653,6 +661,8 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
     else
       out[i] = s_tile[d][jq];
   }
+  __syncthreads();  // s_tile is rewritten by the next unit
+  }
 }
 
 // ---- fp32 as three bf16 planes ("x3") ----------------------------------------------------------
@@ -697,9 +707,12 @@ __device__ __forceinline__ f32x16 mfma_x3(const bf16x8& a0, const bf16x8& a1, co
 }
 
 // fp32 [n] -> bf16 planes [3][n] (plane stride n); 4 elements per thread
-__global__ __launch_bounds__(256) void split3_f32(const float* __restrict__ x, __bf16* __restrict__ y, size_t n4) {
-  const size_t stride = size_t(gridDim.x) * 256;
-  for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < n4; i += stride) {
+__global__ __launch_bounds__(256) void split3_f32(const float* __restrict__ x, __bf16* __restrict__ y, size_t n4,
+                                                  unsigned pin) {
+  const PinnedBlock pb = pinned_block(pin);
+  if (pb.id < 0) return;
+  const size_t stride = size_t(pb.n) * 256;
+  for (size_t i = size_t(pb.id) * 256 + threadIdx.x; i < n4; i += stride) {
     const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
     bf16x4 p0, p1, p2;
     split3(v, p0, p1, p2);
@@ -927,9 +940,12 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
   static_assert(G == 4 || G == 8, "4 or 8 query tiles per workgroup");
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
-  // bit 30 of the grid word: logical workgroup = physical (no XCD-major remap; A/B switch)
-  const int P = Pk & 0x3fffffff;
-  const int w = (Pk >> 30) ? int(blockIdx.x) : sk_logical(blockIdx.x, P);
+  // grid word: bits 0-21 = P (logical workgroups), 22-29 = partition pin (pin.h), bit 30 = logical
+  // workgroup order = dispatch order (no XCD-major remap; A/B switch)
+  const int P = Pk & 0x3fffff;
+  const PinnedBlock pb = pinned_block(unsigned(Pk >> 22) & 0xffu);
+  if (pb.id < 0 || pb.id >= P) return;
+  const int w = (Pk >> 30) ? pb.id : xcd_major_n(pb.id, P, pb.nx);
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
   long long u = sk_begin(w, U, P);
@@ -1260,7 +1276,39 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
 
 }  // namespace
 
+// ------------------------------------------------------------------------------------------
+// Pinning census (tests/test_gpu_pin.py): every logical block of a pinned launch counts itself and
+// records the XCD it ran on.
+__global__ __launch_bounds__(64) void pin_census(int* __restrict__ counts, int* __restrict__ xcc, int n,
+                                                 unsigned pin) {
+  const PinnedBlock pb = pinned_block(pin);
+  if (pb.id < 0 || pb.id >= n || threadIdx.x) return;
+  atomicAdd(&counts[pb.id], 1);
+  xcc[pb.id] = xcc_id();
+}
+
 extern "C" {
+
+static thread_local unsigned g_pin = 0;  // per enqueuing thread, like the Python slice state
+
+// XCD mask of the partition whose launches are being enqueued (0 = unpinned; pin.h). Set per slice
+// before its work is enqueued or captured, like its CU count: a captured graph keeps the pin.
+int nos_set_pin(unsigned mask) {
+  if (mask > 0xffu) {
+    g_err = "pin: XCD mask must fit 8 bits";
+    return -1;
+  }
+  g_pin = mask;
+  return 0;
+}
+
+unsigned nos_pin_mask() { return g_pin; }
+
+int nos_pin_census(int* counts, int* xcc, int n, unsigned pin, void* stream) {
+  hipLaunchKernelGGL(pin_census, dim3(pinned_grid(n, pin)), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), counts,
+                     xcc, n, pin);
+  return check_launch("pin_census");
+}
 
 const char* nos_kernels_last_error() { return g_err.c_str(); }
 
@@ -1272,8 +1320,8 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
   }
   const size_t n4 = n / 4;
   const int grid = int(std::min<size_t>((n4 + 255) / 256, 4096));
-  hipLaunchKernelGGL(split3_f32, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x,
-                     reinterpret_cast<__bf16*>(planes), n4);
+  hipLaunchKernelGGL(split3_f32, dim3(pinned_grid(pinned_cap(grid, g_pin), g_pin)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     x, reinterpret_cast<__bf16*>(planes), n4, g_pin);
   return check_launch("split3_f32");
 }
 
@@ -1361,32 +1409,44 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   __bf16* op = reinterpret_cast<__bf16*>(outp);
   const float sl2 = scale * 1.4426950408889634f;
   const __bf16* q3 = reinterpret_cast<const __bf16*>(qkv3);
-  const int pk = waves | ((g_x3_flags & 4) ? (1 << 30) : 0);
+  if (waves >= (1 << 22)) {
+    g_err = "attention x3: at most 2^22 workgroups";
+    return -1;
+  }
+  if (g_pin && !g_x3_pipelined) {
+    g_err = "attention x3: pinned launches need the pipelined kernel";
+    return -1;
+  }
+  const unsigned pin = g_pin;
+  const int pk = waves | int(pin << 22) | ((g_x3_flags & 4) ? (1 << 30) : 0);
+  const dim3 grid(pinned_grid(waves, pin));
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
                        sl2, waves);
   else if (G == 8 && f32in && (g_x3_flags & 2))
-    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op,
+    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op,
                        part_o, part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8 && f32in)
-    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
+    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op, part_o,
                        part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8 && (g_x3_flags & 1))
-    hipLaunchKernelGGL((attn_fwd_x3p<8, true>), dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o,
+    hipLaunchKernelGGL((attn_fwd_x3p<8, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op, part_o,
                        part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8)
-    hipLaunchKernelGGL(attn_fwd_x3p<8>, dim3(waves), dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
+    hipLaunchKernelGGL(attn_fwd_x3p<8>, grid, dim3(512), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
                        T, hn, h0, H, sl2, pk);
   else
-    hipLaunchKernelGGL(attn_fwd_x3p<4>, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
+    hipLaunchKernelGGL(attn_fwd_x3p<4>, grid, dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
                        T, hn, h0, H, sl2, pk);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (G == 8)
-    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(B * hn * QG * 8), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
-                       waves, op, h0, H);
+    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(B * hn * QG * 8, pin)), dim3(256), 0, s,
+                       part_o, part_ml,
+                       out, B, T, hn, waves, op, h0, H, pin);
   else
-    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * hn * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, hn,
-                       waves, op, h0, H);
+    hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(pinned_grid(B * hn * QG * 4, pin)), dim3(256), 0, s,
+                       part_o, part_ml,
+                       out, B, T, hn, waves, op, h0, H, pin);
   return check_launch("attn_sk_lds_fixup");
 }
 
@@ -1417,14 +1477,15 @@ int nos_layernorm_f32_grid(const float* x, const float* w, const float* b, float
   if (rows <= 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int full = (rows + 3) / 4;
-  const dim3 grid(wgs > 0 ? std::min(wgs, full) : full), block(256);
+  const dim3 grid(pinned_grid(pinned_cap(wgs > 0 ? std::min(wgs, full) : full, g_pin), g_pin)), block(256);
   __bf16* p = reinterpret_cast<__bf16*>(yp);
+  const unsigned pin = g_pin;
   switch (D) {
-    case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
-    case 768: hipLaunchKernelGGL(layernorm_f32<12>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
-    case 1024: hipLaunchKernelGGL(layernorm_f32<16>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
-    case 1536: hipLaunchKernelGGL(layernorm_f32<24>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
-    case 2048: hipLaunchKernelGGL(layernorm_f32<32>, grid, block, 0, s, x, w, b, y, p, rows, eps); break;
+    case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
+    case 768: hipLaunchKernelGGL(layernorm_f32<12>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
+    case 1024: hipLaunchKernelGGL(layernorm_f32<16>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
+    case 1536: hipLaunchKernelGGL(layernorm_f32<24>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
+    case 2048: hipLaunchKernelGGL(layernorm_f32<32>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
     default:
       g_err = "layernorm: unsupported hidden size " + std::to_string(D);
       return -1;
@@ -1502,7 +1563,7 @@ int nos_attention_f32_sk(const float* qkv, float* out, float* ws, int B, int T, 
                        scale_log2e, waves);
     if (int rc = check_launch("attn_fwd_sk_lds")) return rc;
     hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(B * H * QG * 4), dim3(256), 0, s, part_o, part_ml, out, B, T, H, waves,
-                       static_cast<__bf16*>(nullptr), 0, H);
+                       static_cast<__bf16*>(nullptr), 0, H, 0u);
     return check_launch("attn_sk_lds_fixup");
   }
   float* part_o = ws;

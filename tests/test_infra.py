@@ -143,12 +143,21 @@ def test_yolos_matches_transformers_reference():
 
 
 def test_bench_control_plane_and_slice_masks():
-    from walkai_nos_amd.bench_core import BenchConfig, ChurnProcess, NodeBench, slice_cus
-    assert slice_cus("spx_nps1", 0) is None
-    assert slice_cus("cpx_nps1", 3) == list(range(96, 128))
-    assert len(slice_cus("dpx_nps1", 1)) == 128
-    # every CPX slice covers all 8 XCDs (bit i -> XCD i mod 8)
-    assert {c % 8 for c in slice_cus("cpx_nps1", 5)} == set(range(8))
+    from walkai_nos_amd.bench_core import BenchConfig, ChurnProcess, NodeBench, slice_cus, slice_pin
+    assert slice_cus("spx_nps1", 0) is None and slice_pin("spx_nps1", 0) == 0
+    # spread emulation: every CPX slice covers all 8 XCDs (bit i -> XCD i mod 8)
+    assert slice_cus("cpx_nps1", 3, emulation="spread") == list(range(96, 128))
+    assert len(slice_cus("dpx_nps1", 1, emulation="spread")) == 128
+    assert {c % 8 for c in slice_cus("cpx_nps1", 5, emulation="spread")} == set(range(8))
+    assert slice_pin("cpx_nps1", 5, "spread") == 0
+    # pinned emulation: partition k of CPX / QPX / DPX owns XCD k / 2k..2k+1 / 4k..4k+3 and all their CUs
+    assert {c % 8 for c in slice_cus("cpx_nps1", 5, emulation="pinned")} == {5}
+    assert len(slice_cus("cpx_nps1", 5, emulation="pinned")) == 32
+    assert slice_pin("cpx_nps1", 5, "pinned") == 1 << 5
+    assert slice_pin("qpx_nps1", 1, "pinned") == 0b1100 and len(slice_cus("qpx_nps1", 1, emulation="pinned")) == 64
+    assert slice_pin("dpx_nps1", 1, "pinned") == 0xF0 and len(slice_cus("dpx_nps1", 1, emulation="pinned")) == 128
+    masks = [slice_pin("cpx_nps1", k, "pinned") for k in range(8)]
+    assert sum(masks) == 0xFF and len(set(masks)) == 8
     a, b = ChurnProcess(BenchConfig(seed=7)), ChurnProcess(BenchConfig(seed=7))
     assert [a.arrivals() for _ in range(20)] == [b.arrivals() for _ in range(20)]
     nb = NodeBench(BenchConfig(gpus=2, flip_cost_s=1.0, quantum_s=0.5), gpu_data_plane=False)

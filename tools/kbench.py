@@ -56,6 +56,8 @@ def main() -> int:
     ap.add_argument("--only", choices=("all", "attn", "gemm", "model", "modes"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
+    ap.add_argument("--emulation", default="pinned", choices=("pinned", "spread"),
+                    help="modes: compute-partition emulation (bench_core.EMULATION)")
     a = ap.parse_args()
     torch.manual_seed(0)
     if a.only == "modes":
@@ -137,7 +139,7 @@ def modes_bench(a) -> int:
     """Whole-GPU throughput of each partition mode as the flagship bench runs it: every partition
     of the mode busy at once (its own CU-masked stream and graph-captured model replica), each
     running 8 x fraction inferences per round; inferences/s per GPU."""
-    from walkai_nos_amd.bench_core import BenchConfig, Slot
+    from walkai_nos_amd.bench_core import BenchConfig, Slot, slice_pin
     from walkai_nos_amd.models.workload.yolos import YolosSmall
     cfg = BenchConfig()
     template = YolosSmall()
@@ -146,7 +148,8 @@ def modes_bench(a) -> int:
         if prof.split("_")[0] not in a.slices.split(","):
             continue
         n = min(n, a.partitions) if a.partitions else n
-        slots = [Slot(slice_cus(prof, k), 0, cfg, template, seed=k) for k in range(n)]
+        slots = [Slot(slice_cus(prof, k, emulation=a.emulation), 0, cfg, template, seed=k,
+                      pin=slice_pin(prof, k, a.emulation)) for k in range(n)]
         for sl in slots:
             sl.warm()
         torch.cuda.synchronize()
@@ -164,7 +167,7 @@ def modes_bench(a) -> int:
                 sl.drain()
         dt = time.perf_counter() - t0
         busy = sampler.stop()
-        r = {"mode": prof, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
+        r = {"mode": prof, "emulation": a.emulation, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
              "ms_per_round": round(1000 * dt / rounds, 2), "hw_busy_pct": busy, **sampler.power_summary()}
         print(json.dumps(r), flush=True)
         results.append(r)

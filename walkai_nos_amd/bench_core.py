@@ -23,8 +23,11 @@ One step = one **serving quantum** of ``quantum_s`` wall seconds:
 Because the box is not root, compute-partition modes cannot be flipped on the real device; a
 CPX/QPX/DPX partition is emulated by an XCD-symmetric CU mask of the same CU count (32/64/128
 CUs; mask bit i -> XCD i mod 8, and an XCD whose mask bits are all zero is NOT disabled, so every
-slice must span all eight XCDs).  Mode changes go through the fake amd-smi backend (whose device
-map re-enumerates like the real one); everything else — kernels, streams, collectives — is real.
+slice must span all eight XCDs). An XCD-pinned emulation (``--emulation pinned``, ``csrc/pin.h``)
+gives each partition its own XCDs like real hardware, but its exit-only workgroups on the other
+XCDs couple the partitions (see EMULATION). Mode changes go through the fake amd-smi backend
+(whose device map re-enumerates like the real one); everything else — kernels, streams,
+collectives — is real.
 
 After the timed window a **density** phase saturates the node through the same control plane and
 data plane: 8 CPX pods per GPU (the reference's MIG maximum is 7 per A100), then a CU-mask node
@@ -56,6 +59,19 @@ MIX = (("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2))
 CUMASK_DENSITY = {"cumask": (("32cu.24gb", 6), ("8gb", 10)), "cumask_shared": (("16gb", 16),)}
 
 
+#: How a compute partition is emulated on the SPX device (the box is not root, so modes cannot be
+#: flipped): "spread" — an XCD-symmetric CU mask of the partition's CU count over all eight XCDs;
+#: "pinned" — the partition's kernels run only on its own XCDs (CPX partition k = XCD k, QPX k = XCDs
+#: 2k..2k+1, DPX k = XCDs 4k..4k+3; ``csrc/pin.h``), the layout a real partition has. Pinned is
+#: correct (tests/test_gpu_pin.py) but cannot stand in for real partitions: every pinned launch also
+#: dispatches exit-only workgroups to the other XCDs, which need a free slot there, so a partition's
+#: kernel waits on its neighbours' workgroups — 8 busy CPX partitions run at 253 inf/s pinned vs 375
+#: spread, while one partition alone runs 16.1 vs 14.8 ms per inference
+#: (profiles/partition_emulation_r2.json). ``NOS_PARTITION_EMULATION`` overrides.
+EMULATION = os.environ.get("NOS_PARTITION_EMULATION", "spread")
+XCDS = 8
+
+
 @dataclass
 class BenchConfig:
     gpus: int = 1
@@ -75,6 +91,7 @@ class BenchConfig:
     world: int = 1
     policy: str = "pack"                 # planner policy (pack | fifo | batch | simulate)
     density: bool = True
+    emulation: str = EMULATION           # compute-partition emulation: pinned | spread
 
     @property
     def outage_steps(self) -> int:
@@ -116,12 +133,36 @@ class ChurnProcess:
         return self.rng.randint(*self.cfg.lifetime)
 
 
-def slice_cus(profile: str, partition: int, total_cus: int = 256) -> Optional[List[int]]:
-    """XCD-symmetric CU set emulating compute partition ``partition`` of ``profile``: a contiguous
-    run of mask bits (bit i -> XCD i mod 8), i.e. total/partitions CUs spread evenly over all XCDs."""
+
+
+def partition_xcds(profile: str, partition: int) -> Optional[List[int]]:
+    """The XCDs of compute partition ``partition`` of ``profile`` (None = the whole GPU)."""
     n = COMPUTE_MODES[profile.split("_")[0]]
     if n == 1:
         return None
+    per = XCDS // n
+    return list(range(partition * per, (partition + 1) * per))
+
+
+def slice_pin(profile: str, partition: int, emulation: Optional[str] = None) -> int:
+    """XCD mask the partition's kernels are pinned to (0 = unpinned: SPX, or the spread emulation)."""
+    xcds = partition_xcds(profile, partition)
+    if xcds is None or (emulation or EMULATION) != "pinned":
+        return 0
+    return sum(1 << x for x in xcds)
+
+
+def slice_cus(profile: str, partition: int, total_cus: int = 256,
+              emulation: Optional[str] = None) -> Optional[List[int]]:
+    """CU-mask bits (bit i -> XCD i mod 8) of compute partition ``partition`` of ``profile``.
+    pinned: every CU of the partition's XCDs; spread: a contiguous run of total/partitions bits, i.e.
+    that many CUs spread evenly over all XCDs."""
+    n = COMPUTE_MODES[profile.split("_")[0]]
+    if n == 1:
+        return None
+    if (emulation or EMULATION) == "pinned":
+        xcds = set(partition_xcds(profile, partition))
+        return [i for i in range(total_cus) if i % XCDS in xcds]
     per = total_cus // n
     return list(range(partition * per, (partition + 1) * per))
 
@@ -130,7 +171,8 @@ class Slot:
     """One partition (or CU-mask slice) of this rank's GPU: a CU-masked stream, a model replica
     and an input; an inference is one HIP graph replay."""
 
-    def __init__(self, cus: Optional[List[int]], device: int, cfg: BenchConfig, template: Any, seed: int = 0):
+    def __init__(self, cus: Optional[List[int]], device: int, cfg: BenchConfig, template: Any, seed: int = 0,
+                 pin: int = 0):
         import copy
 
         import torch
@@ -138,6 +180,7 @@ class Slot:
         from .ops.probe import Stream
 
         self.cus = cus
+        self.pin = pin
         self.hip_stream = Stream(device, cus)
         self.stream = self.hip_stream.torch_stream()
         with torch.cuda.stream(self.stream):
@@ -157,6 +200,7 @@ class Slot:
 
         from .ops import kernels as K
         K.set_slice_cus(self.n_cus)
+        K.set_slice_pin(self.pin)
         with torch.no_grad(), torch.cuda.stream(self.stream):
             for _ in range(2):
                 self.out = self.model(self.x)
@@ -175,6 +219,7 @@ class Slot:
 
         from .ops import kernels as K
         K.set_slice_cus(self.n_cus)
+        K.set_slice_pin(self.pin)
         with torch.no_grad(), torch.cuda.stream(self.stream):
             if self.graph is not None:
                 self.graph.replay()
@@ -220,7 +265,8 @@ class DataPlane:
         self.slots: Dict[Any, Slot] = {}
         for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
             for k in range(n):
-                self.slots[(prof, k)] = Slot(slice_cus(prof, k), self.device, cfg, self.template, seed=k)
+                self.slots[(prof, k)] = Slot(slice_cus(prof, k, emulation=cfg.emulation), self.device, cfg,
+                                             self.template, seed=k, pin=slice_pin(prof, k, cfg.emulation))
         for s in self.slots.values():
             s.warm()
         torch.cuda.synchronize()
@@ -628,6 +674,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
                    "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
                    "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
+                   "partition_emulation": cfg.emulation,
                    "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
 

@@ -222,6 +222,8 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
             104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
             108: (128, 64, 4, "p"), 109: (64, 128, 4, "p")}
+#: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
+X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
 #: split-K configs (csrc/gemm_x3.hip split_reduce): id -> (LDS-DMA base tile, K splits). Each tile's
 #: K range is spread over `splits` workgroups and the last to finish reduces the fp32 partials in
 #: split order (bit-reproducible) and runs the epilogue: the N = 384 GEMMs have 81-162 tiles at
@@ -238,7 +240,7 @@ X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 1
                    100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1}
 for _id, (_base, _sp) in X3_SPLIT.items():
     X3_SLOTS_PER_CU[_id] = X3_SLOTS_PER_CU[_base]
-_x3_cache: Dict[Tuple[int, int, int, int, int, int], int] = {}
+_x3_cache: Dict[Tuple[int, int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
 
@@ -458,11 +460,11 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
     epi = (EPI_BIAS if bias is not None else 0) | (EPI_GELU if gelu else 0) | (EPI_RES if residual is not None else 0) \
         | (EPI_RES2 if residual2 is not None else 0)
     if tile is None:
-        cus = K.slice_cus()
-        key = (M, N, Kd, epi, int(out_f32) | 2 * int(out_x3), cus)
+        cus, pin = K.slice_cus(), K.slice_pin()
+        key = (M, N, Kd, epi, int(out_f32) | 2 * int(out_x3), cus, pin)
         with _lock:
             tile = _x3_cache.get(key)
-        if tile is None:
+        if tile is None and not pin:  # the contention table was measured on spread (unpinned) slices
             tile = tuned_table().get(f"M{M}_N{N}_K{Kd}_epi{epi}_out{key[4]}_cus{cus}")
             if tile is not None and N % X3_TILES[tile][1] == 0:
                 with _lock:
@@ -473,7 +475,12 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
             cands = x3_eligible(N, Kd)
             if not cands:
                 raise ValueError(f"gemm_x3: unsupported shape N={N} K={Kd}")
-            cands = shared_slice_tiles(cands, cus)
+            if not pin:  # a pinned partition owns its XCDs' L2s: tiles are timed as it runs them
+                cands = shared_slice_tiles(cands, cus)
+            else:
+                # pinned launches dispatch 8 / popcount(pin) physical workgroups per logical one (the
+                # others exit at once, pin.h): only the persistent kernels keep that to one round
+                cands = [c for c in cands if c in X3_PERSISTENT] or cands
             if torch.cuda.is_current_stream_capturing():
                 tile = x3_heuristic(M, N, cus, cands)
             else:

@@ -50,6 +50,22 @@ def slice_cus() -> int:
     return getattr(_slice, "cus", None) or total_cus()
 
 
+def set_slice_pin(mask: int) -> None:
+    """Pin the current thread's launches to the XCDs in ``mask`` (bit x = XCD x; 0 = unpinned): the
+    emulation of a compute partition on an SPX device (``csrc/pin.h``). The pin is thread-local on
+    both sides, like the slice's CU count, and a captured HIP graph keeps the pin it was captured with."""
+    mask = int(mask or 0)
+    if not 0 <= mask <= 0xFF:
+        raise ValueError("pin: XCD mask must fit 8 bits")
+    _slice.pin = mask
+    if hip_available():
+        _check(_L().nos_set_pin(mask))
+
+
+def slice_pin() -> int:
+    return getattr(_slice, "pin", 0)
+
+
 def total_cus() -> int:
     """CUs of the whole device (256 on MI355X; the device query when a GPU is visible)."""
     global _total_cus
@@ -284,6 +300,8 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_ws_bytes.argtypes = [i32]
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
+            L.nos_set_pin.argtypes = [ctypes.c_uint]
+            L.nos_pin_mask.restype = ctypes.c_uint
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
             L.nos_attention_x3_set_group.argtypes = [i32]
