@@ -34,7 +34,9 @@ def main() -> int:
     ap.add_argument("--flip-cost", type=float, default=2.0,
                     help="seconds a GPU serves nothing after a compute-partition flip")
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
-    ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod")
+    ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod stream")
+    ap.add_argument("--pod-streams", type=int, default=1,
+                    help="concurrent request streams per pod (1 = one inference at a time, as the reference demo)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--emulation", default=None, choices=("pinned", "spread"),
                     help="compute-partition emulation on the SPX device (default: pinned; bench_core.EMULATION)")
@@ -62,7 +64,8 @@ def main() -> int:
     cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
                       preroll=args.preroll, quantum_s=args.quantum, flip_cost_s=args.flip_cost,
-                      policy=args.policy, depth=args.depth, density=not args.no_density)
+                      policy=args.policy, depth=args.depth, density=not args.no_density,
+                      pod_streams=args.pod_streams)
     if args.emulation:
         cfg.emulation = args.emulation
     res = run_bench(cfg)

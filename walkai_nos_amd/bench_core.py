@@ -85,7 +85,8 @@ class BenchConfig:
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"
     graphs: bool = True
-    depth: int = 2                       # inferences in flight per pod
+    depth: int = 2                       # inferences in flight per pod stream
+    pod_streams: int = 1                 # concurrent request streams per pod (1 = the reference demo's loop)
     preroll: int = 60                    # control-plane-only steps before warmup (steady state)
     rank: int = 0
     world: int = 1
@@ -167,9 +168,37 @@ def slice_cus(profile: str, partition: int, total_cus: int = 256,
     return list(range(partition * per, (partition + 1) * per))
 
 
+class _Lane:
+    """One stream of a pod: a CU-masked HIP stream, an input, and the inference graph captured on it."""
+
+    def __init__(self, cus: Optional[List[int]], device: int, cfg: "BenchConfig", seed: int):
+        import torch
+
+        from .models.workload.yolos import demo_input
+        from .ops.probe import Stream
+        self.hip_stream = Stream(device, cus)
+        self.stream = self.hip_stream.torch_stream()
+        with torch.cuda.stream(self.stream):
+            self.x = demo_input(1, cfg.hw, f"cuda:{device}", seed=seed)
+        self.graph = None
+        self.out = None
+        self.inflight: collections.deque = collections.deque()
+
+    def close(self) -> None:
+        self.inflight.clear()
+        self.graph = None
+        self.x = None
+        self.out = None
+        self.stream = None
+        if self.hip_stream is not None:
+            self.hip_stream.close()
+            self.hip_stream = None
+
+
 class Slot:
-    """One partition (or CU-mask slice) of this rank's GPU: a CU-masked stream, a model replica
-    and an input; an inference is one HIP graph replay."""
+    """One partition (or CU-mask slice) of this rank's GPU: a model replica serving
+    ``cfg.pod_streams`` concurrent request streams (lanes), each a CU-masked stream with its own
+    input and captured graph; an inference is one HIP graph replay on the least-loaded lane."""
 
     def __init__(self, cus: Optional[List[int]], device: int, cfg: BenchConfig, template: Any, seed: int = 0,
                  pin: int = 0):
@@ -177,23 +206,30 @@ class Slot:
 
         import torch
 
-        from .ops.probe import Stream
-
         self.cus = cus
         self.pin = pin
-        self.hip_stream = Stream(device, cus)
-        self.stream = self.hip_stream.torch_stream()
-        with torch.cuda.stream(self.stream):
-            self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
-            from .models.workload.yolos import demo_input
-            self.x = demo_input(1, cfg.hw, f"cuda:{device}", seed=seed)
-        self.graph = None
         self.cfg = cfg
-        self.inflight: collections.deque = collections.deque()
+        self.lanes = [_Lane(cus, device, cfg, seed + 1000 * i) for i in range(max(1, cfg.pod_streams))]
+        with torch.cuda.stream(self.lanes[0].stream):
+            self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
+        torch.cuda.synchronize()
 
     @property
     def n_cus(self) -> int:
         return 256 if self.cus is None else len(self.cus)
+
+    @property
+    def stream(self):
+        return self.lanes[0].stream if self.lanes else None
+
+    @property
+    def in_flight(self) -> int:
+        return sum(len(l.inflight) for l in self.lanes)
+
+    @property
+    def capacity(self) -> int:
+        """Inferences this pod keeps in flight: ``depth`` per lane."""
+        return self.cfg.depth * len(self.lanes)
 
     def warm(self) -> None:
         import torch
@@ -201,52 +237,51 @@ class Slot:
         from .ops import kernels as K
         K.set_slice_cus(self.n_cus)
         K.set_slice_pin(self.pin)
-        with torch.no_grad(), torch.cuda.stream(self.stream):
-            for _ in range(2):
-                self.out = self.model(self.x)
-        self.stream.synchronize()
-        if self.cfg.graphs:
-            g = torch.cuda.CUDAGraph()
-            with torch.no_grad():
-                with torch.cuda.graph(g, stream=self.stream):
-                    self.out = self.model(self.x)
-            self.stream.synchronize()
-            self.graph = g
+        for lane in self.lanes:
+            with torch.no_grad(), torch.cuda.stream(lane.stream):
+                for _ in range(2):
+                    lane.out = self.model(lane.x)
+            lane.stream.synchronize()
+            if self.cfg.graphs:
+                g = torch.cuda.CUDAGraph()
+                with torch.no_grad():
+                    with torch.cuda.graph(g, stream=lane.stream):
+                        lane.out = self.model(lane.x)
+                lane.stream.synchronize()
+                lane.graph = g
 
     def submit(self) -> None:
-        """Enqueue one inference and an event marking its end."""
+        """Enqueue one inference on the lane with the fewest in flight, and an event marking its end."""
         import torch
 
         from .ops import kernels as K
         K.set_slice_cus(self.n_cus)
         K.set_slice_pin(self.pin)
-        with torch.no_grad(), torch.cuda.stream(self.stream):
-            if self.graph is not None:
-                self.graph.replay()
+        lane = min(self.lanes, key=lambda l: len(l.inflight))
+        with torch.no_grad(), torch.cuda.stream(lane.stream):
+            if lane.graph is not None:
+                lane.graph.replay()
             else:
-                self.out = self.model(self.x)
+                lane.out = self.model(lane.x)
             ev = torch.cuda.Event()
-            ev.record(self.stream)
-        self.inflight.append(ev)
+            ev.record(lane.stream)
+        lane.inflight.append(ev)
 
     def reap(self) -> None:
-        while self.inflight and self.inflight[0].query():
-            self.inflight.popleft()
+        for lane in self.lanes:
+            while lane.inflight and lane.inflight[0].query():
+                lane.inflight.popleft()
 
     def drain(self) -> None:
-        while self.inflight:
-            self.inflight.popleft().synchronize()
+        for lane in self.lanes:
+            while lane.inflight:
+                lane.inflight.popleft().synchronize()
 
     def close(self) -> None:
-        self.inflight.clear()
-        self.graph = None
+        for lane in self.lanes:
+            lane.close()
+        self.lanes = []
         self.model = None
-        self.x = None
-        self.out = None
-        self.stream = None
-        if self.hip_stream is not None:
-            self.hip_stream.close()
-            self.hip_stream = None
 
 
 class DataPlane:
@@ -294,13 +329,12 @@ class DataPlane:
         so slots of two layouts never overlap."""
         layout = frozenset(k[0] for k in keys)
         if layout != self._layout:
-            if any(s.inflight for s in self.slots.values()):
+            if any(s.in_flight for s in self.slots.values()):
                 self.drains += 1
             self.drain_all()
             self._layout = layout
         active = [self.slots[k] for k in keys]
         n = 0
-        depth = self.cfg.depth
         while True:
             now = time.perf_counter()
             if now >= deadline:
@@ -311,7 +345,7 @@ class DataPlane:
             progressed = False
             for s in active:
                 s.reap()
-                if len(s.inflight) < depth:
+                if s.in_flight < s.capacity:
                     s.submit()
                     n += 1
                     progressed = True
@@ -328,7 +362,8 @@ class DataPlane:
         self.drain_all()
         torch.cuda.synchronize()
         for s in self.slots.values():
-            s.graph = None
+            for lane in s.lanes:
+                lane.graph = None
         gc.collect()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
@@ -674,6 +709,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
                    "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
                    "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
+                   "pod_streams": cfg.pod_streams,
                    "partition_emulation": cfg.emulation,
                    "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
