@@ -509,82 +509,6 @@ __device__ __forceinline__ void store_tile16(const f32x4 (&acc)[TM][TN], int r0,
   }
 }
 
-// ---- split-K with a last-arriver reduction --------------------------------------------------
-// At M = 3401 the model's N = 384 GEMMs (attention projection, fc2) have 81 128x128 tiles for 256
-// CUs, and K = 1536 makes each of them long: splitting K over `splits` workgroups fills the chip.
-// Every split stores its fp32 partial tile to a workspace in the accumulator-native layout (lane-
-// contiguous 8-byte pairs) and counts itself in the tile's arrival counter; the split that arrives
-// LAST adds the partials in split order (0 + p0 + p1 + ... — the same sum whichever split arrives
-// last, so results are bit-reproducible), resets the counter for the next launch and runs the
-// fused epilogue. No workgroup ever waits for another, so co-residency is never assumed
-// (partitions that share CUs cannot deadlock), and no second launch is needed.
-// Coherence without fences: the partials move as agent-scope relaxed atomic stores/loads, which
-// bypass the XCDs' non-coherent L2s, and a store-completion wait orders them before the count.
-// An agent-scope release/acquire fence would do the same by writing back / invalidating the whole
-// L2 of the XCD per workgroup: measured 3-4x slower than the unsplit GEMM.
-typedef unsigned long long u64;
-
-__device__ __forceinline__ u64 pack2(float x, float y) {
-  return u64(__float_as_uint(x)) | (u64(__float_as_uint(y)) << 32);
-}
-
-template <int TM, int TN, int NT>
-__device__ __forceinline__ bool split_reduce(f32x16 (&acc)[TM][TN], float* __restrict__ ws,
-                                             unsigned* __restrict__ ctr, int t, int sp, int splits, int tid,
-                                             int* s_last) {
-  constexpr int CH = TM * TN * 8;  // 8-byte pairs per thread
-  u64* w8 = reinterpret_cast<u64*>(ws);
-  const size_t mine = (size_t(t) * splits + sp) * CH * NT;
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        __hip_atomic_store(&w8[mine + size_t((a * TN + b) * 8 + c) * NT + tid],
-                           pack2(acc[a][b][2 * c], acc[a][b][2 * c + 1]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-  // this wave's partial stores have completed (inline asm: the compiler cannot move stores past it)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0)
-    *s_last = __hip_atomic_fetch_add(&ctr[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              unsigned(splits - 1);
-  __syncthreads();
-  if (!*s_last) return false;
-  if (tid == 0) __hip_atomic_store(&ctr[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  f32x16 sum[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) sum[a][b] = f32x16{0};
-  for (int s = 0; s < splits; ++s) {
-    const size_t base = (size_t(t) * splits + s) * CH * NT;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          float x, y;
-          if (s == sp) {
-            x = acc[a][b][2 * c], y = acc[a][b][2 * c + 1];
-          } else {
-            const u64 v = __hip_atomic_load(&w8[base + size_t((a * TN + b) * 8 + c) * NT + tid], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            x = __uint_as_float(unsigned(v)), y = __uint_as_float(unsigned(v >> 32));
-          }
-          sum[a][b][2 * c] += x;
-          sum[a][b][2 * c + 1] += y;
-        }
-  }
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = sum[a][b];
-  return true;
-}
-
 // BM x BN tile on a WGM x WGN grid of waves (4 or 8 waves: 8 gives each SIMD two waves of one
 // workgroup, so a 128x128 tile — half the bytes per MFMA of 64x64 — still hides its load latency)
 template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32, bool M16 = false>
@@ -593,8 +517,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
                                                   const float* __restrict__ bias, const float* __restrict__ R,
                                                   const float* __restrict__ R2, int r2_rows, float* __restrict__ C,
                                                   __bf16* __restrict__ Cp, size_t c_plane, int M, int N, int K,
-                                                  int epi, int splits, float* __restrict__ ws,
-                                                  unsigned* __restrict__ ctr) {
+                                                  int epi) {
   static_assert(S >= 2 && S <= 4, "2-4 LDS stages");
   constexpr int NW = WGM * WGN;
   constexpr int WM = BM / WGM, WN = BN / WGN;
@@ -618,10 +541,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   if (pb.id < 0) return;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
-  // logical unit = (tile, split), a tile's splits adjacent so they share an XCD (and its L2)
-  const int u = xcd_major_n(pb.id, pb.n, pb.nx);
-  if (u >= tiles * splits) return;
-  const int t = u / splits, sp = u - t * splits;
+  const int t = xcd_major_n(pb.id, pb.n, pb.nx);
+  if (t >= tiles) return;
   int mt, nt;
   tile_rc(t, tiles_m, tiles_n, group, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
@@ -642,8 +563,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #pragma unroll
     for (int b = 0; b < TN16; ++b) acc16[M16 ? a : 0][M16 ? b : 0] = f32x4{0};
 
-  const int nk_all = K / BKS, kb = sp * nk_all / splits;
-  const int nk = (sp + 1) * nk_all / splits - kb;  // this split's stages [kb, kb + nk)
+  const int nk = K / BKS;
   uint32_t voff_a[BM / RPI / NW], voff_b[BN / RPI / NW];
   dma_offsets<BM, NW, BKS, M16>(voff_a, m0, M - 1, K, wave, lane);
   dma_offsets<BN, NW, BKS, M16>(voff_b, n0, N - 1, K, wave, lane);
@@ -662,7 +582,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 // bounds-checked issue and the smaller waits (vm_wait_stage).
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
-    const int k0_ = (kb + (STAGE)) * BKS;                                          \
+    const int k0_ = (STAGE) * BKS;                                                 \
     if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave); \
     if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave); \
   }
@@ -703,13 +623,6 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   // correct run to run but no faster (qkv 27.6 vs 27.6 us, fc1 47.4 vs 46.3 on the whole GPU):
   // the plane bytes, not the instruction count, set the epilogue's time. (A scratch in the freed
   // stage buffers had given run-to-run differences with several workgroups per CU.)
-  if constexpr (!M16) {
-    // the "last arriver" word lives in the (now idle) first stage buffer: a second __shared__
-    // object beside the DMA staging buffers can make the compiler wait for all DMA before every
-    // fragment read of the K loop
-    if (splits > 1 && !split_reduce<TM, TN, 64 * NW>(acc, ws, ctr, t, sp, splits, tid, reinterpret_cast<int*>(A0)))
-      return;
-  }
   if constexpr (M16)
     store_tile16<TM16, TN16>(acc16, m0 + wm * WM, n0 + wn * WN, lane, bias, R, R2, r2_rows, C, Cp, c_plane, M, N,
                              epi);
@@ -721,7 +634,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32, bool M16 = false>
 int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
              const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
-             hipStream_t s, int splits = 1, float* ws = nullptr, unsigned* ctr = nullptr) {
+             hipStream_t s) {
   if (N % BN) {
     g_err = "gemm_x3: N must be a multiple of the tile width " + std::to_string(BN);
     return -1;
@@ -730,14 +643,10 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     g_err = "gemm_x3: K must be a multiple of the stage depth " + std::to_string(BKS);
     return -1;
   }
-  if (splits < 1 || splits > K / BKS || (splits > 1 && (M16 || !ws || !ctr))) {
-    g_err = "gemm_x3: splits must be 1..K/stage, and a split launch needs a workspace and counters (32x32 tiles)";
-    return -1;
-  }
   const int tiles = ((M + BM - 1) / BM) * (N / BN);
-  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(pinned_grid(tiles * splits, unsigned(epi >> 20) & 0xffu)),
+  hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(pinned_grid(tiles, unsigned(epi >> 20) & 0xffu)),
                      dim3(64 * WGM * WGN), 0, s, A,
-                     ap, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi, splits, ws, ctr);
+                     ap, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     g_err = std::string("gemm_x3d: ") + hipGetErrorString(e);
@@ -926,11 +835,7 @@ static const int kCfgX3[35][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128,
 
 static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, const float* bias, const float* R,
                     const float* R2, int r2_rows, float* C, __bf16* cpp, size_t cp, int M, int N, int K, int epi,
-                    int cfg, hipStream_t s, int splits, float* ws, unsigned* ctr) {
-  if (splits > 1 && cfg < 7) {
-    g_err = "gemm_x3: split-K needs an LDS-DMA tile (config 7..34)";
-    return -1;
-  }
+                    int cfg, hipStream_t s) {
   switch (cfg) {
     case 0: return launch<32, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 1: return launch<64, 32, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
@@ -939,34 +844,34 @@ static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, cons
     case 4: return launch<32, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 5: return launch<64, 32, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 6: return launch<32, 64, 1>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 7: return launch_d<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 8: return launch_d<64, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 9: return launch_d<128, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 10: return launch_d<64, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 11: return launch_d<128, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 12: return launch_d<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 13: return launch_d<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 14: return launch_d<128, 128, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 15: return launch_d<32, 64, 1, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 16: return launch_d<32, 64, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 17: return launch_d<64, 32, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 18: return launch_d<64, 64, 2, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 19: return launch_d<64, 64, 2, 2, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 20: return launch_d<64, 32, 2, 1, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 21: return launch_d<32, 64, 1, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 22: return launch_d<64, 32, 2, 1, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 23: return launch_d<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 24: return launch_d<64, 128, 2, 4, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 25: return launch_d<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 26: return launch_d<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 27: return launch_d<64, 64, 2, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 28: return launch_d<64, 64, 2, 2, 3, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 29: return launch_d<128, 128, 2, 4, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 30: return launch_d<32, 64, 1, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 31: return launch_d<64, 32, 2, 1, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 32: return launch_d<128, 192, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 33: return launch_d<64, 96, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
-    case 34: return launch_d<64, 192, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s, splits, ws, ctr);
+    case 7: return launch_d<64, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 8: return launch_d<64, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 9: return launch_d<128, 64, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 10: return launch_d<64, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 11: return launch_d<128, 128, 2, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 12: return launch_d<64, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 13: return launch_d<128, 128, 2, 4, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 14: return launch_d<128, 128, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 15: return launch_d<32, 64, 1, 2, 3>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 16: return launch_d<32, 64, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 17: return launch_d<64, 32, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 18: return launch_d<64, 64, 2, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 19: return launch_d<64, 64, 2, 2, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 20: return launch_d<64, 32, 2, 1, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 21: return launch_d<32, 64, 1, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 22: return launch_d<64, 32, 2, 1, 3, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 23: return launch_d<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 24: return launch_d<64, 128, 2, 4, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 25: return launch_d<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 26: return launch_d<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 27: return launch_d<64, 64, 2, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 28: return launch_d<64, 64, 2, 2, 3, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 29: return launch_d<128, 128, 2, 4, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 30: return launch_d<32, 64, 1, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 31: return launch_d<64, 32, 2, 1, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 32: return launch_d<128, 192, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 33: return launch_d<64, 96, 2, 1, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 34: return launch_d<64, 192, 1, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;
@@ -1046,45 +951,7 @@ int nos_gemm_x3(const void* A, size_t ap, const void* W, size_t wp, const float*
   __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
-  return dispatch(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, cfg, s, 1, nullptr, nullptr);
-}
-
-// Split-K launch of an LDS-DMA tile config (7..34, 32x32 MFMA tiles): each tile's K range is split
-// over `splits` workgroups, the last to finish reduces (see split_reduce). ws: at least
-// nos_gemm_x3_split_ws_bytes(...) bytes; ctr: one zeroed unsigned per tile, private to the stream
-// (every launch leaves the counters zeroed again).
-int nos_gemm_x3_split(const void* A, size_t ap, const void* W, size_t wp, const float* bias, const float* R,
-                      const float* R2, int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi,
-                      int cfg, int splits, void* ws, void* ctr, void* stream) {
-  if (K % BK || ap % 8 || wp % 8 || cp % 8 || (!C && !Cp)) {
-    g_err = "gemm_x3: K must be a multiple of 32, plane strides multiples of 8 elements, and an output given";
-    return -1;
-  }
-  if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R) || ((epi & EPI_RES2) && (!R2 || r2_rows <= 0))) {
-    g_err = "gemm_x3: epilogue operand missing";
-    return -1;
-  }
-  if (cfg < 7 || cfg > 34 || (cfg >= 27 && cfg <= 31)) {
-    g_err = "gemm_x3: split-K needs an LDS-DMA 32x32-MFMA tile (config 7..26, 32..34)";
-    return -1;
-  }
-  epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
-  return dispatch(reinterpret_cast<const __bf16*>(A), ap, reinterpret_cast<const __bf16*>(W), wp, bias, R, R2,
-                  r2_rows, C, reinterpret_cast<__bf16*>(Cp), cp, M, N, K, epi, cfg,
-                  reinterpret_cast<hipStream_t>(stream), splits, reinterpret_cast<float*>(ws),
-                  reinterpret_cast<unsigned*>(ctr));
-}
-
-// workspace bytes and counter count of a split launch
-long long nos_gemm_x3_split_ws_bytes(int cfg, int M, int N, int splits) {
-  if (cfg < 0 || cfg > 34) return -1;
-  const long long bm = kCfgX3[cfg][0], bn = kCfgX3[cfg][1];
-  return ((M + bm - 1) / bm) * (N / bn) * (long long)splits * bm * bn * 4;
-}
-
-int nos_gemm_x3_split_tiles(int cfg, int M, int N) {
-  if (cfg < 0 || cfg > 34) return -1;
-  return ((M + kCfgX3[cfg][0] - 1) / kCfgX3[cfg][0]) * (N / kCfgX3[cfg][1]);
+  return dispatch(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, cfg, s);
 }
 
 }  // extern "C"

@@ -376,29 +376,39 @@ def test_attention_x3_fp32_input_equals_planes_input(K, T, H, B):
         assert (out - ref).abs().max().item() < 2e-6
 
 
-def test_gemm_x3_split_k_reproducible_concurrent_and_counters_reset(K):
-    # split-K: the last-arriving split sums the partials in split order, so repeated launches are
-    # bit-identical; two streams (own workspaces) run concurrently; every launch re-zeroes counters
-    from walkai_nos_amd.ops import gemm as G
-    torch.manual_seed(5)
-    M, N, Kd = 3401, 384, 1536
-    x3 = K.split3(torch.randn(M, Kd, device="cuda"))
-    w = torch.randn(N, Kd, device="cuda") * 0.05
-    b = torch.randn(N, device="cuda")
-    r = torch.randn(M, N, device="cuda")
-    ref = x3.double().sum(0) @ w.double().t() + b.double() + r.double()
-    cfgs = [c for c in G.x3_eligible(N, Kd) if c in G.X3_SPLIT]
-    assert cfgs
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+def test_detection_heads_fused_match_torch(K):
+    # final LayerNorm + class/box MLPs (csrc/head.hip, three launches) vs the torch modules in fp32
+    import torch.nn.functional as F
+    from walkai_nos_amd.models.workload.yolos import YolosSmall
+    torch.manual_seed(4)
+    m = YolosSmall().cuda().eval()
+    for p in list(m.cls_head.parameters()) + list(m.box_head.parameters()) + list(m.ln_f.parameters()):
+        p.data.normal_(0, 0.05)
+    det = torch.randn(100, 384, device="cuda")
+    with torch.no_grad():
+        logits, boxes = K.detection_heads(det, m.ln_f, m.cls_head.layers, m.box_head.layers)
+        h = F.layer_norm(det.double(), (384,), m.ln_f.weight.double(), m.ln_f.bias.double(), m.ln_f.eps)
+
+        def mlp(layers, x):
+            for i, l in enumerate(layers):
+                x = x @ l.weight.double().t() + l.bias.double()
+                if i < len(layers) - 1:
+                    x = torch.relu(x)
+            return x
+        ref_l, ref_b = mlp(m.cls_head.layers, h), torch.sigmoid(mlp(m.box_head.layers, h))
     torch.cuda.synchronize()
-    for cfg in cfgs:
-        outs = []
-        for s in (s1, s2, s1):
-            with torch.cuda.stream(s):
-                outs.append(G.gemm_x3(x3, w, b, residual=r, tile=cfg))
+    assert logits.shape == (100, 92) and boxes.shape == (100, 4)
+    assert (logits.double() - ref_l).abs().max().item() < 1e-5
+    assert (boxes.double() - ref_b).abs().max().item() < 1e-6
+
+
+def test_patch_planes_equal_im2col_split(K):
+    torch.manual_seed(6)
+    for (B, H, W, p) in [(1, 800, 1066, 16), (2, 64, 98, 16), (1, 36, 40, 4)]:
+        px = torch.randn(B, 3, H, W, device="cuda")
+        gh, gw = H // p, W // p
+        cols = px[:, :, :gh * p, :gw * p].reshape(B, 3, gh, p, gw, p).permute(0, 2, 4, 1, 3, 5) \
+            .reshape(B * gh * gw, 3 * p * p)
+        planes = K.patch_planes(px, p)
         torch.cuda.synchronize()
-        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]), cfg
-        assert (outs[0].double() - ref).abs().max().item() < 2e-4, cfg
-    for ws in G._split_ws.values():
-        if ws.ctr is not None:
-            assert int(ws.ctr.abs().sum().item()) == 0
+        assert torch.equal(planes, K.split3(cols.contiguous())), (B, H, W, p)

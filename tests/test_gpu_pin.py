@@ -4,7 +4,7 @@ partition's kernels on its own XCDs only.
 * census: under 8 concurrent streams, every logical block of a pinned launch runs exactly once and
   only on an XCD of its mask (the dispatcher's round-robin XCD placement, read back from
   HW_REG_XCC_ID);
-* numerics: every pinned hot op (split3, LayerNorm, x3 GEMM tiles incl. persistent and split-K, x3
+* numerics: every pinned hot op (split3, LayerNorm, x3 GEMM tiles incl. persistent ones, x3
   attention, the whole model) is bit-identical to its unpinned launch — pinning changes only where
   workgroups run, never what they compute.
 """
@@ -82,13 +82,13 @@ def test_pinned_ops_bit_identical_to_unpinned(K, mask):
                                          K.layernorm(x[None], w, b, 1e-12)))
     for r, g in zip(ref, got):
         assert torch.equal(r, g)
-    # x3 GEMM: one tile of every kind (register-staged, LDS-DMA, 16x16 MFMA, persistent, split-K)
+    # x3 GEMM: one tile of every kind (register-staged, LDS-DMA, 16x16 MFMA, persistent)
     a3 = K.split3(torch.randn(T, D, device="cuda"))
     wt = torch.randn(3 * D, D, device="cuda") * 0.05
     bt = torch.randn(3 * D, device="cuda")
     res = torch.randn(T, 3 * D, device="cuda")
-    cfgs = [c for c in (3, 11, 14, 24, 29, 102, 107, 1142, 1143) if c in G.x3_eligible(3 * D, D)]
-    assert len(cfgs) >= 7
+    cfgs = [c for c in (3, 11, 14, 24, 29, 102, 107) if c in G.x3_eligible(3 * D, D)]
+    assert len(cfgs) >= 6
     for cfg in cfgs:
         r = _pinned(K, 0, cus, lambda: G.gemm_x3(a3, wt, bt, residual=res, tile=cfg, out_f32=True, out_x3=True))
         g = _pinned(K, mask, cus, lambda: G.gemm_x3(a3, wt, bt, residual=res, tile=cfg, out_f32=True, out_x3=True))

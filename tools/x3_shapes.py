@@ -1,7 +1,7 @@
 """Every eligible x3 GEMM config on the model's four GEMM shapes (with their real epilogues and
 outputs) on one slice, timed by HIP-graph replay: python tools/x3_shapes.py [--slice spx]
-[--only split|all] [--out gpurun_out/x3_shapes.json]. Prints the five fastest per shape and the
-fastest unsplit one, then the per-layer GEMM total of the tuner's pick."""
+[--out gpurun_out/x3_shapes.json]. Prints the three fastest per shape, then the per-layer GEMM
+total of the fastest picks."""
 from __future__ import annotations
 
 import argparse
@@ -71,16 +71,12 @@ def main() -> int:
                                           s, a.iters), 2)
             flops = 2.0 * T * N * Kd
             order = sorted(times, key=times.get)
-            best_plain = next(c for c in order if c not in G.X3_SPLIT)
-            res[name] = {"top5": [{"cfg": c, "tile": G.X3_TILES[c], "split": G.X3_SPLIT.get(c, (c, 1))[1],
-                                   "us": times[c], "fp32eq_tflops": round(flops / times[c] / 1e6, 1)}
-                                  for c in order[:5]],
-                         "best_unsplit": {"cfg": best_plain, "tile": G.X3_TILES[best_plain], "us": times[best_plain]},
+            res[name] = {"top5": [{"cfg": c, "tile": G.X3_TILES[c], "us": times[c],
+                                   "fp32eq_tflops": round(flops / times[c] / 1e6, 1)} for c in order[:5]],
                          "all_us": {str(c): t for c, t in times.items()}}
-            print(name, json.dumps(res[name]["top5"][:3]), "unsplit", res[name]["best_unsplit"], flush=True)
+            print(name, json.dumps(res[name]["top5"][:3]), flush=True)
     res["layer_best_us"] = round(sum(r["top5"][0]["us"] for k, r in res.items() if k in SHAPES), 1)
-    res["layer_best_unsplit_us"] = round(sum(r["best_unsplit"]["us"] for k, r in res.items() if k in SHAPES), 1)
-    print("per-layer GEMMs: best", res["layer_best_us"], "us; best unsplit", res["layer_best_unsplit_us"], "us")
+    print("per-layer GEMMs: best", res["layer_best_us"], "us")
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump({"slice": a.slice, **res}, f, indent=1)

@@ -172,28 +172,53 @@ class YolosSmall(nn.Module):
 
     def invalidate_cache(self) -> None:
         self._pos_cache.clear()
+        self._tok_key = None
 
     # -- forward -------------------------------------------------------------------------
     def forward(self, pixels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         B, _, Hh, Ww = pixels.shape
         pe, mid = self.position_embeddings((Hh, Ww))
         nd = self.c.num_detection_tokens
-        if B == 1 and pixels.is_cuda and K.get_backend() == "hip":
-            # patch rows written straight into the token buffer by the GEMM (bias + pos fused)
+        hip = B == 1 and pixels.is_cuda and K.get_backend() == "hip"
+        if hip:
+            # one copy of the token template (class/detection token rows already + pos), then the
+            # patch rows written straight into it by the GEMM (bias + pos fused)
             P = (Hh // self.c.patch_size) * (Ww // self.c.patch_size)
-            x = torch.empty(1, 1 + P + nd, self.c.hidden_size, device=pixels.device, dtype=pixels.dtype)
+            x = self.token_template((Hh, Ww)).clone()
             K.patch_embed(pixels, self.patch.weight, self.patch.bias, self.c.patch_size, pe[0, 1:1 + P],
                           out=x[0, 1:1 + P])
-            x[:, :1] = self.cls_token + pe[:, :1]
-            x[:, 1 + P:] = self.det_tokens + pe[:, 1 + P:]
         else:
             xp = K.patch_embed(pixels, self.patch.weight, self.patch.bias, self.c.patch_size)   # [B, P, D]
             x = torch.cat((self.cls_token.expand(B, -1, -1), xp, self.det_tokens.expand(B, -1, -1)), dim=1) + pe
         for i, blk in enumerate(self.blocks):
             x = blk(x, mid[i] if mid is not None and i < self.c.num_layers - 1 else None)
         det = x[:, -self.c.num_detection_tokens:, :]
+        if hip and x.is_contiguous() and self.heads_fusable():
+            # final LayerNorm + both MLP heads in three launches (csrc/head.hip)
+            logits, boxes = K.detection_heads(det[0], self.ln_f, self.cls_head.layers, self.box_head.layers)
+            return logits[None], boxes[None]
         det = K.layernorm(det.contiguous(), self.ln_f.weight, self.ln_f.bias, self.c.layer_norm_eps)
         return self.cls_head(det), torch.sigmoid(self.box_head(det))
+
+    def heads_fusable(self) -> bool:
+        ch, bh = self.cls_head.layers, self.box_head.layers
+        return (len(ch) == 3 and len(bh) == 3 and ch[0].weight.shape == bh[0].weight.shape
+                and ch[1].weight.shape == bh[1].weight.shape)
+
+    def token_template(self, hw: Tuple[int, int]) -> torch.Tensor:
+        """[1, T, D]: the class-token row + its position embedding, zero patch rows, the detection-token
+        rows + theirs — cached per parameter versions (every forward copies it once)."""
+        key = (hw, str(self.pos_embed.device), self.pos_embed._version, self.cls_token._version,
+               self.det_tokens._version)
+        if getattr(self, "_tok_key", None) != key:
+            pe, _ = self.position_embeddings(hw)
+            nd = self.c.num_detection_tokens
+            with torch.no_grad():
+                t = torch.zeros_like(pe)
+                t[:, :1] = self.cls_token + pe[:, :1]
+                t[:, -nd:] = self.det_tokens + pe[:, -nd:]
+            self._tok, self._tok_key = t, key
+        return self._tok
 
     def flops_per_inference(self, hw: Tuple[int, int] = DEMO_INPUT_HW) -> float:
         c = self.c

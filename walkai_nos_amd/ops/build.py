@@ -94,7 +94,7 @@ TARGETS: Sequence[Target] = (
     Target("libnos_hbmlimit.so", ["hbm_limit.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"], libs=["dl"]),
     Target("libnos_barrier.so", ["rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
            libs=["rccl", "amdhip64"]),
-    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip"], "hipcc"),
+    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip"], "hipcc"),
 )
 
 

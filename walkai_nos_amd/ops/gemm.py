@@ -224,22 +224,12 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             108: (128, 64, 4, "p"), 109: (64, 128, 4, "p")}
 #: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
 X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
-#: split-K configs (csrc/gemm_x3.hip split_reduce): id -> (LDS-DMA base tile, K splits). Each tile's
-#: K range is spread over `splits` workgroups and the last to finish reduces the fp32 partials in
-#: split order (bit-reproducible) and runs the epilogue: the N = 384 GEMMs have 81-162 tiles at
-#: M = 3401, too few for 256 CUs.
-X3_SPLIT = {1000 + 10 * base + sp: (base, sp) for base in (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 32)
-            for sp in (2, 3, 4)}
-for _id, (_base, _sp) in X3_SPLIT.items():
-    X3_TILES[_id] = X3_TILES[_base][:3] + ("s" + X3_TILES[_base][3],)
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
                    18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 3, 28: 2, 29: 1, 30: 4, 31: 4,
                    32: 1, 33: 2, 34: 1,
                    100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1}
-for _id, (_base, _sp) in X3_SPLIT.items():
-    X3_SLOTS_PER_CU[_id] = X3_SLOTS_PER_CU[_base]
 _x3_cache: Dict[Tuple[int, int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
@@ -252,11 +242,6 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_persistent.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32,
                                              i32, vp]
-        L.nos_gemm_x3_split.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32,
-                                        i32, vp, vp, vp]
-        L.nos_gemm_x3_split_ws_bytes.argtypes = [i32, i32, i32, i32]
-        L.nos_gemm_x3_split_ws_bytes.restype = ctypes.c_longlong
-        L.nos_gemm_x3_split_tiles.argtypes = [i32, i32, i32]
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         L.nos_gemm_x3_set_group.argtypes = [i32]
         L.nos_gemm_x3_set_ablate.argtypes = [i32]
@@ -302,43 +287,6 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
     return p
 
 
-class _SplitWorkspace:
-    """A stream's split-K scratch: fp32 partial tiles and per-tile arrival counters (zeroed once;
-    every launch leaves them zeroed). Buffers are only ever added, never freed or replaced while
-    the process runs: a captured HIP graph keeps their addresses."""
-
-    def __init__(self):
-        self.ws: Optional[torch.Tensor] = None
-        self.ctr: Optional[torch.Tensor] = None
-        self.keep: list = []
-
-    def get(self, nbytes: int, tiles: int, device) -> Optional[Tuple[torch.Tensor, torch.Tensor]]:
-        grow_ws = self.ws is None or self.ws.numel() * 4 < nbytes
-        grow_ctr = self.ctr is None or self.ctr.numel() < tiles
-        if grow_ws or grow_ctr:
-            if torch.cuda.is_current_stream_capturing():
-                return None  # never allocate under capture: the caller runs unsplit
-            if grow_ws:
-                self.ws = torch.empty(max(nbytes // 4, 1 << 20), dtype=torch.float32, device=device)
-                self.keep.append(self.ws)
-            if grow_ctr:
-                self.ctr = torch.zeros(max(tiles, 4096), dtype=torch.int32, device=device)
-                self.keep.append(self.ctr)
-        return self.ws, self.ctr
-
-
-_split_ws: Dict[Tuple[int, int], _SplitWorkspace] = {}
-
-
-def split_workspace(device, stream) -> _SplitWorkspace:
-    key = (device.index if device.index is not None else torch.cuda.current_device(), int(stream.cuda_stream))
-    with _lock:
-        w = _split_ws.get(key)
-        if w is None:
-            w = _split_ws[key] = _SplitWorkspace()
-    return w
-
-
 def x3_eligible(N: int, Kd: int) -> list:
     """Tiles that can run this shape; ``NOS_X3_EXCLUDE`` (comma-separated kind prefixes, e.g.
     ``m16,p``) and ``NOS_X3_MIN_TILE`` (minimum BM*BN) drop tiles from autotuning for A/B runs."""
@@ -348,7 +296,7 @@ def x3_eligible(N: int, Kd: int) -> list:
     min_area = int(os.environ.get("NOS_X3_MIN_TILE", "0"))
     return [c for c, (bm, bn, _, kind) in X3_TILES.items()
             if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))
-            and bm * bn >= min_area and (c not in X3_SPLIT or Kd // (64 if kind.endswith("64") else 32) >= 2 * X3_SPLIT[c][1])]
+            and bm * bn >= min_area]
 
 
 #: tiles at least this large (BM*BN) on a partition that shares the GPU with sibling partitions
@@ -390,10 +338,9 @@ def x3_heuristic(M: int, N: int, cus: int, cands: list) -> int:
     best, best_key = cands[0], None
     for c in cands:
         bm, bn, _, _ = X3_TILES[c]
-        sp = X3_SPLIT[c][1] if c in X3_SPLIT else 1
-        tiles = -(-M // bm) * (N // bn) * sp
+        tiles = -(-M // bm) * (N // bn)
         rounds = -(-tiles // (X3_SLOTS_PER_CU[c] * cus))
-        key = (rounds * bm * bn / sp / min(X3_SLOTS_PER_CU[c], 2), sp, -bm * bn)
+        key = (rounds * bm * bn / min(X3_SLOTS_PER_CU[c], 2), -bm * bn)
         if best_key is None or key < best_key:
             best, best_key = c, key
     return best
@@ -410,16 +357,7 @@ def _launch_x3(cfg, a3, w3, bias, res, r2, out, out3, epi) -> None:
             out3.data_ptr() if out3 is not None else None, out3[0].numel() if out3 is not None else 0,
             M, N, Kd, epi)
     stream = torch.cuda.current_stream().cuda_stream
-    if cfg in X3_SPLIT:
-        base, sp = X3_SPLIT[cfg]
-        L = _lib_x3()
-        w = split_workspace(a3.device, torch.cuda.current_stream()).get(
-            L.nos_gemm_x3_split_ws_bytes(base, M, N, sp), L.nos_gemm_x3_split_tiles(base, M, N), a3.device)
-        if w is None:
-            rc = L.nos_gemm_x3(*args, base, stream)
-        else:
-            rc = L.nos_gemm_x3_split(*args, base, sp, w[0].data_ptr(), w[1].data_ptr(), stream)
-    elif cfg >= 100:
+    if cfg >= 100:
         grid = max(1, X3_SLOTS_PER_CU[cfg] * K.slice_cus() - int(os.environ.get("NOS_X3_PGRID_SLACK", "0")))
         rc = _lib_x3().nos_gemm_x3_persistent(*args, cfg - 100, grid, stream)
     else:

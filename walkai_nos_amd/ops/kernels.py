@@ -24,7 +24,7 @@ import ctypes
 import math
 import os
 import threading
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -440,6 +440,87 @@ def linear_x3(a3: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], gelu
                    out=out)
 
 
+def _head_lib() -> ctypes.CDLL:
+    L = _L()
+    if not getattr(L, "_nos_head_bound", False):
+        vp, i32 = ctypes.c_void_p, ctypes.c_int
+        P = ctypes.POINTER
+        L.nos_small_linear_f32.argtypes = [i32, P(vp), P(i32), P(vp), P(vp), P(vp), P(i32), P(i32), P(i32), i32, i32,
+                                           vp, vp, ctypes.c_float, vp]
+        L.nos_patch_planes_f32.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, i32, vp]
+        L.nos_head_last_error.restype = ctypes.c_char_p
+        L._nos_head_bound = True
+    return L
+
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID = 0, 1, 2
+
+
+def small_linear(groups, M: int, K: int, ln: Optional[Tuple[torch.Tensor, torch.Tensor, float]] = None) -> None:
+    """Up to two row-aligned fp32 GEMMs in one launch (``csrc/head.hip``): each group is
+    ``(x, ldx, w, b, y, ldy, act)`` with ``x``/``y`` device pointers (ints) or tensors whose rows are
+    ``ldx``/``ldy`` apart; ``y[m, :n] = act(LN?(x[m, :K]) @ w.T + b)``; ``ln = (weight, bias, eps)``
+    normalises x's rows (over K) while staging them. Exact fp32 FMAs on the vector ALUs."""
+    L = _head_lib()
+    n = len(groups)
+    VP, I32 = ctypes.c_void_p * n, ctypes.c_int * n
+
+    def ptr(t):
+        return t if isinstance(t, int) else (t.data_ptr() if t is not None else None)
+    xs = VP(*[ptr(g[0]) for g in groups])
+    ldx = I32(*[g[1] for g in groups])
+    ws = VP(*[g[2].data_ptr() for g in groups])
+    bs = VP(*[ptr(g[3]) for g in groups])
+    ys = VP(*[ptr(g[4]) for g in groups])
+    ldy = I32(*[g[5] for g in groups])
+    ns = I32(*[g[2].shape[0] for g in groups])
+    acts = I32(*[g[6] for g in groups])
+    lw, lb, eps = (ln[0].data_ptr(), ln[1].data_ptr(), float(ln[2])) if ln is not None else (None, None, 0.0)
+    rc = L.nos_small_linear_f32(n, xs, ldx, ws, bs, ys, ldy, ns, acts, M, K, lw, lb, eps, _stream())
+    if rc != 0:
+        raise RuntimeError(f"nos small_linear failed: {L.nos_head_last_error().decode()} (rc={rc})")
+
+
+def detection_heads(det: torch.Tensor, ln_f, cls_layers, box_layers) -> Tuple[torch.Tensor, torch.Tensor]:
+    """YOLOS' final LayerNorm + class MLP + box MLP (3 Linear layers each, ReLU between, sigmoid on
+    the boxes) on ``det`` ``[M, D]`` (contiguous rows) in three launches: layer 1 of both heads with
+    the LayerNorm fused, then layers 2 and 3 of both heads side by side. Returns ``(logits, boxes)``."""
+    M, D = det.shape
+    c1, c2, c3 = cls_layers
+    b1, b2, b3 = box_layers
+    hid = c1.weight.shape[0]
+    h1 = torch.empty(M, 2 * hid, device=det.device)
+    h2 = torch.empty(M, 2 * hid, device=det.device)
+    logits = torch.empty(M, c3.weight.shape[0], device=det.device)
+    boxes = torch.empty(M, b3.weight.shape[0], device=det.device)
+    eb = h1.element_size() * hid
+    small_linear([(det, D, c1.weight, c1.bias, h1, 2 * hid, ACT_RELU),
+                  (det, D, b1.weight, b1.bias, h1.data_ptr() + eb, 2 * hid, ACT_RELU)],
+                 M, D, ln=(ln_f.weight, ln_f.bias, ln_f.eps))
+    small_linear([(h1, 2 * hid, c2.weight, c2.bias, h2, 2 * hid, ACT_RELU),
+                  (h1.data_ptr() + eb, 2 * hid, b2.weight, b2.bias, h2.data_ptr() + eb, 2 * hid, ACT_RELU)],
+                 M, hid)
+    small_linear([(h2, 2 * hid, c3.weight, c3.bias, logits, logits.shape[1], ACT_NONE),
+                  (h2.data_ptr() + eb, 2 * hid, b3.weight, b3.bias, boxes, boxes.shape[1], ACT_SIGMOID)],
+                 M, hid)
+    return logits, boxes
+
+
+def patch_planes(pixels: torch.Tensor, patch: int) -> Optional[torch.Tensor]:
+    """x3 planes ``[3, B*gh*gw, C*p*p]`` of the patch matrix straight from the image (im2col and
+    split in one kernel); None when the image layout does not allow it (odd patch or width)."""
+    B, C, Hh, Ww = pixels.shape
+    if patch % 2 or Ww % 2 or not pixels.is_contiguous():
+        return None
+    gh, gw = Hh // patch, Ww // patch
+    out = torch.empty(3, B * gh * gw, C * patch * patch, dtype=torch.bfloat16, device=pixels.device)
+    L = _head_lib()
+    rc = L.nos_patch_planes_f32(pixels.data_ptr(), out.data_ptr(), B, C, Hh, Ww, patch, gh, gw, _stream())
+    if rc != 0:
+        raise RuntimeError(f"nos patch_planes failed: {L.nos_head_last_error().decode()} (rc={rc})")
+    return out
+
+
 def patch_embed(pixels: torch.Tensor, w: torch.Tensor, b: torch.Tensor, patch: int,
                 pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Non-overlapping patch embedding (a stride-``patch`` conv) as one unfold copy + the MFMA GEMM,
@@ -450,12 +531,16 @@ def patch_embed(pixels: torch.Tensor, w: torch.Tensor, b: torch.Tensor, patch: i
     if not _use_hip(pixels) or pixels.dtype != torch.float32:
         y = F.conv2d(pixels, w, b, stride=patch).flatten(2).transpose(1, 2)
         return y + pos if pos is not None else y
-    cols = pixels[:, :, :gh * patch, :gw * patch].reshape(B, C, gh, patch, gw, patch) \
-        .permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * patch * patch)
+    def im2col() -> torch.Tensor:
+        return pixels[:, :, :gh * patch, :gw * patch].reshape(B, C, gh, patch, gw, patch) \
+            .permute(0, 2, 4, 1, 3, 5).reshape(B * gh * gw, C * patch * patch)
     if x3_active(pixels) and (C * patch * patch) % 32 == 0:
         from .gemm import gemm_x3
-        y = gemm_x3(split3(cols), w.reshape(w.shape[0], -1), b, residual2=pos, out=out)
+        planes = patch_planes(pixels, patch)
+        y = gemm_x3(planes if planes is not None else split3(im2col()), w.reshape(w.shape[0], -1), b,
+                    residual2=pos, out=out)
         return y.view(B, gh * gw, -1)
+    cols = im2col()
     from .gemm import gemm
     y = gemm(cols, w.reshape(w.shape[0], -1), b, residual2=pos, out=out)
     return y.view(B, gh * gw, -1)
