@@ -535,14 +535,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
   __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS], B2[S > 2 ? 3 * BN * BKS : 8],
       B3[S > 3 ? 3 * BN * BKS : 8];
 
-  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7;
+  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7, splits = 1 + ((epi >> 28) & 7);
   const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
   epi &= 0xff;
   if (pb.id < 0) return;
   const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
   const int tiles = tiles_m * tiles_n;
-  const int t = xcd_major_n(pb.id, pb.n, pb.nx);
-  if (t >= tiles) return;
+  // split-K partials (splits > 1): unit = (tile, split), a tile's splits adjacent (one XCD's L2);
+  // split sp sums K stages [sp*nk/splits, (sp+1)*nk/splits) into fp32 plane sp of C [splits][M][N]
+  // with no epilogue — the consumer (splitk_layernorm) adds the planes, bias and residuals
+  const int u = xcd_major_n(pb.id, pb.n, pb.nx);
+  if (u >= tiles * splits) return;
+  const int t = u / splits, sp = u - t * splits;
+  if (splits > 1) C += size_t(sp) * M * N;
   int mt, nt;
   tile_rc(t, tiles_m, tiles_n, group, mt, nt);
   const int m0 = mt * BM, n0 = nt * BN;
@@ -563,7 +568,8 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 #pragma unroll
     for (int b = 0; b < TN16; ++b) acc16[M16 ? a : 0][M16 ? b : 0] = f32x4{0};
 
-  const int nk = K / BKS;
+  const int nk_all = K / BKS, kb = sp * nk_all / splits;
+  const int nk = (sp + 1) * nk_all / splits - kb;
   uint32_t voff_a[BM / RPI / NW], voff_b[BN / RPI / NW];
   dma_offsets<BM, NW, BKS, M16>(voff_a, m0, M - 1, K, wave, lane);
   dma_offsets<BN, NW, BKS, M16>(voff_b, n0, N - 1, K, wave, lane);
@@ -582,7 +588,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3d(const __bf16* __re
 // bounds-checked issue and the smaller waits (vm_wait_stage).
 #define X3D_ISSUE(STAGE, BUF)                                                      \
   {                                                                                \
-    const int k0_ = (STAGE) * BKS;                                                 \
+    const int k0_ = (kb + (STAGE)) * BKS;                                          \
     if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3D_A(BUF), wave); \
     if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3D_B(BUF), wave); \
   }
@@ -643,7 +649,7 @@ int launch_d(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
     g_err = "gemm_x3: K must be a multiple of the stage depth " + std::to_string(BKS);
     return -1;
   }
-  const int tiles = ((M + BM - 1) / BM) * (N / BN);
+  const int tiles = ((M + BM - 1) / BM) * (N / BN) * (1 + ((epi >> 28) & 7));
   hipLaunchKernelGGL((gemm_x3d<BM, BN, WGM, WGN, S, BKS, M16>), dim3(pinned_grid(tiles, unsigned(epi >> 20) & 0xffu)),
                      dim3(64 * WGM * WGN), 0, s, A,
                      ap, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi);
@@ -917,6 +923,24 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
       g_err = "gemm_x3s: unknown config";
       return -1;
   }
+}
+
+// Split-K partial sums of C = A · W^T (LDS-DMA configs 7..34): plane s of C [splits][M][N] fp32
+// holds the K stages [s*nk/splits, (s+1)*nk/splits); no epilogue (the consumer adds the planes in
+// order, then bias and residuals: splitk_layernorm in kernels.hip). 2 <= splits <= min(8, K/stage).
+int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, float* C, int M, int N, int K, int cfg,
+                         int splits, void* stream) {
+  if (K % BK || ap % 8 || wp % 8 || !C) {
+    g_err = "gemm_x3 partials: K % 32, plane strides % 8 and an output";
+    return -1;
+  }
+  if (cfg < 7 || cfg > 34 || splits < 2 || splits > 8 || splits > K / BK) {
+    g_err = "gemm_x3 partials: an LDS-DMA config (7..34) and 2..8 splits";
+    return -1;
+  }
+  const int epi = (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20) | ((splits - 1) << 28);
+  return dispatch(reinterpret_cast<const __bf16*>(A), ap, reinterpret_cast<const __bf16*>(W), wp, nullptr, nullptr,
+                  nullptr, 0, C, nullptr, 0, M, N, K, epi, cfg, reinterpret_cast<hipStream_t>(stream));
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {

@@ -134,6 +134,85 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
 }
 
 // ------------------------------------------------------------------------------------------
+// Split-K combine + residuals + LayerNorm: x = (part_0 + ... + part_{S-1}) + bias + res (+ r2[row %
+// r2_rows]) — the split-K GEMM's epilogue, in the same order as the fused one — stored as the fp32
+// residual stream xout, and, when w is given, LayerNorm(x) stored as x3 planes yp (the next GEMM's
+// operand). One wave per row, grid-stride, lanes on column pairs as layernorm_f32.
+template <int NPL>
+__global__ __launch_bounds__(256) void splitk_layernorm_f32(const float* __restrict__ part, int splits,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ res,
+                                                            const float* __restrict__ r2, int r2_rows,
+                                                            float* __restrict__ xout, const float* __restrict__ w,
+                                                            const float* __restrict__ b, __bf16* __restrict__ yp,
+                                                            int rows, float eps, unsigned pin) {
+  constexpr int D = NPL * 64, NP = NPL / 2;
+  const PinnedBlock pb = pinned_block(pin);
+  if (pb.id < 0) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t pstride = size_t(rows) * (D / 2);  // partial plane stride in float2
+  const float2* p2 = reinterpret_cast<const float2*>(part);
+  const float2* bias2 = reinterpret_cast<const float2*>(bias);
+  for (int row = pb.id * 4 + wave; row < rows; row += pb.n * 4) {
+    const size_t r2i = size_t(row) * (D / 2);
+    float2 v[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) v[i] = p2[r2i + i * 64 + lane];
+    for (int sp = 1; sp < splits; ++sp) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const float2 q = p2[sp * pstride + r2i + i * 64 + lane];
+        v[i].x += q.x;
+        v[i].y += q.y;
+      }
+    }
+    const float2* rr = reinterpret_cast<const float2*>(res) + r2i;
+    const float2* rr2 = r2 ? reinterpret_cast<const float2*>(r2) + size_t(row % r2_rows) * (D / 2) : nullptr;
+    float2* xo = reinterpret_cast<float2*>(xout) + r2i;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int c2 = i * 64 + lane;
+      const float2 bb = bias2[c2], r = rr[c2];
+      v[i].x = v[i].x + bb.x + r.x;
+      v[i].y = v[i].y + bb.y + r.y;
+      if (rr2) {
+        const float2 q = rr2[c2];
+        v[i].x += q.x;
+        v[i].y += q.y;
+      }
+      xo[c2] = v[i];
+      s += v[i].x + v[i].y;
+    }
+    if (!w) continue;
+    const float mean = wave_sum(s) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      v[i].x -= mean;
+      v[i].y -= mean;
+      q += v[i].x * v[i].x + v[i].y * v[i].y;
+    }
+    const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+    const float2* w2 = reinterpret_cast<const float2*>(w);
+    const float2* b2 = reinterpret_cast<const float2*>(b);
+    const size_t plane2 = size_t(rows) * D / 2;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(yp) + r2i;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int c2 = i * 64 + lane;
+      const float2 ww = w2[c2], bb = b2[c2];
+      const f32x2 val = {v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y};
+      bf16x2 h0, h1, h2;
+      split3(val, h0, h1, h2);
+      dst[c2] = __builtin_bit_cast(uint32_t, h0);
+      dst[plane2 + c2] = __builtin_bit_cast(uint32_t, h1);
+      dst[2 * plane2 + c2] = __builtin_bit_cast(uint32_t, h2);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // bias + exact GELU, in place
 __global__ __launch_bounds__(256) void bias_gelu_f32(float* __restrict__ y, const float* __restrict__ b, size_t n4,
                                                      int N4) {
@@ -1491,6 +1570,39 @@ int nos_layernorm_f32_grid(const float* x, const float* w, const float* b, float
       return -1;
   }
   return check_launch("layernorm_f32");
+}
+
+// Split-K combine (+ bias, residual, broadcast residual r2 or null) into xout, and LayerNorm(xout) as
+// x3 planes into yp when w/b/yp are given; part = [splits][rows][D] fp32; D in {384, 768}; `wgs`
+// workgroups of 4 rows (grid-stride), 0 = one per 4 rows.
+int nos_splitk_layernorm_f32(const float* part, int splits, const float* bias, const float* res, const float* r2,
+                             int r2_rows, float* xout, const float* w, const float* b, void* yp, int rows, int D,
+                             float eps, int wgs, void* stream) {
+  if (!part || splits < 1 || !bias || !res || !xout || (r2 && r2_rows <= 0) || ((w == nullptr) != (yp == nullptr)) ||
+      ((w == nullptr) != (b == nullptr))) {
+    g_err = "splitk_layernorm: partials, bias, residual and output required; LayerNorm needs w, b and yp";
+    return -1;
+  }
+  if (rows <= 0) return 0;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int full = (rows + 3) / 4;
+  const unsigned pin = g_pin;
+  const dim3 grid(pinned_grid(pinned_cap(wgs > 0 ? std::min(wgs, full) : full, pin), pin)), block(256);
+  __bf16* p = reinterpret_cast<__bf16*>(yp);
+  switch (D) {
+    case 384:
+      hipLaunchKernelGGL(splitk_layernorm_f32<6>, grid, block, 0, s, part, splits, bias, res, r2, r2_rows, xout, w,
+                         b, p, rows, eps, pin);
+      break;
+    case 768:
+      hipLaunchKernelGGL(splitk_layernorm_f32<12>, grid, block, 0, s, part, splits, bias, res, r2, r2_rows, xout, w,
+                         b, p, rows, eps, pin);
+      break;
+    default:
+      g_err = "splitk_layernorm: unsupported hidden size " + std::to_string(D);
+      return -1;
+  }
+  return check_launch("splitk_layernorm_f32");
 }
 
 int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,

@@ -412,3 +412,55 @@ def test_patch_planes_equal_im2col_split(K):
         planes = K.patch_planes(px, p)
         torch.cuda.synchronize()
         assert torch.equal(planes, K.split3(cols.contiguous())), (B, H, W, p)
+
+
+@pytest.mark.parametrize("M,N,Kd", [(3401, 384, 1536), (3401, 384, 384), (300, 768, 256)])
+def test_splitk_partials_and_combine_layernorm(K, M, N, Kd):
+    # split-K partial GEMM (every offered tile x split count) + the combine/residual/LayerNorm kernel
+    # vs fp64; the partial planes sum to the unsplit product
+    import torch.nn.functional as F
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(8)
+    x3 = K.split3(torch.randn(M, Kd, device="cuda"))
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda")
+    r2 = torch.randn(1, 97, N, device="cuda")
+    lw, lb = torch.randn(N, device="cuda"), torch.randn(N, device="cuda")
+    a = x3.double().sum(0)
+    hb = a @ G.weight_planes(w).double().sum(0).t()
+    ref_x = hb + b.double() + r.double() + r2.double().reshape(97, N)[torch.arange(M) % 97]
+    ref_ln = F.layer_norm(ref_x, (N,), lw.double(), lb.double(), 1e-12)
+    cands = G.split_candidates(N, Kd)
+    assert cands
+    for cfg, sp in cands:
+        part = G.gemm_x3_partials(x3, w, cfg, sp)
+        x, planes = K.splitk_layernorm(part, b, r, r2, (lw, lb, 1e-12))
+        torch.cuda.synchronize()
+        assert (part.double().sum(0) - hb).abs().max().item() < 1e-4, (cfg, sp)
+        assert (x.double() - ref_x).abs().max().item() < 1e-4, (cfg, sp)
+        assert (planes.double().sum(0) - ref_ln).abs().max().item() < 1e-4, (cfg, sp)
+        x_only, none = K.splitk_layernorm(part, b, r, None)
+        torch.cuda.synchronize()
+        assert none is None
+        assert (x_only.double() - (hb + b.double() + r.double())).abs().max().item() < 1e-4, (cfg, sp)
+
+
+def test_linear_residual_ln_x3_tuned_pipeline(K):
+    # whichever pipeline the tuner picks, the result matches the unfused ops
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(9)
+    M, N, Kd = 3401, 384, 1536
+    f3 = K.split3(torch.randn(M, Kd, device="cuda"))
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(1, M, N, device="cuda")
+    lw, lb = torch.ones(N, device="cuda"), torch.zeros(N, device="cuda")
+    x, h3 = K.linear_residual_ln_x3(f3, w, b, r, ln=(lw, lb, 1e-12))
+    x_ref = G.gemm_x3(f3, w, b, residual=r)
+    h_ref = K.layernorm_x3(x_ref, lw, lb, 1e-12)
+    torch.cuda.synchronize()
+    assert x.shape == r.shape and h3.shape == (3,) + r.shape
+    assert (x - x_ref).abs().max().item() < 1e-4
+    assert (h3.double().sum(0) - h_ref.double().sum(0)).abs().max().item() < 1e-4
+    assert G.fused_table()

@@ -74,6 +74,29 @@ class _Block(nn.Module):
         self.fc1 = nn.Linear(d, f)
         self.fc2 = nn.Linear(f, d)
 
+    def forward_x3(self, x: torch.Tensor, mid: Optional[torch.Tensor], h3: Optional[torch.Tensor],
+                   next_ln: Optional[nn.LayerNorm]) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """The x3 path with the LayerNorms folded into the producing step: ``h3`` is LN1(x) as planes
+        when the previous block already made it; the projection step returns x and LN2(x), the fc2
+        step x and ``next_ln``(x) (the next block's LN1) — each either the fused-epilogue GEMM + a
+        LayerNorm kernel or a split-K GEMM + one combine-and-LayerNorm kernel, whichever is faster
+        on the slice (``ops.gemm.linear_residual_ln_x3``)."""
+        H, Dh = self.c.num_heads, self.c.head_dim
+        eps = self.c.layer_norm_eps
+        if h3 is None:
+            h3 = K.layernorm_x3(x, self.ln1.weight, self.ln1.bias, eps)
+        if K.attention_input_f32():
+            qkv = K.linear_x3(h3, self.qkv.weight, self.qkv.bias)
+            o3 = K.attention_qkv_x3f(qkv, H, Dh, 1.0 / math.sqrt(Dh))
+        else:
+            qkv3 = K.linear_x3(h3, self.qkv.weight, self.qkv.bias, out_x3=True)
+            o3 = K.attention_qkv_x3(qkv3, H, Dh, 1.0 / math.sqrt(Dh))
+        x, h3 = K.linear_residual_ln_x3(o3, self.proj.weight, self.proj.bias, x,
+                                        ln=(self.ln2.weight, self.ln2.bias, eps))
+        f3 = K.linear_x3(h3, self.fc1.weight, self.fc1.bias, gelu=True, out_x3=True)
+        nl = (next_ln.weight, next_ln.bias, next_ln.eps) if next_ln is not None else None
+        return K.linear_residual_ln_x3(f3, self.fc2.weight, self.fc2.bias, x, residual2=mid, ln=nl)
+
     def forward(self, x: torch.Tensor, mid: Optional[torch.Tensor] = None) -> torch.Tensor:
         B, T, D = x.shape
         H, Dh = self.c.num_heads, self.c.head_dim
@@ -190,8 +213,14 @@ class YolosSmall(nn.Module):
         else:
             xp = K.patch_embed(pixels, self.patch.weight, self.patch.bias, self.c.patch_size)   # [B, P, D]
             x = torch.cat((self.cls_token.expand(B, -1, -1), xp, self.det_tokens.expand(B, -1, -1)), dim=1) + pe
-        for i, blk in enumerate(self.blocks):
-            x = blk(x, mid[i] if mid is not None and i < self.c.num_layers - 1 else None)
+        if K.x3_active(x):
+            h3 = None
+            for i, blk in enumerate(self.blocks):
+                nxt = self.blocks[i + 1].ln1 if i + 1 < len(self.blocks) else None
+                x, h3 = blk.forward_x3(x, mid[i] if mid is not None and i < self.c.num_layers - 1 else None, h3, nxt)
+        else:
+            for i, blk in enumerate(self.blocks):
+                x = blk(x, mid[i] if mid is not None and i < self.c.num_layers - 1 else None)
         det = x[:, -self.c.num_detection_tokens:, :]
         if hip and x.is_contiguous() and self.heads_fusable():
             # final LayerNorm + both MLP heads in three launches (csrc/head.hip)

@@ -243,6 +243,7 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3_persistent.argtypes = [vp, sz, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32,
                                              i32, vp]
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
+        L.nos_gemm_x3_partials.argtypes = [vp, sz, vp, sz, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_set_group.argtypes = [i32]
         L.nos_gemm_x3_set_ablate.argtypes = [i32]
         ablate = int(os.environ.get("NOS_X3_ABLATE", "0"))  # timing studies only: results are invalid
@@ -434,3 +435,89 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
     if out_f32 and out_x3:
         return rf, r3
     return rf if out_f32 else r3
+
+
+# ---- split-K partials + combine-and-LayerNorm --------------------------------------------------
+#: LDS-DMA tiles offered to the split-K partial path (32x32 MFMA and 16x16 MFMA, 4 and 8 waves)
+SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32)
+SPLIT_COUNTS = (2, 3, 4)
+
+
+def gemm_x3_partials(a3: torch.Tensor, w: torch.Tensor, cfg: int, splits: int,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Split-K partial sums of ``a @ w^T``: ``[splits, M, N]`` fp32, plane s summing the s-th K range
+    (``csrc/gemm_x3.hip``, one launch of tiles x splits workgroups, no epilogue). The consumer adds
+    the planes (``kernels.splitk_layernorm``): the hand-off is the kernel boundary."""
+    Kd = a3.shape[-1]
+    a3 = a3.reshape(3, -1, Kd)
+    if not a3.is_contiguous():
+        a3 = a3.contiguous()
+    M = a3.shape[1]
+    w3 = w if w.dim() == 3 else weight_planes(w)
+    N = w3.shape[1]
+    if out is None:
+        out = torch.empty(splits, M, N, dtype=torch.float32, device=a3.device)
+    rc = _lib_x3().nos_gemm_x3_partials(a3.data_ptr(), a3[0].numel(), w3.data_ptr(), w3[0].numel(), out.data_ptr(),
+                                        M, N, Kd, cfg, splits, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"nos gemm_x3 partials failed: {_lib_x3().nos_gemm_x3_last_error().decode()} (rc={rc})")
+    return out
+
+
+def split_candidates(N: int, Kd: int) -> list:
+    """(tile, splits) pairs that can run this shape in the partials mode."""
+    out = []
+    for c in SPLIT_TILES:
+        bm, bn, _, kind = X3_TILES[c]
+        bk = 64 if kind.endswith("64") else 32
+        if N % bn or Kd % bk:
+            continue
+        out += [(c, sp) for sp in SPLIT_COUNTS if Kd // bk >= 2 * sp]
+    return out
+
+
+_fused_cache: Dict[tuple, tuple] = {}
+
+
+def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, residual: torch.Tensor,
+                          residual2: Optional[torch.Tensor] = None, ln=None):
+    """``x = a @ w^T + b + residual (+ residual2)`` and, with ``ln = (weight, bias, eps)``, the x3
+    planes of LayerNorm(x): the transformer's projection/fc2 step and the LayerNorm after it. Two
+    pipelines, picked per (shape, slice) by timing both on the caller's stream: the fused-epilogue
+    GEMM + a LayerNorm kernel, or a split-K partial GEMM (more workgroups for the N = 384 shapes)
+    + one kernel that adds the partials, bias and residuals and normalises. Returns ``(x, planes)``
+    (planes None without ``ln``)."""
+    from . import kernels as K
+    lead = residual.shape
+    N = w.shape[0] if w.dim() == 2 else w.shape[1]
+    Kd = a3.shape[-1]
+    M = residual.numel() // N
+    key = (M, N, Kd, residual2 is not None, ln is not None, K.slice_cus(), K.slice_pin())
+    with _lock:
+        choice = _fused_cache.get(key)
+
+    def unsplit():
+        x = gemm_x3(a3, w, b, residual=residual, residual2=residual2)
+        return x, (K.layernorm_x3(x, ln[0], ln[1], ln[2]) if ln is not None else None)
+
+    def split(cfg, sp):
+        part = gemm_x3_partials(a3, w, cfg, sp)
+        return K.splitk_layernorm(part, b, residual, residual2, ln, lead)
+    if choice is None:
+        if torch.cuda.is_current_stream_capturing() or os.environ.get("NOS_SPLITK", "1") == "0":
+            choice = ("unsplit",)  # NOS_SPLITK=0: the fused-epilogue GEMM + LayerNorm only (A/B runs)
+        else:
+            stream = torch.cuda.current_stream()
+            times = {("unsplit",): _gpu_time(unsplit, stream)}
+            for c, sp in split_candidates(N, Kd):
+                times[("split", c, sp)] = _gpu_time(lambda c=c, sp=sp: split(c, sp), stream)
+            choice = min(times, key=times.get)
+            with _lock:
+                _fused_cache[key] = choice
+    return unsplit() if choice[0] == "unsplit" else split(choice[1], choice[2])
+
+
+def fused_table() -> Dict[str, str]:
+    with _lock:
+        return {f"M{m}_N{n}_K{k}_r2{int(r2)}_ln{int(ln)}_cus{c}_pin{p}": "/".join(map(str, v))
+                for (m, n, k, r2, ln, c, p), v in sorted(_fused_cache.items())}

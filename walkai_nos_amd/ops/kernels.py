@@ -301,6 +301,7 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_ws_bytes.restype = ctypes.c_size_t
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             L.nos_set_pin.argtypes = [ctypes.c_uint]
+            L.nos_splitk_layernorm_f32.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, f32, i32, vp]
             L.nos_pin_mask.restype = ctypes.c_uint
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
@@ -358,6 +359,38 @@ def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> 
     _check(_L().nos_layernorm_f32_grid(x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), None, rows, D, eps,
                                        layernorm_wgs(rows), _stream()))
     return out
+
+
+def splitk_layernorm(part: torch.Tensor, bias: torch.Tensor, res: torch.Tensor, res2: Optional[torch.Tensor],
+                     ln=None, shape=None):
+    """``x = sum(part) + bias + res (+ res2 broadcast by row)`` from split-K partials ``[S, M, N]``
+    (planes added in order), and with ``ln = (weight, bias, eps)`` LayerNorm(x) as x3 planes, in
+    one kernel. Returns ``(x, planes or None)`` shaped like ``shape`` (default ``res.shape``)."""
+    S, M, N = part.shape
+    shape = tuple(shape if shape is not None else res.shape)
+    x = torch.empty(shape, dtype=torch.float32, device=part.device)
+    planes = torch.empty((3,) + shape, dtype=torch.bfloat16, device=part.device) if ln is not None else None
+    r2 = res2.reshape(-1, N).contiguous() if res2 is not None else None
+    res = res.contiguous()
+    _check(_L().nos_splitk_layernorm_f32(part.data_ptr(), S, bias.data_ptr(), res.data_ptr(),
+                                         r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+                                         x.data_ptr(), ln[0].data_ptr() if ln is not None else None,
+                                         ln[1].data_ptr() if ln is not None else None,
+                                         planes.data_ptr() if planes is not None else None, M, N,
+                                         float(ln[2]) if ln is not None else 0.0, layernorm_wgs(M), _stream()))
+    return x, planes
+
+
+def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, residual: torch.Tensor,
+                          residual2: Optional[torch.Tensor] = None, ln=None):
+    """``x = a @ w^T + b + residual (+ residual2)`` and (``ln = (weight, bias, eps)``) the x3 planes of
+    LayerNorm(x); on the GPU the faster of the fused-epilogue GEMM + LayerNorm and the split-K
+    partial GEMM + combine-and-LayerNorm kernel (``gemm.linear_residual_ln_x3``)."""
+    if not _use_hip(a3) or a3.shape[-1] % 32 or residual.shape[-1] not in (384, 768):
+        x = linear_x3(a3, w, b, residual=residual, residual2=residual2)
+        return x, (layernorm_x3(x, ln[0], ln[1], ln[2]) if ln is not None else None)
+    from .gemm import linear_residual_ln_x3 as fused
+    return fused(a3, w, b, residual, residual2, ln)
 
 
 def layernorm_x3(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
