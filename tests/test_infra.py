@@ -237,3 +237,52 @@ def test_shipped_x3_tuned_table_names_known_tiles():
         n = int(key.split("_")[1][1:])
         assert n % G.X3_TILES[v["tile"]][1] == 0, key
     assert os.path.basename(G._TUNED_PATH) == "x3_tuned.json"
+
+
+def test_split_candidates_and_partials_contract():
+    # split-K partial configs: only LDS-DMA tiles whose width divides N and whose stage depth
+    # divides K, each split covering at least two stages
+    from walkai_nos_amd.ops import gemm as G
+    c = G.split_candidates(384, 1536)
+    assert c and all(cfg in G.SPLIT_TILES and sp in G.SPLIT_COUNTS for cfg, sp in c)
+    for cfg, sp in c:
+        bm, bn, _, kind = G.X3_TILES[cfg]
+        bk = 64 if kind.endswith("64") else 32
+        assert 384 % bn == 0 and 1536 // bk >= 2 * sp
+    assert all(sp == 2 for _, sp in G.split_candidates(384, 128))  # 4 stages of 32: at most 2 splits
+    assert G.split_candidates(100, 1536) == []                     # no tile width divides 100
+
+
+def test_linear_residual_ln_x3_cpu_reference():
+    # the CPU path of the fused projection/fc2 step equals linear + residual + LayerNorm
+    import torch
+    import torch.nn.functional as F
+    from walkai_nos_amd.ops import kernels as K
+    torch.manual_seed(2)
+    a = torch.randn(2, 5, 64)
+    w, b = torch.randn(32, 64) * 0.1, torch.randn(32)
+    r, r2 = torch.randn(2, 5, 32), torch.randn(1, 5, 32)
+    lw, lb = torch.randn(32), torch.randn(32)
+    x, h3 = K.linear_residual_ln_x3(K.split3(a), w, b, r, residual2=r2, ln=(lw, lb, 1e-6))
+    ref = F.linear(a, w, b) + r + r2
+    assert torch.allclose(x, ref, atol=1e-5)
+    assert torch.allclose(h3.float().sum(0) if h3.dtype != torch.float32 else h3.sum(0),
+                          F.layer_norm(ref, (32,), lw, lb, 1e-6), atol=1e-4)
+    x2, none = K.linear_residual_ln_x3(K.split3(a), w, b, r)
+    assert none is None and torch.allclose(x2, F.linear(a, w, b) + r, atol=1e-5)
+
+
+def test_detection_token_template_cached_per_parameter_version():
+    import torch
+    from walkai_nos_amd.models.workload.yolos import YolosConfig, YolosSmall
+    m = YolosSmall(YolosConfig(num_layers=1))
+    t1 = m.token_template((64, 64))
+    assert m.token_template((64, 64)) is t1
+    nd = m.c.num_detection_tokens
+    pe, _ = m.position_embeddings((64, 64))
+    assert torch.equal(t1[:, :1], m.cls_token + pe[:, :1]) and torch.equal(t1[:, -nd:], m.det_tokens + pe[:, -nd:])
+    assert t1[:, 1:-nd].abs().max().item() == 0
+    with torch.no_grad():
+        m.det_tokens.add_(1.0)
+    t2 = m.token_template((64, 64))
+    assert t2 is not t1 and torch.equal(t2[:, -nd:], m.det_tokens + pe[:, -nd:])
