@@ -286,3 +286,14 @@ def test_detection_token_template_cached_per_parameter_version():
         m.det_tokens.add_(1.0)
     t2 = m.token_template((64, 64))
     assert t2 is not t1 and torch.equal(t2[:, -nd:], m.det_tokens + pe[:, -nd:])
+
+
+def test_density_phase_control_plane_at_four_gpus():
+    # saturation through the real control plane: 8 CPX pods per GPU, 16 CU-mask pods per GPU on
+    # average (first-fit may leave the last GPU lighter: the minimum is reported beside the mean)
+    from walkai_nos_amd.bench_core import BenchConfig, density_phase
+    d = density_phase(BenchConfig(gpus=4), None)
+    assert d["xcp"]["pods_per_gpu"] == 8 and d["xcp"]["pending"] == 0 and d["xcp"]["pods_per_node"] == 32
+    for v in ("cumask", "cumask_shared"):
+        assert d[v]["pending"] == 0 and d[v]["pods_per_node"] == 64 and d[v]["pods_per_gpu"] == 16
+        assert 0 < d[v]["pods_per_gpu_min"] <= 16
