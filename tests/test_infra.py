@@ -165,8 +165,8 @@ def test_bench_control_plane_and_slice_masks():
     for _ in range(20):
         nb.control_step()
         served += len(nb.my_pods())
-        dark += 1 if nb.outage.get(0, 0) > 0 else 0
-        if nb.outage.get(0, 0) > 0:
+        dark += 1 if nb.dark(0) else 0
+        if nb.dark(0):
             assert nb.my_pods() == []  # a flipped GPU serves nothing during its outage
         nb.end_step()
     assert served > 0 and max(nb.util_samples) > 0

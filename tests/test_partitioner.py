@@ -262,3 +262,17 @@ def test_pack_gain_drain_rotates_an_underused_gpu():
     assert changed["n0"].gpus[0].target == {"spx_nps1": 1}
     assert plan_cluster_pack(models, pending, params=PackParams(drain_gain_after=0)) == {}
     assert plan_cluster_pack(models, [({"spx_nps1": 1}, 100.0)], params=PackParams()) == {}
+
+
+def test_multi_node_cluster_bench_tracks_flips_per_node():
+    # the bench's control plane + outage model on a 3-node cluster (nos-simulate --nodes): every
+    # flip darkens its own (node, GPU); the planner keeps the cluster allocated
+    from walkai_nos_amd.bench_core import BenchConfig, NodeBench
+    nb = NodeBench(BenchConfig(gpus=2, nodes=3, flip_cost_s=1.0, quantum_s=0.5, seed=3), gpu_data_plane=False)
+    assert len(nb.cluster.nodes) == 3
+    for _ in range(40):
+        nb.control_step()
+        assert all(isinstance(k, tuple) and k[0] in nb.cluster.nodes for k in nb.outage)
+        nb.end_step()
+    assert nb.flips > 0 and max(nb.util_samples) > 50.0
+    assert nb.gpu_steps == 40 * 6

@@ -93,6 +93,7 @@ class BenchConfig:
     policy: str = "pack"                 # planner policy (pack | fifo | batch | simulate)
     density: bool = True
     emulation: str = EMULATION           # compute-partition emulation: pinned | spread
+    nodes: int = 1                       # cluster nodes of `gpus` GPUs (control-plane simulation only)
 
     @property
     def outage_steps(self) -> int:
@@ -108,7 +109,7 @@ class ChurnProcess:
         self.seq = 0
         mean_frac = sum((1.0 / COMPUTE_MODES[p.split("_")[0]]) * w for p, w in MIX)
         mean_life = (cfg.lifetime[0] + cfg.lifetime[1]) / 2
-        self.rate = cfg.offered_load * cfg.gpus / (mean_frac * mean_life)
+        self.rate = cfg.offered_load * cfg.gpus * cfg.nodes / (mean_frac * mean_life)
 
     def arrivals(self) -> List[str]:
         # Poisson(rate) via inversion, seeded
@@ -420,22 +421,24 @@ class HwBusySampler:
 
 
 class NodeBench:
-    """The simulated node (real control plane) + the outage model + this rank's data plane."""
+    """The simulated node (real control plane) + the outage model + this rank's data plane. With
+    ``cfg.nodes > 1`` (control plane only, ``nos-simulate --nodes``) the cluster has that many nodes
+    and the outage model tracks every (node, GPU); the data plane serves the first node."""
 
     def __init__(self, cfg: BenchConfig, barrier_factory=None, gpu_data_plane: bool = True,
                  verify=None):
         from .sim.cluster import SimCluster
 
         self.cfg = cfg
-        self.cluster = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
-        self.sn = next(iter(self.cluster.nodes.values()))
+        self.cluster = SimCluster(n_nodes=cfg.nodes, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
+        self.sn = next(iter(self.cluster.nodes.values()))  # the node this rank's data plane serves
         if barrier_factory is not None or verify is not None:
             self._set_commit(barrier_factory, verify)
         self.churn = ChurnProcess(cfg)
         self.cluster.run(30)  # node initialisation (SPX everywhere)
         self.live: Dict[str, int] = {}          # running pod -> served quanta left
-        self.outage: Dict[int, int] = {}        # GPU -> quanta of outage left
-        self._flips_seen = len(self.sn.smi.set_calls)
+        self.outage: Dict[Tuple[str, int], int] = {}  # (node, GPU) -> quanta of outage left
+        self._flips_seen = {n: len(sn.smi.set_calls) for n, sn in self.cluster.nodes.items()}
         self.reset_stats()
         self.data: Optional[DataPlane] = DataPlane(cfg) if gpu_data_plane else None
 
@@ -451,6 +454,10 @@ class NodeBench:
         self.host_s = {"control": 0.0, "serve": 0.0}
         self.empty_steps = 0
 
+    def dark(self, gpu: int, node: Optional[str] = None) -> bool:
+        """Is ``gpu`` of ``node`` (default: this rank's node) in a flip outage this quantum?"""
+        return self.outage.get((node or self.sn.name, gpu), 0) > 0
+
     def _set_commit(self, factory: Any, verify: Any) -> None:
         for c in self.sn.manager.controllers:
             actuator = getattr(c.reconciler, "__self__", None)
@@ -463,8 +470,9 @@ class NodeBench:
     # -- control plane + outage model ------------------------------------------------------
     def pod_gpus(self) -> Dict[str, set]:
         out: Dict[str, set] = {}
-        for (_, name), devs in self.sn.kubelet.allocations.items():
-            out[name] = {self.sn.smi.resolve(d).gpu_index for _, d in devs}
+        for sn in self.cluster.nodes.values():
+            for (_, name), devs in sn.kubelet.allocations.items():
+                out[name] = {(sn.name, sn.smi.resolve(d).gpu_index) for _, d in devs}
         return out
 
     def control_step(self) -> None:
@@ -483,23 +491,24 @@ class NodeBench:
             c.submit({f"amd.com/{prof}": 1}, name=f"p{self.churn.seq}")
             self.churn.seq += 1
         c.run(60)
-        calls = self.sn.smi.set_calls
-        for kind, gpu, _ in calls[self._flips_seen:]:
-            self.flips += 1
-            for g in (range(self.cfg.gpus) if gpu is None else (gpu,)):
-                self.outage[g] = max(self.outage.get(g, 0), self.cfg.outage_steps)
-        self._flips_seen = len(calls)
+        for nname, sn in c.nodes.items():
+            calls = sn.smi.set_calls
+            for kind, gpu, _ in calls[self._flips_seen[nname]:]:
+                self.flips += 1
+                for g in (range(self.cfg.gpus) if gpu is None else (gpu,)):
+                    self.outage[(nname, g)] = max(self.outage.get((nname, g), 0), self.cfg.outage_steps)
+            self._flips_seen[nname] = len(calls)
         for p in c.running_pods():
             n = ko.name(p)
             if n not in self.live:
                 self.live[n] = self.churn.lifetime()
         frac = c.gpu_allocated_fraction()
-        dark = {g for g, k in self.outage.items() if k > 0}
+        dark = {k for k, v in self.outage.items() if v > 0}
         self.raw_util_samples.append(100.0 * sum(frac.values()) / max(1, len(frac)))
-        self.util_samples.append(100.0 * sum(v for (_, g), v in frac.items() if g not in dark) / max(1, len(frac)))
+        self.util_samples.append(100.0 * sum(v for k, v in frac.items() if k not in dark) / max(1, len(frac)))
         self.pods_samples.append(len(c.running_pods()))
         self.pending_samples.append(len(c.pending_pods()))
-        self.gpu_steps += self.cfg.gpus
+        self.gpu_steps += self.cfg.gpus * self.cfg.nodes
         self.outage_gpu_steps += len(dark)
         self.host_s["control"] += time.perf_counter() - t0
 
@@ -511,7 +520,7 @@ class NodeBench:
 
     def my_pods(self) -> List[Tuple[str, int]]:
         """(profile, partition index) of the pods served on this rank's GPU this quantum."""
-        if self.outage.get(self.cfg.rank, 0) > 0:
+        if self.dark(self.cfg.rank):
             return []
         out = []
         for devs in self.sn.kubelet.allocations.values():
@@ -733,7 +742,7 @@ def control_only(cfg: BenchConfig, steps: int) -> Dict[str, Any]:
     for _ in range(steps):
         nb.control_step()
         for g in range(cfg.gpus):
-            if nb.outage.get(g, 0) > 0:
+            if nb.dark(g):
                 continue
             for devs in nb.sn.kubelet.allocations.values():
                 for r, d in devs:

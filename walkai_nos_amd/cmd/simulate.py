@@ -17,7 +17,8 @@ from ..bench_core import BenchConfig, NodeBench
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="nos control-plane simulation")
-    ap.add_argument("--gpus", type=int, default=8)
+    ap.add_argument("--gpus", type=int, default=8, help="GPUs per node")
+    ap.add_argument("--nodes", type=int, default=1, help="cluster nodes (the planner plans across all of them)")
     ap.add_argument("--epochs", type=int, default=50)
     ap.add_argument("--load", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1234)
@@ -28,8 +29,9 @@ def main(argv=None) -> int:
     ap.add_argument("--quiet", action="store_true", help="print only the summary line")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
-    nb = NodeBench(BenchConfig(gpus=args.gpus, offered_load=args.load, seed=args.seed, policy=args.policy,
-                               flip_cost_s=args.flip_cost, quantum_s=args.quantum), gpu_data_plane=False)
+    nb = NodeBench(BenchConfig(gpus=args.gpus, nodes=args.nodes, offered_load=args.load, seed=args.seed,
+                               policy=args.policy, flip_cost_s=args.flip_cost, quantum_s=args.quantum),
+                   gpu_data_plane=False)
     for _ in range(args.preroll):
         nb.control_step()
         nb.end_step()
@@ -42,9 +44,9 @@ def main(argv=None) -> int:
             print(json.dumps({"epoch": e, "util_pct": round(nb.util_samples[-1], 2), "pods": nb.pods_samples[-1],
                               "pending": nb.pending_samples[-1]}))
     dt = time.perf_counter() - t0
-    print(json.dumps({"policy": args.policy, "gpus": args.gpus, "load": args.load,
+    print(json.dumps({"policy": args.policy, "nodes": args.nodes, "gpus_per_node": args.gpus, "load": args.load,
                       "mean_util_pct": round(sum(nb.util_samples) / len(nb.util_samples), 2),
-                      "mean_pods_per_node": round(sum(nb.pods_samples) / len(nb.pods_samples), 2),
+                      "mean_pods_per_node": round(sum(nb.pods_samples) / len(nb.pods_samples) / args.nodes, 2),
                       "pending_mean": round(sum(nb.pending_samples) / len(nb.pending_samples), 2),
                       "pending_max": max(nb.pending_samples), "flips": nb.flips, "flip_cost_s": args.flip_cost,
                       "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),

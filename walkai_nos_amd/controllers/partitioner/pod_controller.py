@@ -214,11 +214,29 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
     changed: Dict[str, NodeModel] = {}
     extra = {p: q for p, q in (incoming or {}).items() if q > 0}
     unserved: List[Tuple[Dict[str, int], float]] = []
+    names = sorted(current)
+
+    def best_free(m: NodeModel) -> Dict[str, int]:
+        """Most free partitions of each profile on one offered (non-draining) GPU of the node: a
+        single-GPU request can only fit where this covers it (the screen that keeps the pass from
+        trying — and failing — every GPU of every node for every pending pod at cluster scale)."""
+        out: Dict[str, int] = {}
+        for g in m.gpus:
+            if g.target is None:
+                for prof, q in g.free.items():
+                    if q > out.get(prof, 0):
+                        out[prof] = q
+        return out
+    free_of = {n: best_free(current[n]) for n in names}
     for req, age in pending:
         placed = False
-        for name in sorted(current):
+        for name in names:
+            bf = free_of[name]
+            if any(bf.get(prof, 0) < q for prof, q in req.items()):
+                continue
             try:
                 current[name].add_pod(req)
+                free_of[name] = best_free(current[name])
                 placed = True
                 break
             except ValueError:

@@ -179,11 +179,41 @@ class SimScheduler:
         pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
         node_objs = {n.name: self.api.get("Node", n.name) for n in self.nodes.values()}
         draining = {name: draining_gpus(o) for name, o in node_objs.items()}
+        # per pass: free-device counts per (node, resource), recomputed only for a node that just
+        # took a pod, and filter verdicts per (node, scheduling constraints) — pods of one shape share
+        # them (the pass was O(pods x nodes x devices) at 64 nodes)
+        free: Dict[Tuple[str, str], int] = {}
+        verdict: Dict[Tuple[str, str], bool] = {}
+
+        def fits(n: SimNode, reqs: Dict[str, int]) -> bool:
+            for r, q in reqs.items():
+                if not is_managed(r):
+                    continue
+                k = (n.name, r)
+                if k not in free:
+                    free[k] = len(n.kubelet.free_devices(r, draining[n.name]))
+                if free[k] < q:
+                    return False
+            return True
+
+        def passes(p: Dict[str, Any], shape: str, n: SimNode) -> bool:
+            k = (n.name, shape)
+            if k not in verdict:
+                verdict[k] = filter_node(p, node_objs[n.name])[0]
+            return verdict[k]
+        unplaceable = set()  # (shape, request) that fit no node in this pass: free devices only shrink
         for p in pods:
             reqs = res.compute_pod_request(p)
-            order = sorted(self.nodes.values(), key=lambda n: (-len(n.kubelet.allocations), n.name))
-            target = next((n for n in order if filter_node(p, node_objs[n.name])[0]
-                           and n.kubelet.can_fit(reqs, draining[n.name])), None)
+            spec = p["spec"]
+            shape = repr((spec.get("nodeSelector"), spec.get("tolerations"), spec.get("affinity"),
+                          spec.get("nodeName")))
+            rkey = (shape, tuple(sorted((r, q) for r, q in reqs.items() if is_managed(r))))
+            target = None
+            if rkey not in unplaceable:
+                order = sorted(self.nodes.values(), key=lambda n: (-len(n.kubelet.allocations), n.name))
+                target = next((n for n in order if passes(p, shape, n) and fits(n, reqs)), None)
+                if target is None:
+                    unplaceable.add(rkey)
             if target is None:
                 if not podutil.is_unschedulable(p):
                     st = {"conditions": [{"type": "PodScheduled", "status": "False", "reason": "Unschedulable",
@@ -200,6 +230,8 @@ class SimScheduler:
                 continue
             self.bound += 1
             self.on_bind(p, target.name, draining[target.name])
+            for k in [k for k in free if k[0] == target.name]:
+                del free[k]
         return Result()
 
 
