@@ -230,9 +230,13 @@ class YolosSmall(nn.Module):
         return self.cls_head(det), torch.sigmoid(self.box_head(det))
 
     def heads_fusable(self) -> bool:
+        """Both heads are 3-layer MLPs of one shape with rows of at most 384 (a multiple of 4) —
+        what the fused kernel stages in LDS (``csrc/head.hip``); otherwise the module path runs."""
         ch, bh = self.cls_head.layers, self.box_head.layers
+        d, hid = self.c.hidden_size, ch[0].weight.shape[0]
         return (len(ch) == 3 and len(bh) == 3 and ch[0].weight.shape == bh[0].weight.shape
-                and ch[1].weight.shape == bh[1].weight.shape)
+                and ch[1].weight.shape == bh[1].weight.shape and d <= 384 and hid <= 384
+                and d % 4 == 0 and hid % 4 == 0)
 
     def token_template(self, hw: Tuple[int, int]) -> torch.Tensor:
         """[1, T, D]: the class-token row + its position embedding, zero patch rows, the detection-token
