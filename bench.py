@@ -37,6 +37,9 @@ def main() -> int:
     ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod stream")
     ap.add_argument("--pod-streams", type=int, default=1,
                     help="concurrent request streams per pod (1 = one inference at a time, as the reference demo)")
+    ap.add_argument("--lane-cus", type=int, default=128,
+                    help="a partition pod wider than this many CUs runs one batch-1 request loop per disjoint "
+                         "run of this many CUs (0 = one loop per pod)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--emulation", default=None, choices=("pinned", "spread"),
                     help="compute-partition emulation on the SPX device (default: pinned; bench_core.EMULATION)")
@@ -65,7 +68,7 @@ def main() -> int:
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
                       preroll=args.preroll, quantum_s=args.quantum, flip_cost_s=args.flip_cost,
                       policy=args.policy, depth=args.depth, density=not args.no_density,
-                      pod_streams=args.pod_streams)
+                      pod_streams=args.pod_streams, lane_cus=args.lane_cus)
     if args.emulation:
         cfg.emulation = args.emulation
     res = run_bench(cfg)

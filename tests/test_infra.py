@@ -175,6 +175,20 @@ def test_bench_control_plane_and_slice_masks():
     assert BenchConfig(flip_cost_s=0.0).outage_steps == 0
 
 
+def test_request_lanes_split_a_partition_into_disjoint_xcd_balanced_runs():
+    from walkai_nos_amd.bench_core import lane_cu_runs, slice_cus
+    runs = lane_cu_runs(None, 128)  # a whole-GPU pod: two lanes of 128 CUs
+    assert [len(r) for r in runs] == [128, 128] and set(runs[0]).isdisjoint(runs[1])
+    assert sorted(runs[0] + runs[1]) == list(range(256))
+    assert all({c % 8 for c in r} == set(range(8)) for r in runs)  # 16 CUs on each XCD
+    dpx = slice_cus("dpx_nps1", 1, emulation="spread")
+    assert lane_cu_runs(dpx, 64) == [dpx[:64], dpx[64:]]
+    # no split: off, a partition not wider than a lane, or a lane that would unbalance the XCDs
+    assert lane_cu_runs(None, 0) == [None]
+    assert lane_cu_runs(dpx, 128) == [dpx]
+    assert lane_cu_runs(None, 100) == [None] and lane_cu_runs(None, 20) == [None]
+
+
 def test_split3_cpu_reconstructs_exactly():
     import torch
 

@@ -87,6 +87,8 @@ class BenchConfig:
     graphs: bool = True
     depth: int = 2                       # inferences in flight per pod stream
     pod_streams: int = 1                 # concurrent request streams per pod (1 = the reference demo's loop)
+    lane_cus: int = 128                  # >0: a partition pod wider than this serves on disjoint CU runs of
+                                         # this many CUs, one batch-1 request loop per run (0 = one loop)
     preroll: int = 60                    # control-plane-only steps before warmup (steady state)
     rank: int = 0
     world: int = 1
@@ -169,6 +171,19 @@ def slice_cus(profile: str, partition: int, total_cus: int = 256,
     return list(range(partition * per, (partition + 1) * per))
 
 
+def lane_cu_runs(cus: Optional[List[int]], lane_cus: int, total_cus: int = 256) -> List[Optional[List[int]]]:
+    """Split a partition's CUs into request lanes of ``lane_cus`` CUs each (disjoint, contiguous runs
+    of the partition's CU bits; bit i sits on XCD i mod 8, so a run of a multiple of 8 bits is
+    XCD-balanced).  A batch-1 YOLOS inference does not fill a whole MI355X — its attention tail,
+    LayerNorms and heads leave CUs idle — while two inferences on disjoint halves keep every CU
+    busy (profiles/kbench_r2_modes_final.json: SPX 370, DPX 418 inf/s per GPU).  ``lane_cus`` <= 0,
+    or a partition not wider than it, gives one lane on the whole partition."""
+    all_cus = list(range(total_cus)) if cus is None else list(cus)
+    if lane_cus <= 0 or len(all_cus) <= lane_cus or len(all_cus) % lane_cus or lane_cus % XCDS:
+        return [cus]
+    return [all_cus[i:i + lane_cus] for i in range(0, len(all_cus), lane_cus)]
+
+
 class _Lane:
     """One stream of a pod: a CU-masked HIP stream, an input, and the inference graph captured on it."""
 
@@ -177,6 +192,7 @@ class _Lane:
 
         from .models.workload.yolos import demo_input
         from .ops.probe import Stream
+        self.n_cus = 256 if cus is None else len(cus)
         self.hip_stream = Stream(device, cus)
         self.stream = self.hip_stream.torch_stream()
         with torch.cuda.stream(self.stream):
@@ -198,11 +214,12 @@ class _Lane:
 
 class Slot:
     """One partition (or CU-mask slice) of this rank's GPU: a model replica serving
-    ``cfg.pod_streams`` concurrent request streams (lanes), each a CU-masked stream with its own
-    input and captured graph; an inference is one HIP graph replay on the least-loaded lane."""
+    ``cfg.pod_streams`` concurrent request streams (lanes) per CU run (``lane_cu_runs``; one run
+    unless ``split`` and ``cfg.lane_cus``), each a CU-masked stream with its own input and captured
+    graph; an inference is one HIP graph replay on the least-loaded lane."""
 
     def __init__(self, cus: Optional[List[int]], device: int, cfg: BenchConfig, template: Any, seed: int = 0,
-                 pin: int = 0):
+                 pin: int = 0, split: bool = False):
         import copy
 
         import torch
@@ -210,7 +227,9 @@ class Slot:
         self.cus = cus
         self.pin = pin
         self.cfg = cfg
-        self.lanes = [_Lane(cus, device, cfg, seed + 1000 * i) for i in range(max(1, cfg.pod_streams))]
+        runs = lane_cu_runs(cus, cfg.lane_cus) if split and not pin else [cus]
+        self.lanes = [_Lane(run, device, cfg, seed + 1000 * i + 100 * j)
+                      for j, run in enumerate(runs) for i in range(max(1, cfg.pod_streams))]
         with torch.cuda.stream(self.lanes[0].stream):
             self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
         torch.cuda.synchronize()
@@ -236,9 +255,9 @@ class Slot:
         import torch
 
         from .ops import kernels as K
-        K.set_slice_cus(self.n_cus)
         K.set_slice_pin(self.pin)
         for lane in self.lanes:
+            K.set_slice_cus(lane.n_cus)
             with torch.no_grad(), torch.cuda.stream(lane.stream):
                 for _ in range(2):
                     lane.out = self.model(lane.x)
@@ -256,9 +275,9 @@ class Slot:
         import torch
 
         from .ops import kernels as K
-        K.set_slice_cus(self.n_cus)
-        K.set_slice_pin(self.pin)
         lane = min(self.lanes, key=lambda l: len(l.inflight))
+        K.set_slice_cus(lane.n_cus)
+        K.set_slice_pin(self.pin)
         with torch.no_grad(), torch.cuda.stream(lane.stream):
             if lane.graph is not None:
                 lane.graph.replay()
@@ -302,7 +321,8 @@ class DataPlane:
         for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
             for k in range(n):
                 self.slots[(prof, k)] = Slot(slice_cus(prof, k, emulation=cfg.emulation), self.device, cfg,
-                                             self.template, seed=k, pin=slice_pin(prof, k, cfg.emulation))
+                                             self.template, seed=k, pin=slice_pin(prof, k, cfg.emulation),
+                                             split=True)
         for s in self.slots.values():
             s.warm()
         torch.cuda.synchronize()
@@ -722,7 +742,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
                    "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
                    "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
-                   "pod_streams": cfg.pod_streams,
+                   "pod_streams": cfg.pod_streams, "lane_cus": cfg.lane_cus,
                    "partition_emulation": cfg.emulation,
                    "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
