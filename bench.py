@@ -41,7 +41,7 @@ def main() -> int:
                     help="a partition pod wider than this many CUs runs one batch-1 request loop per disjoint "
                          "run of this many CUs (0 = one loop per pod)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
-    ap.add_argument("--emulation", default=None, choices=("pinned", "spread"),
+    ap.add_argument("--emulation", default=None, choices=("pinned", "spread", "landing"),
                     help="compute-partition emulation on the SPX device (default: pinned; bench_core.EMULATION)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()

@@ -111,3 +111,22 @@ def test_pinned_model_matches_unpinned_on_a_cpx_slice(K):
     # the autotuner may pick different tiles per key, so compare to fp32-accurate tolerance
     for r, g in zip(ref, got):
         assert (r - g).abs().max().item() < 1e-4
+
+
+def test_landing_mask_places_work_on_own_xcd_and_one_cu_elsewhere(K):
+    """The "landing" emulation's CU mask (bench_core.slice_cus): a CPX partition's workgroups run on
+    31 CUs of one XCD, and on exactly one (the landing) CU of every other XCD; under the partition's
+    pin (census above) the latter are the exit-only ones."""
+    import collections
+
+    from walkai_nos_amd.bench_core import slice_cus, slice_pin
+    from walkai_nos_amd.ops import probe
+    cus = slice_cus("cpx_nps1", 3, emulation="landing")
+    assert len(cus) == 31 + 7 and slice_pin("cpx_nps1", 3, "landing") == 1 << 3
+    with probe.Stream(0, cus) as s:
+        placements = probe.census(0, s, n_wg=2048, spin=200)
+    per_xcc = collections.defaultdict(set)
+    for p in placements:
+        per_xcc[p["xcc"]].add((p["se"], p["sh"], p["cu"]))
+    sizes = sorted(len(v) for v in per_xcc.values())
+    assert sizes == [1] * 7 + [31], dict((x, len(v)) for x, v in per_xcc.items())

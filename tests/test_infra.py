@@ -158,6 +158,21 @@ def test_bench_control_plane_and_slice_masks():
     assert slice_pin("dpx_nps1", 1, "pinned") == 0xF0 and len(slice_cus("dpx_nps1", 1, emulation="pinned")) == 128
     masks = [slice_pin("cpx_nps1", k, "pinned") for k in range(8)]
     assert sum(masks) == 0xFF and len(set(masks)) == 8
+    # landing emulation: own XCDs minus the landing CU (index 31 in each XCD), plus the landing CU of
+    # every other XCD; no two partitions share a working CU, and no partition works on a landing CU
+    from walkai_nos_amd.bench_core import working_cus
+    for prof, n in (("cpx_nps1", 8), ("qpx_nps1", 4), ("dpx_nps1", 2)):
+        work = []
+        for k in range(n):
+            cus, pin = slice_cus(prof, k, emulation="landing"), slice_pin(prof, k, "landing")
+            assert pin == slice_pin(prof, k, "pinned")
+            own = [c for c in cus if (pin >> (c % 8)) & 1]
+            assert working_cus(cus, pin) == len(own) == 31 * (8 // n)
+            assert all(c // 8 != 31 for c in own)
+            assert sorted(c % 8 for c in cus if not (pin >> (c % 8)) & 1) == [x for x in range(8) if not (pin >> x) & 1]
+            assert all(c // 8 == 31 for c in cus if not (pin >> (c % 8)) & 1)
+            work += own
+        assert len(work) == len(set(work)) == 248
     a, b = ChurnProcess(BenchConfig(seed=7)), ChurnProcess(BenchConfig(seed=7))
     assert [a.arrivals() for _ in range(20)] == [b.arrivals() for _ in range(20)]
     nb = NodeBench(BenchConfig(gpus=2, flip_cost_s=1.0, quantum_s=0.5), gpu_data_plane=False)

@@ -56,7 +56,7 @@ def main() -> int:
     ap.add_argument("--only", choices=("all", "attn", "gemm", "model", "modes"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
-    ap.add_argument("--emulation", default="pinned", choices=("pinned", "spread"),
+    ap.add_argument("--emulation", default="pinned", choices=("pinned", "spread", "landing"),
                     help="modes: compute-partition emulation (bench_core.EMULATION)")
     a = ap.parse_args()
     torch.manual_seed(0)

@@ -70,6 +70,20 @@ CUMASK_DENSITY = {"cumask": (("32cu.24gb", 6), ("8gb", 10)), "cumask_shared": ((
 #: (profiles/partition_emulation_r2.json). ``NOS_PARTITION_EMULATION`` overrides.
 EMULATION = os.environ.get("NOS_PARTITION_EMULATION", "spread")
 XCDS = 8
+#: emulations whose partitions run on their own XCDs (kernels pinned with ``csrc/pin.h``). "landing":
+#: pinned, and the CU mask gives a partition its own XCDs minus one CU per XCD plus that reserved
+#: "landing" CU on every other XCD, so the launch's exit-only workgroups never wait for a slot behind
+#: the other partitions' real work (the coupling that made "pinned" slow); 31 of 32 CUs per XCD work.
+PINNED_EMULATIONS = ("pinned", "landing")
+
+
+def working_cus(cus: Optional[List[int]], pin: int, total_cus: int = 256) -> int:
+    """CUs that run a slice's real work: every masked CU, or under a pin only those on its XCDs."""
+    if cus is None:
+        return total_cus
+    if not pin:
+        return len(cus)
+    return sum(1 for c in cus if (pin >> (c % XCDS)) & 1)
 
 
 @dataclass
@@ -151,7 +165,7 @@ def partition_xcds(profile: str, partition: int) -> Optional[List[int]]:
 def slice_pin(profile: str, partition: int, emulation: Optional[str] = None) -> int:
     """XCD mask the partition's kernels are pinned to (0 = unpinned: SPX, or the spread emulation)."""
     xcds = partition_xcds(profile, partition)
-    if xcds is None or (emulation or EMULATION) != "pinned":
+    if xcds is None or (emulation or EMULATION) not in PINNED_EMULATIONS:
         return 0
     return sum(1 << x for x in xcds)
 
@@ -164,9 +178,18 @@ def slice_cus(profile: str, partition: int, total_cus: int = 256,
     n = COMPUTE_MODES[profile.split("_")[0]]
     if n == 1:
         return None
-    if (emulation or EMULATION) == "pinned":
+    emulation = emulation or EMULATION
+    if emulation == "pinned":
         xcds = set(partition_xcds(profile, partition))
         return [i for i in range(total_cus) if i % XCDS in xcds]
+    if emulation == "landing":
+        # own XCDs minus their landing CU, plus the landing CU of every other XCD: a pinned launch's
+        # exit-only workgroups on a foreign XCD can only be placed on that XCD's landing CU, which
+        # no partition runs real work on (an all-zero XCD in a CU mask would enable the whole XCD)
+        xcds = set(partition_xcds(profile, partition))
+        land = total_cus // XCDS - 1
+        return [i for i in range(total_cus)
+                if (i % XCDS in xcds and i // XCDS != land) or (i % XCDS not in xcds and i // XCDS == land)]
     per = total_cus // n
     return list(range(partition * per, (partition + 1) * per))
 
@@ -187,12 +210,12 @@ def lane_cu_runs(cus: Optional[List[int]], lane_cus: int, total_cus: int = 256) 
 class _Lane:
     """One stream of a pod: a CU-masked HIP stream, an input, and the inference graph captured on it."""
 
-    def __init__(self, cus: Optional[List[int]], device: int, cfg: "BenchConfig", seed: int):
+    def __init__(self, cus: Optional[List[int]], device: int, cfg: "BenchConfig", seed: int, pin: int = 0):
         import torch
 
         from .models.workload.yolos import demo_input
         from .ops.probe import Stream
-        self.n_cus = 256 if cus is None else len(cus)
+        self.n_cus = working_cus(cus, pin)
         self.hip_stream = Stream(device, cus)
         self.stream = self.hip_stream.torch_stream()
         with torch.cuda.stream(self.stream):
@@ -228,7 +251,7 @@ class Slot:
         self.pin = pin
         self.cfg = cfg
         runs = lane_cu_runs(cus, cfg.lane_cus) if split and not pin else [cus]
-        self.lanes = [_Lane(run, device, cfg, seed + 1000 * i + 100 * j)
+        self.lanes = [_Lane(run, device, cfg, seed + 1000 * i + 100 * j, pin)
                       for j, run in enumerate(runs) for i in range(max(1, cfg.pod_streams))]
         with torch.cuda.stream(self.lanes[0].stream):
             self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
@@ -236,7 +259,7 @@ class Slot:
 
     @property
     def n_cus(self) -> int:
-        return 256 if self.cus is None else len(self.cus)
+        return working_cus(self.cus, self.pin)
 
     @property
     def stream(self):
