@@ -774,13 +774,14 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
 def control_only(cfg: BenchConfig, steps: int) -> Dict[str, Any]:
     """The control plane + outage model alone (no GPU): allocation, flips and queue over ``steps``
     quanta after the preroll.  ``inf_per_s_model`` prices the served partition-quanta with the
-    measured per-mode full-GPU rates (``profiles/kbench_r1_s5_modes.json``)."""
+    measured per-mode full-GPU rates (``profiles/partition_emulation_landing_r2.json`` spread modes;
+    SPX as two 128-CU request lanes, ``profiles/bench_r2_request_lanes.json``)."""
     nb = NodeBench(cfg, gpu_data_plane=False)
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
     nb.reset_stats()
-    rate = {"spx": 356.0, "dpx": 402.1, "qpx": 414.5, "cpx": 359.1}
+    rate = {"spx": 413.9, "dpx": 414.9, "qpx": 416.2, "cpx": 359.0}
     served = 0.0
     for _ in range(steps):
         nb.control_step()
