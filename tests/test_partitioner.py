@@ -276,3 +276,19 @@ def test_multi_node_cluster_bench_tracks_flips_per_node():
         nb.end_step()
     assert nb.flips > 0 and max(nb.util_samples) > 50.0
     assert nb.gpu_steps == 40 * 6
+
+
+def test_pack_reserve_break_flips_a_reserved_idle_spx_gpu_for_a_full_queue():
+    # GPU 0 serves a whole-GPU pod, GPU 1 is an idle SPX GPU held as the whole-GPU reserve
+    # (spx_demand 2): a DPX queue of 1.5 GPUs leaves it reserved, 2 GPUs' worth takes it
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, new_node_model, plan_cluster_pack
+    node = xnode("n0", gpus=2, anns={"nos.nebuly.com/status-gpu-0-spx_nps1-used": "1",
+                                     "nos.nebuly.com/status-gpu-1-spx_nps1-free": "1"})
+    models = {"n0": new_node_model("xcp", node)}
+    three = [({"dpx_nps1": 1}, 60.0)] * 3
+    assert plan_cluster_pack(models, three, params=PackParams(), spx_demand=2.0) == {}
+    changed = plan_cluster_pack(models, three + [({"dpx_nps1": 1}, 60.0)], params=PackParams(), spx_demand=2.0)
+    assert changed["n0"].gpus[1].geometry() == {"dpx_nps1": 2}
+    assert changed["n0"].gpus[0].geometry() == {"spx_nps1": 1}  # the busy GPU is never touched
+    # without a reserve the idle GPU flips for a half-GPU queue already (min_fill)
+    assert "n0" in plan_cluster_pack(models, three[:1], params=PackParams(), spx_demand=0.0)

@@ -72,12 +72,14 @@ class GpuPartitionerConfig(ManagerConfig):
     planningPolicy: str = "pack"
     scoring: str = "fraction"
     #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
-    #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds
+    #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds,
+    #: reserveBreakFill
     packing: Dict[str, Any] = field(default_factory=dict)
 
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
                     "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
-                    "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after"}
+                    "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after",
+                    "reserveBreakFill": "reserve_break_fill"}
 
     def pack_params(self) -> Any:
         from ..controllers.partitioner.pod_controller import PackParams

@@ -171,6 +171,7 @@ class PackParams:
     reserve_decay: float = 0.9      # EMA decay of the whole-GPU demand estimate per planning pass
     drain_gain: float = 0.625       # drain a busy GPU whose used fraction is this much below the
     drain_gain_after: float = 600.0  # ... fill a profile waiting this long would give it (0 = off)
+    reserve_break_fill: float = 2.0  # a queue filling this many GPUs takes a reserved idle SPX GPU
 
 
 def _mode_of(gpu: Any) -> Optional[str]:
@@ -197,7 +198,9 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
        profile's oldest pod has waited ``starve_after`` (so nothing starves): otherwise it keeps
        its mode (hysteresis — an idle GPU left as it is costs nothing, a flip costs an outage);
     4. on multi-GPU nodes idle SPX GPUs are kept as a reserve sized from the recent whole-GPU demand
-       (``spx_demand``, an EMA in GPUs), unless a starving pod needs them;
+       (``spx_demand``, an EMA in GPUs), unless a starving pod needs them or a profile's queue
+       would fill ``reserve_break_fill`` GPUs (an idle GPU held against a whole GPU of waiting work
+       serves nothing; the EMA lags behind whole-GPU pods that have already left);
     5. a profile whose oldest pod has waited ``drain_after``, and whose queue would fill
        ``drain_backlog`` GPUs (a drain idles partitions, so it must buy a full GPU of work), or whose
        oldest pod has waited ``drain_gain_after`` and whose queue would fill a GPU at least
@@ -286,7 +289,8 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         if best is None:
             continue
         (starving, _, _), p = best
-        if cur is not None and cur.startswith("spx") and spx_kept < reserve and not starving:
+        if (cur is not None and cur.startswith("spx") and spx_kept < reserve and not starving
+                and demand[p] + 1e-9 < params.reserve_break_fill):
             spx_kept += 1
             continue  # keep this idle SPX GPU for the whole-GPU demand
         trial = g.clone()
