@@ -253,6 +253,7 @@ class Slot:
         runs = lane_cu_runs(cus, cfg.lane_cus) if split and not pin else [cus]
         self.lanes = [_Lane(run, device, cfg, seed + 1000 * i + 100 * j, pin)
                       for j, run in enumerate(runs) for i in range(max(1, cfg.pod_streams))]
+        self.latency_ms: List[float] = []  # GPU time of each completed inference (its lane's events)
         with torch.cuda.stream(self.lanes[0].stream):
             self.model = copy.deepcopy(template).to(f"cuda:{device}").eval()
         torch.cuda.synchronize()
@@ -302,23 +303,30 @@ class Slot:
         K.set_slice_cus(lane.n_cus)
         K.set_slice_pin(self.pin)
         with torch.no_grad(), torch.cuda.stream(lane.stream):
+            st = torch.cuda.Event(enable_timing=True)
+            st.record(lane.stream)  # runs when the lane's previous inference has finished
             if lane.graph is not None:
                 lane.graph.replay()
             else:
                 lane.out = self.model(lane.x)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=True)
             ev.record(lane.stream)
-        lane.inflight.append(ev)
+        lane.inflight.append((st, ev))
+
+    def _done(self, st, ev) -> None:
+        self.latency_ms.append(st.elapsed_time(ev))
 
     def reap(self) -> None:
         for lane in self.lanes:
-            while lane.inflight and lane.inflight[0].query():
-                lane.inflight.popleft()
+            while lane.inflight and lane.inflight[0][1].query():
+                self._done(*lane.inflight.popleft())
 
     def drain(self) -> None:
         for lane in self.lanes:
             while lane.inflight:
-                lane.inflight.popleft().synchronize()
+                st, ev = lane.inflight.popleft()
+                ev.synchronize()
+                self._done(st, ev)
 
     def close(self) -> None:
         for lane in self.lanes:
@@ -661,6 +669,25 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
 
 
 # -- driver ---------------------------------------------------------------------------------
+def inference_latency(data: Optional[DataPlane]) -> Dict[str, Dict[str, float]]:
+    """GPU time of the inferences completed on this rank since the slots' lists were cleared, per
+    compute mode: each inference is timed between events around its graph replay on its lane, so
+    under concurrency (other partitions, the pod's other lane) it is the latency a request sees
+    once the lane starts it."""
+    out: Dict[str, Dict[str, float]] = {}
+    if data is None:
+        return out
+    by_mode: Dict[str, List[float]] = collections.defaultdict(list)
+    for key, s in data.slots.items():
+        by_mode[str(key[0]).split("_")[0]] += s.latency_ms
+    for mode, v in sorted(by_mode.items()):
+        if v:
+            v = sorted(v)
+            out[mode] = {"n": len(v), "mean": round(sum(v) / len(v), 3), "p50": round(v[len(v) // 2], 3),
+                         "p99": round(v[min(len(v) - 1, int(0.99 * len(v)))], 3)}
+    return out
+
+
 def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     import torch
     import torch.distributed as dist
@@ -688,6 +715,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     if distributed:
         dist.barrier()
     nb.reset_stats()
+    for s in nb.data.slots.values():
+        s.latency_ms.clear()
     busy = HwBusySampler(nb.data.device)
     busy.start()
     t0 = time.perf_counter()
@@ -713,6 +742,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         hw_busy = round(float(s[1].item()) / cfg.world, 1) if hw_busy is not None else None
     else:
         total_inf = float(nb.inferences)
+    latency = inference_latency(nb.data)
     density = density_phase(cfg, nb.data) if cfg.density else {}
     nb.close()
     value = total_inf / elapsed
@@ -744,6 +774,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "hw_busy_source": "amd-smi gfx_activity, sampled every 100 ms in the timed window" if hw_busy is not None
         else f"unavailable: {busy.error}",
         "hw_power_clock": busy.power_summary(),
+        "inference_latency_ms": latency,
         "pods_per_node": round(pods, 2),
         "pods_per_gpu": round(pods / cfg.gpus, 2),
         "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},
