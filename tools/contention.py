@@ -98,7 +98,8 @@ def wall(graphs_streams, reps=3):
 
 
 GEMM_KEYS = {  # op -> (M, N, K, epilogue flags, output flags) as gemm_x3 keys its tuning cache
-    "qkv": (T, 3 * D, D, 1, 2), "proj": (T, D, D, 1 | 4, 1), "fc1": (T, FF, D, 1 | 2, 2), "fc2": (T, D, FF, 1 | 4, 1)}
+    "qkv": (T, 3 * D, D, 1, 2), "proj": (T, D, D, 1 | 4, 1), "fc1": (T, FF, D, 1 | 2, 2), "fc2": (T, D, FF, 1 | 4, 1),
+    "qkv_f32": (T, 3 * D, D, 1, 1), "fc1_f32": (T, FF, D, 1 | 2, 1)}
 
 
 def emit_table(path, results, sl, cus):
