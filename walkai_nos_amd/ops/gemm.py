@@ -441,7 +441,7 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
 
 # ---- split-K partials + combine-and-LayerNorm --------------------------------------------------
 #: LDS-DMA tiles offered to the split-K partial path (32x32 MFMA and 16x16 MFMA, 4 and 8 waves)
-SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32)
+SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36)
 SPLIT_COUNTS = (2, 3, 4)
 
 
