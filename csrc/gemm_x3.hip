@@ -898,7 +898,8 @@ int nos_gemm_x3_num_configs() { return 38; }
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
 // cfg: 0 = 64x64 S3 (4 waves), 1 = 64x64 S2, 2 = 128x128 S3 (8 waves), 3 = 64x128 S3, 4 = 128x64 S3;
-// 64-deep stages: 5 = 64x64 S2, 6 = 64x32 S2 (2 waves), 7 = 128x64 S2 (8 waves); 8/9 = 128x64, 64x128 S4.
+// 64-deep stages: 5 = 64x64 S2, 6 = 64x32 S2 (2 waves), 7 = 128x64 S2 (8 waves); 8/9 = 128x64, 64x128 S4;
+// 10 = 256x128 S2 (8 waves of 64x64).
 int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, const float* bias, const float* R,
                            const float* R2, int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi,
                            int cfg, int grid, void* stream) {
@@ -926,6 +927,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
     case 7: return launch_s<128, 64, 4, 2, 2, 64>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 8: return launch_s<128, 64, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     case 9: return launch_s<64, 128, 2, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
+    case 10: return launch_s<256, 128, 4, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, grid, s);
     default:
       g_err = "gemm_x3s: unknown config";
       return -1;

@@ -223,7 +223,7 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
             104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
-            108: (128, 64, 4, "p"), 109: (64, 128, 4, "p")}
+            108: (128, 64, 4, "p"), 109: (64, 128, 4, "p"), 110: (256, 128, 2, "p8")}
 #: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
 X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
 #: resident workgroups per CU (LDS- or VGPR-limited)
@@ -231,7 +231,7 @@ X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 1
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
                    18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 3, 28: 2, 29: 1, 30: 4, 31: 4,
                    32: 1, 33: 2, 34: 1, 35: 1, 36: 1, 37: 1,
-                   100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1}
+                   100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1, 110: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int, int], int] = {}
 _x3_bound = False
 
