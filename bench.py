@@ -37,7 +37,7 @@ def main() -> int:
     ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod stream")
     ap.add_argument("--pod-streams", type=int, default=1,
                     help="concurrent request streams per pod (1 = one inference at a time, as the reference demo)")
-    ap.add_argument("--lane-cus", type=int, default=128,
+    ap.add_argument("--lane-cus", type=int, default=64,
                     help="a partition pod wider than this many CUs runs one batch-1 request loop per disjoint "
                          "run of this many CUs (0 = one loop per pod)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")

@@ -101,7 +101,7 @@ class BenchConfig:
     graphs: bool = True
     depth: int = 2                       # inferences in flight per pod stream
     pod_streams: int = 1                 # concurrent request streams per pod (1 = the reference demo's loop)
-    lane_cus: int = 128                  # >0: a partition pod wider than this serves on disjoint CU runs of
+    lane_cus: int = 64                   # >0: a partition pod wider than this serves on disjoint CU runs of
                                          # this many CUs, one batch-1 request loop per run (0 = one loop)
     preroll: int = 60                    # control-plane-only steps before warmup (steady state)
     rank: int = 0
