@@ -326,3 +326,18 @@ def test_density_phase_control_plane_at_four_gpus():
     for v in ("cumask", "cumask_shared"):
         assert d[v]["pending"] == 0 and d[v]["pods_per_node"] == 64 and d[v]["pods_per_gpu"] == 16
         assert 0 < d[v]["pods_per_gpu_min"] <= 16
+
+
+def test_inference_latency_summary_per_mode():
+    from types import SimpleNamespace
+
+    from walkai_nos_amd.bench_core import inference_latency
+    slots = {("spx_nps1", 0): SimpleNamespace(latency_ms=[9.0, 9.5, 9.2]),
+             ("cpx_nps1", 3): SimpleNamespace(latency_ms=[20.0]),
+             ("cpx_nps1", 4): SimpleNamespace(latency_ms=[22.0]),
+             ("dpx_nps1", 1): SimpleNamespace(latency_ms=[])}
+    out = inference_latency(SimpleNamespace(slots=slots))
+    assert set(out) == {"spx", "cpx"}  # modes that completed nothing are left out
+    assert out["spx"]["n"] == 3 and out["spx"]["p50"] == 9.2 and abs(out["spx"]["mean"] - 9.233) < 1e-3
+    assert out["cpx"] == {"n": 2, "mean": 21.0, "p50": 22.0, "p99": 22.0}
+    assert inference_latency(None) == {}
