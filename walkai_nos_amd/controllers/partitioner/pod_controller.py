@@ -168,7 +168,7 @@ class PackParams:
     drain_after: float = 7200.0     # seconds: a pod waiting this long makes a busy GPU drain for it
     drain_backlog: float = 2.0      # ... if its profile's queue would fill at least this many GPUs
     spx_reserve: bool = True        # keep idle SPX GPUs for recent whole-GPU demand (multi-GPU)
-    reserve_decay: float = 0.9      # EMA decay of the whole-GPU demand estimate per planning pass
+    reserve_decay: float = 0.5      # EMA decay of the whole-GPU demand estimate per planning pass
     drain_gain: float = 0.625       # drain a busy GPU whose used fraction is this much below the
     drain_gain_after: float = 600.0  # ... fill a profile waiting this long would give it (0 = off)
     reserve_break_fill: float = 2.0  # a queue filling this many GPUs takes a reserved idle SPX GPU
