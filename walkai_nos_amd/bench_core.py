@@ -198,9 +198,10 @@ def lane_cu_runs(cus: Optional[List[int]], lane_cus: int, total_cus: int = 256) 
     """Split a partition's CUs into request lanes of ``lane_cus`` CUs each (disjoint, contiguous runs
     of the partition's CU bits; bit i sits on XCD i mod 8, so a run of a multiple of 8 bits is
     XCD-balanced).  A batch-1 YOLOS inference does not fill a whole MI355X — its attention tail,
-    LayerNorms and heads leave CUs idle — while two inferences on disjoint halves keep every CU
-    busy (profiles/kbench_r2_modes_final.json: SPX 370, DPX 418 inf/s per GPU).  ``lane_cus`` <= 0,
-    or a partition not wider than it, gives one lane on the whole partition."""
+    LayerNorms and heads leave CUs idle — while inferences on disjoint quarters keep every CU busy
+    (profiles/kbench_r2_modes_tiles256.json: one loop on the whole GPU 358, four 64-CU partitions
+    440 inf/s per GPU; profiles/bench_r2_lane_width_ab.json: 64- vs 128-CU lanes).  ``lane_cus``
+    <= 0, or a partition not wider than it, gives one lane on the whole partition."""
     all_cus = list(range(total_cus)) if cus is None else list(cus)
     if lane_cus <= 0 or len(all_cus) <= lane_cus or len(all_cus) % lane_cus or lane_cus % XCDS:
         return [cus]
