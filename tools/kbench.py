@@ -56,6 +56,8 @@ def main() -> int:
     ap.add_argument("--only", choices=("all", "attn", "gemm", "model", "modes"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
+    ap.add_argument("--lane-cus", type=int, default=0,
+                    help="modes: serve partitions wider than this as request lanes of this many CUs (the bench's --lane-cus)")
     ap.add_argument("--emulation", default="pinned", choices=("pinned", "spread", "landing"),
                     help="modes: compute-partition emulation (bench_core.EMULATION)")
     a = ap.parse_args()
@@ -141,7 +143,7 @@ def modes_bench(a) -> int:
     running 8 x fraction inferences per round; inferences/s per GPU."""
     from walkai_nos_amd.bench_core import BenchConfig, Slot, slice_pin
     from walkai_nos_amd.models.workload.yolos import YolosSmall
-    cfg = BenchConfig()
+    cfg = BenchConfig(lane_cus=a.lane_cus)
     template = YolosSmall()
     results = []
     for prof, n in (("spx_nps1", 1), ("dpx_nps1", 2), ("qpx_nps1", 4), ("cpx_nps1", 8)):
@@ -149,7 +151,7 @@ def modes_bench(a) -> int:
             continue
         n = min(n, a.partitions) if a.partitions else n
         slots = [Slot(slice_cus(prof, k, emulation=a.emulation), 0, cfg, template, seed=k,
-                      pin=slice_pin(prof, k, a.emulation)) for k in range(n)]
+                      pin=slice_pin(prof, k, a.emulation), split=a.lane_cus > 0) for k in range(n)]
         for sl in slots:
             sl.warm()
         torch.cuda.synchronize()
@@ -167,7 +169,8 @@ def modes_bench(a) -> int:
                 sl.drain()
         dt = time.perf_counter() - t0
         busy = sampler.stop()
-        r = {"mode": prof, "emulation": a.emulation, "partitions": n, "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
+        r = {"mode": prof, "emulation": a.emulation, "partitions": n, "lanes_per_partition": len(slots[0].lanes),
+             "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
              "ms_per_round": round(1000 * dt / rounds, 2), "hw_busy_pct": busy, **sampler.power_summary()}
         print(json.dumps(r), flush=True)
         results.append(r)
