@@ -443,6 +443,11 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
 #: LDS-DMA tiles offered to the split-K partial path (32x32 MFMA and 16x16 MFMA, 4 and 8 waves)
 SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36)
 SPLIT_COUNTS = (2, 3, 4)
+#: smallest slice that times split-K against the fused path: on 32-CU (CPX) slices the isolated
+#: timing picks split-K, but with all eight partitions busy the fused path serves 2% more
+#: (383.0 vs 375.6 inf/s per GPU; 64-CU request lanes keep split-K: 438.6 vs 430.7,
+#: profiles/splitk_slice_ab_r2.json)
+SPLITK_MIN_CUS = 64
 
 
 def gemm_x3_partials(a3: torch.Tensor, w: torch.Tensor, cfg: int, splits: int,
@@ -506,8 +511,12 @@ def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, re
         part = gemm_x3_partials(a3, w, cfg, sp)
         return K.splitk_layernorm(part, b, residual, residual2, ln, lead)
     if choice is None:
-        if torch.cuda.is_current_stream_capturing() or os.environ.get("NOS_SPLITK", "1") == "0":
-            choice = ("unsplit",)  # NOS_SPLITK=0: the fused-epilogue GEMM + LayerNorm only (A/B runs)
+        if torch.cuda.is_current_stream_capturing() or os.environ.get("NOS_SPLITK", "1") == "0" \
+                or K.slice_cus() < SPLITK_MIN_CUS:
+            # NOS_SPLITK=0: the fused-epilogue GEMM + LayerNorm only (A/B runs); slices below
+            # SPLITK_MIN_CUS have enough tiles per CU already, and there the partial planes' extra
+            # write + read costs more than it balances under sibling partitions
+            choice = ("unsplit",)
         else:
             stream = torch.cuda.current_stream()
             times = {("unsplit",): _gpu_time(unsplit, stream)}
