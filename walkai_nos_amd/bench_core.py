@@ -806,14 +806,14 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
 def control_only(cfg: BenchConfig, steps: int) -> Dict[str, Any]:
     """The control plane + outage model alone (no GPU): allocation, flips and queue over ``steps``
     quanta after the preroll.  ``inf_per_s_model`` prices the served partition-quanta with the
-    measured per-mode full-GPU rates (``profiles/kbench_r2_modes_lanes64.json``)."""
+    measured per-mode full-GPU rates (``profiles/kbench_r2_modes_lanes64_splitk_rule.json``)."""
     nb = NodeBench(cfg, gpu_data_plane=False)
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
     nb.reset_stats()
-    # SPX and DPX pods serve as 64-CU request lanes (cfg.lane_cus); profiles/kbench_r2_modes_lanes64.json
-    rate = {"spx": 435.5, "dpx": 444.7, "qpx": 445.2, "cpx": 370.5}
+    # SPX and DPX pods serve as 64-CU request lanes (cfg.lane_cus); profiles/kbench_r2_modes_lanes64_splitk_rule.json
+    rate = {"spx": 437.9, "dpx": 445.2, "qpx": 438.9, "cpx": 389.2}
     served = 0.0
     for _ in range(steps):
         nb.control_step()
