@@ -341,3 +341,32 @@ def test_inference_latency_summary_per_mode():
     assert out["spx"]["n"] == 3 and out["spx"]["p50"] == 9.2 and abs(out["spx"]["mean"] - 9.233) < 1e-3
     assert out["cpx"] == {"n": 2, "mean": 21.0, "p50": 22.0, "p99": 22.0}
     assert inference_latency(None) == {}
+
+
+def test_splitk_is_only_timed_on_slices_of_64_cus_or_more(monkeypatch):
+    # below SPLITK_MIN_CUS the fused-epilogue path is taken without timing split-K (it loses under
+    # sibling partitions, profiles/splitk_slice_ab_r2.json); from 64 CUs both pipelines are timed
+    import torch
+
+    from walkai_nos_amd.ops import gemm as G
+    from walkai_nos_amd.ops import kernels as K
+    timed = []
+    monkeypatch.setattr(G, "gemm_x3", lambda a3, w, b, residual=None, residual2=None: residual.clone())
+    monkeypatch.setattr(K, "layernorm_x3", lambda x, w, b, eps: torch.zeros((3,) + tuple(x.shape)))
+    monkeypatch.setattr(G, "_gpu_time", lambda fn, stream: timed.append(fn) or 1.0)
+    monkeypatch.setattr(G, "split_candidates", lambda N, Kd: [])
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda: None)
+    G._fused_cache.clear()
+    a3, w, b = torch.zeros(3, 8, 64), torch.zeros(32, 64), torch.zeros(32)
+    r = torch.zeros(8, 32)
+    K.set_slice_cus(32)
+    try:
+        x, h3 = G.linear_residual_ln_x3(a3, w, b, r, ln=(b, b, 1e-12))
+        assert not timed and x.shape == r.shape
+        K.set_slice_cus(64)
+        G.linear_residual_ln_x3(a3, w, b, r, ln=(b, b, 1e-12))
+        assert len(timed) == 1  # the fused path timed (no split candidates offered here)
+    finally:
+        K.set_slice_cus(None)
+        G._fused_cache.clear()
