@@ -42,7 +42,7 @@ def main() -> int:
                          "run of this many CUs (0 = one loop per pod)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--emulation", default=None, choices=("pinned", "spread", "landing"),
-                    help="compute-partition emulation on the SPX device (default: pinned; bench_core.EMULATION)")
+                    help="compute-partition emulation on the SPX device (default: spread; bench_core.EMULATION)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
