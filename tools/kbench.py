@@ -58,7 +58,7 @@ def main() -> int:
     ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
     ap.add_argument("--lane-cus", type=int, default=0,
                     help="modes: serve partitions wider than this as request lanes of this many CUs (the bench's --lane-cus)")
-    ap.add_argument("--emulation", default="pinned", choices=("pinned", "spread", "landing"),
+    ap.add_argument("--emulation", default="spread", choices=("pinned", "spread", "landing"),
                     help="modes: compute-partition emulation (bench_core.EMULATION)")
     a = ap.parse_args()
     torch.manual_seed(0)
