@@ -166,10 +166,20 @@ int nos_barrier_allreduce_all(void* handle, const int32_t* votes, int32_t* resul
     if (int rc = hip_check(hipMemcpyAsync(b->bufs[i], &votes[i], sizeof(int32_t), hipMemcpyHostToDevice, b->streams[i]), "h2d")) return rc;
   }
   if (int rc = nccl_check(ncclGroupStart(), "ncclGroupStart")) return rc;
-  for (int i = 0; i < b->n; ++i) {
-    if (int rc = nccl_check(ncclAllReduce(b->bufs[i], b->bufs[i], 1, ncclInt32, ncclSum, b->comms[i], b->streams[i]), "ncclAllReduce")) return rc;
+  // every enqueue error is recorded, but the group is always closed: returning from inside an
+  // open group leaves the calling thread's group depth at 1, and the next NCCL call of this
+  // process would silently join a group that is never launched
+  int enq = 0;
+  for (int i = 0; i < b->n && !enq; ++i)
+    enq = nccl_check(ncclAllReduce(b->bufs[i], b->bufs[i], 1, ncclInt32, ncclSum, b->comms[i], b->streams[i]),
+                     "ncclAllReduce");
+  std::string enq_err = g_err;
+  int end = nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  if (enq) {
+    g_err = enq_err;
+    return enq;
   }
-  if (int rc = nccl_check(ncclGroupEnd(), "ncclGroupEnd")) return rc;
+  if (end) return end;
   for (int i = 0; i < b->n; ++i) {
     if (int rc = hip_check(hipSetDevice(b->devs[i]), "hipSetDevice")) return rc;
     if (int rc = hip_check(hipStreamSynchronize(b->streams[i]), "hipStreamSynchronize")) return rc;

@@ -263,3 +263,49 @@ def test_local_barrier_timeout_closes_the_generation():
     assert b.vote(True) is True            # a fresh round, not completed by the stale vote
     t.join()
     assert late == [True]
+
+
+def test_veto_when_a_gpu_drops_out_of_the_map_after_the_switch():
+    """a flip after which a GPU is missing from the re-enumerated map has no device to
+    carry its veto, and the GPUs behind it are renumbered: the commit must still be vetoed and the
+    rollback must address the surviving GPUs by BDF, not by (shifted) index."""
+    e = Env(n_gpus=3)
+    real = e.smi._set_compute_partition
+
+    def switch_and_lose(proc, mode):
+        real(proc, mode)
+        g = e.smi._gpu_of(proc)
+        if g.index == 1 and mode == "CPX":
+            e.smi._gpus.remove(g)          # GPU 1 did not come back from the mode change
+    e.smi._set_compute_partition = switch_and_lose
+    e.spec({"nos.nebuly.com/spec-gpu-0-dpx_nps1": "2", "nos.nebuly.com/spec-gpu-1-cpx_nps1": "8",
+            api.ANNOTATION_PARTITIONING_PLAN: "5"})
+    e.reporter.reconcile(Request("node-a"))
+    with pytest.raises(GpuError):
+        e.actuator.reconcile(Request("node-a"))
+    votes = e.actuator.last_votes
+    assert votes and not any(votes)
+    assert e.shared.last_commit == "failed"
+    m = e.smi.device_map()
+    assert [g.bdf for g in m.gpus] == ["0000:05:00.0", "0000:25:00.0"]
+    # GPU 0 rolled back to SPX; the old GPU 2 (now index 1) was never flipped
+    assert e.smi.get_compute_partition(0) == "SPX" and e.smi.get_compute_partition(1) == "SPX"
+    assert sorted(e.smi.set_calls) == [("compute", 0, "DPX"), ("compute", 0, "SPX"), ("compute", 1, "CPX")]
+
+
+def test_native_helper_vetoes_a_device_count_mismatch():
+    """The native commit-barrier helper (csrc/gpuhelper.cpp) vetoes when the HIP devices it sees
+    differ from the device map — more votes than the map has, or (on this CPU host) no device at
+    all — and still prints its one JSON line with the phase timings."""
+    from walkai_nos_amd.ops import native
+    from walkai_nos_amd.parallel.spawned import NATIVE_HELPER, SpawnedNodeBarrier, run_helper
+    if not native.available(NATIVE_HELPER):
+        pytest.skip("native helper not built")
+    res = run_helper(["barrier", "--votes", "1,1,1", "--expect", "2"], 60.0, program=native.lib_path(NATIVE_HELPER))
+    assert res["native"] is True and res["n"] == 3 and res["sum"] == 0 and "error" in res
+    assert set(res) >= {"hip_init_ms", "comm_init_ms", "allreduce_ms", "destroy_ms", "total_ms"}
+    b = SpawnedNodeBarrier(2, backend="rccl", native=True)
+    assert not b.vote_all([True, True, True])          # more votes than the map's devices
+    assert b.last.get("error") and b.last["wall_ms"] > 0
+    if not native.gpu_present():
+        assert not b.vote_all([True, True])            # no GPU here: the helper sees 0 != 2

@@ -123,3 +123,96 @@ def test_kubeconfig_client_certificate_and_inline_data():
             yaml.safe_dump(cfg, f)
         c = from_kubeconfig(path)
         assert c.token == "s3cr3t" and c.cert_file is None
+
+
+class _DelayedPodEvents:
+    """An API server whose Pod watch events are held back until ``flush()`` (a slow watch)."""
+
+    def __init__(self, api):
+        self.api = api
+        self.held = []
+
+    def __getattr__(self, name):
+        return getattr(self.api, name)
+
+    def watch(self, kind, handler, replay=True, on_synced=None):
+        if kind != "Pod":
+            return self.api.watch(kind, handler, replay, on_synced)
+        live = [False]
+
+        def hold(t, o, old):
+            if live[0]:
+                self.held.append((handler, t, o, old))
+            else:
+                handler(t, o, old)
+        cancel = self.api.watch(kind, hold, replay, on_synced)
+        live[0] = True
+        return cancel
+
+    def flush(self):
+        held, self.held = self.held, []
+        for h, t, o, old in held:
+            h(t, o, old)
+
+
+def test_bind_is_assumed_until_the_watch_confirms_it():
+    """a scheduling cycle that starts before the binding's watch event must still see
+    the pod on its node, or it places the next pod on capacity that pod already holds."""
+    from walkai_nos_amd.quota.scheduler import NosScheduler
+    api = InMemoryAPIServer()
+    api.create(ko.new_node("n1", allocatable={"cpu": "8", "memory": "8Gi", "pods": "10", "amd.com/spx_nps1": "1"}))
+    for name in ("a", "b"):
+        api.create(ko.new_pod(name, "default", requests={"amd.com/spx_nps1": 1}, scheduler_name="nos-scheduler"))
+    slow = _DelayedPodEvents(api)
+    c = CachedClient(slow, kinds=("Node", "Pod"))
+    s = NosScheduler(c)
+    s.reconcile(NosScheduler.KEY)                       # binds a; its watch event is held back
+    assert ko.pod_node_name(api.get("Pod", "a", "default")) == "n1"
+    assert ko.pod_node_name(c.get("Pod", "a", "default")) == "n1"   # assumed in the cache
+    # an older event (e.g. a status patch made before the binding) must not un-assume it
+    stale = c.get("Pod", "a", "default")
+    stale["spec"].pop("nodeName")
+    c.informer("Pod").apply("MODIFIED", stale)
+    assert ko.pod_node_name(c.get("Pod", "a", "default")) == "n1"
+    s.reconcile(NosScheduler.KEY)                       # a new cycle before the watch caught up
+    assert not ko.pod_node_name(api.get("Pod", "b", "default"))     # n1's only GPU is taken
+    slow.flush()
+    assert ko.pod_node_name(c.get("Pod", "a", "default")) == "n1"
+    assert c.informer("Pod").assumed == {}
+
+
+class _ListRacesWatch:
+    """Watch replays p1, then p1 is deleted before the informer could have listed again; a LIST
+    issued now would return the stale view that still holds p1."""
+
+    def __init__(self):
+        self.api = backing()
+        self.lists = 0
+
+    def __getattr__(self, name):
+        return getattr(self.api, name)
+
+    def list(self, kind, *a, **kw):
+        self.lists += 1
+        stale = self.api.list(kind, *a, **kw)
+        return stale
+
+    def watch(self, kind, handler, replay=True, on_synced=None):
+        snapshot = self.api.list(kind)
+        for o in snapshot:
+            handler("ADDED", o, None)
+        if kind == "Pod":
+            gone = self.api.get("Pod", "p1", "default")
+            handler("DELETED", gone, gone)              # arrives on the watch before "synced"
+        if on_synced is not None:
+            on_synced()
+        return lambda: None
+
+
+def test_informer_syncs_from_its_watch_without_a_second_list():
+    """no second LIST after the watch's own replay, so a DELETED that arrives in between
+    can never be undone by a stale ADDED (a zombie pod the planner would keep planning for)."""
+    api = _ListRacesWatch()
+    c = CachedClient(api, kinds=("Pod",))
+    assert c.list("Pod") == []
+    assert api.lists == 0

@@ -3,8 +3,8 @@
 * the native amd-smi device map (physical GPU <-> logical partitions, HIP ordinals, render nodes)
   and a timed re-enumeration (the step every flip pays);
 * the spawned commit-barrier helper: wall time of a vote including process spawn, HIP init and
-  ncclCommInitAll over every logical device, and its own init / all-reduce split (the agent pays
-  this per commit because a flip changes the device set);
+  ncclCommInitAll over every logical device, and its own phase split (the agent pays this per
+  commit because a flip changes the device set) — native executable vs the Python helper;
 * the spawned probe round on every logical device;
 * amd-smi power / clock / activity at rest.
 
@@ -36,14 +36,32 @@ def main() -> int:
     out["power_clock_idle"] = smi.power_clock(0)
     out["process_count"] = smi.process_count(0)
     n = len(m.devices)
-    votes = []
-    for ok in (True, True, False):
-        b = SpawnedNodeBarrier(n, backend="rccl")
-        t0 = time.perf_counter()
-        res = b.vote_all([ok] * n)
-        votes.append({"votes_ok": ok, "result": res, "wall_ms": round(1e3 * (time.perf_counter() - t0), 1),
-                      "helper": b.last})
-    out["commit_barrier"] = votes
+    # the commit barrier per helper flavour: native executable with the init tunables (the agent's
+    # default), native with RCCL's default init, and the round-2 Python helper; a first call on a
+    # fresh box pays cold file-cache costs, so every flavour runs 4 times (1 vetoed)
+    flavours = {"native_tuned": ({}, True), "native_rccl_defaults": ({"NOS_BARRIER_KEEP_NCCL_ENV": "1"}, True),
+                "python": ({}, False)}
+    out["commit_barrier"] = {}
+    for name, (env, native) in flavours.items():
+        votes = []
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            for ok in (True, True, True, False):
+                b = SpawnedNodeBarrier(n, backend="rccl", native=native)
+                t0 = time.perf_counter()
+                res = b.vote_all([ok] * n)
+                votes.append({"votes_ok": ok, "result": res, "wall_ms": round(1e3 * (time.perf_counter() - t0), 1),
+                              "helper": b.last})
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+        walls = sorted(v["wall_ms"] for v in votes[1:])
+        out["commit_barrier"][name] = {"calls": votes, "wall_ms_warm_median": walls[len(walls) // 2],
+                                       "correct": [v["result"] for v in votes] == [True, True, True, False]}
     t0 = time.perf_counter()
     targets = [(d.hip_id, None, f"gpu{d.gpu_index}.p{d.partition_index}") for d in m.devices]
     out["probe_round"] = {"results": spawned_probe_round(targets), "wall_s": round(time.perf_counter() - t0, 2)}

@@ -78,6 +78,7 @@ class Actuator:
         self.applied_plans = 0
         self.last_votes: List[bool] = []
         self._vote_devices: List[Any] = []
+        self._gpus_before: Dict[int, str] = {}
 
     def reconcile(self, req: Request) -> Result:
         if not self.shared.at_least_one_report_since_last_apply():
@@ -151,6 +152,7 @@ class Actuator:
         except Exception as e:  # noqa: BLE001 - no durable record, no flip
             REGISTRY.apply_errors.labels(node=self.node_name, op="journal").inc()
             return GpuError(f"unable to journal plan {plan_id!r} before applying it: {e}")
+        self._gpus_before = self._physical_gpus()
         helpers = self.shared.helpers
         gate = helpers.held() if hasattr(helpers, "held") else contextlib.nullcontext()
         with gate:  # no helper may start between the quiesce and the last switch
@@ -253,6 +255,20 @@ class Actuator:
                 votes.append(ok)
             return votes
         m = dm_fn()
+        devices = sorted(m.devices, key=lambda d: (d.hip_id, d.gpu_index, d.partition_index))
+        self._vote_devices = devices
+        # the physical GPUs must come back as they were: a GPU whose partitions all vanished from the
+        # re-enumerated map has no device to carry its veto, and build_device_map numbers GPUs by
+        # position in the sorted BDF list, so every GPU after it is renumbered and the per-GPU
+        # checks below would look at the wrong hardware. Every device votes no (the barrier still
+        # runs: on a multi-rank node every rank must take part in the all-reduce).
+        before = getattr(self, "_gpus_before", None)
+        after = {g.index: g.bdf.lower() for g in m.gpus}
+        missing = [g for g in target if not m.partitions_of(g)]
+        if (before and after != before) or missing:
+            log.error("device map after the flip does not match the node: GPUs before %s, after %s, "
+                      "target GPUs without partitions %s", before, after, missing)
+            return [False] * max(1, len(devices))
         gpu_ok: Dict[int, bool] = {}
         for g, p in target.items():
             parts = m.partitions_of(g)
@@ -261,15 +277,33 @@ class Actuator:
             if ok and self.verify is not None:
                 ok = bool(self.verify(g, p))
             gpu_ok[g] = ok
-        devices = sorted(m.devices, key=lambda d: (d.hip_id, d.gpu_index, d.partition_index))
-        self._vote_devices = devices
         return [gpu_ok.get(d.gpu_index, True) for d in devices]
 
+    def _physical_gpus(self) -> Dict[int, str]:
+        """GPU index -> BDF of the current device map ({} without one)."""
+        dm_fn = getattr(self.pc, "device_map", None)
+        if dm_fn is None:
+            return {}
+        try:
+            return {g.index: g.bdf.lower() for g in dm_fn().gpus}
+        except GpuError as e:
+            log.warning("device map unavailable before the flip: %s", e)
+            return {}
+
     def _rollback(self, flipped: List[Tuple[int, Optional[str]]]) -> None:
+        """Flip the GPUs of this plan back, addressed by BDF: if a GPU dropped out of the map the
+        others were renumbered, and index ``g`` may now be a different card."""
         log.info("rolling back %d GPU mode change(s)", len(flipped))
+        now = {bdf: i for i, bdf in self._physical_gpus().items()}
         for g, prev in reversed(flipped):
             if prev is None:
                 continue
+            bdf = self._gpus_before.get(g)
+            if bdf is not None and now:
+                if bdf not in now:
+                    log.error("unable to roll back GPU %d (%s) to %s: it is gone from the device map", g, bdf, prev)
+                    continue
+                g = now[bdf]
             try:
                 self.pc.set_profile(g, prev)
             except GpuError as e:

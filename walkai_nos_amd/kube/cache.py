@@ -53,27 +53,38 @@ class Informer:
         self.synced = threading.Event()
         self.lock = threading.RLock()
         self.events = 0
+        self.assumed: Dict[Tuple[str, str], str] = {}  # pods bound by us, not yet confirmed by the watch
         self._stop: Optional[Callable[[], None]] = None
 
     def start(self) -> None:
         def on_event(t: str, o: Obj, old: Optional[Obj]) -> None:
             self.apply(t, o)
-        # the REST watch thread lists first (every object arrives as ADDED), then streams
-        self._stop = self.api.watch(self.kind, on_event, replay=True)
-        # a LIST of our own marks the store as complete for readers
-        for o in self.api.list(self.kind):
-            self.apply("ADDED", o)
-        self.synced.set()
+        # the watch lists first (every object arrives as ADDED), then streams; the store is complete
+        # for readers once that first LIST has been applied — signalled from the watch's own thread,
+        # in order with its events. A second LIST of our own would race the stream: a DELETED
+        # delivered between that LIST's response and applying it would be undone by a stale ADDED,
+        # and nothing would ever remove the zombie.
+        self._stop = self.api.watch(self.kind, on_event, replay=True, on_synced=self.synced.set)
 
     def apply(self, t: str, o: Obj) -> None:
         k = (ko.namespace(o), ko.name(o))
         with self.lock:
             old = self.store.get(k)
             if t == "DELETED":
+                self.assumed.pop(k, None)
                 if old is None:
                     return
                 self.store.pop(k, None)
             else:
+                node = self.assumed.get(k)
+                if node is not None:
+                    if ko.pod_node_name(o):
+                        self.assumed.pop(k, None)  # the watch confirmed the binding
+                    else:
+                        # an event older than the binding: keep the pod assumed on its node
+                        o = _copy.deepcopy(o)
+                        o.setdefault("spec", {})["nodeName"] = node
+                        ko.set_condition(o, "PodScheduled", "True", "", "")
                 if old is not None and _rv(o) and _rv(old) > _rv(o):
                     return  # a stale event (e.g. the watch replaying what a write-through already stored)
                 if old is not None and old == o:
@@ -171,7 +182,21 @@ class CachedClient:
         self.api.delete(kind, name, namespace)
 
     def bind(self, pod_name: str, namespace: str, node_name: str) -> Obj:
-        return self.api.bind(pod_name, namespace, node_name)
+        """POST pods/binding, then *assume* the binding in the cache (kube-scheduler's assumed
+        pods): the API answers a Binding with a Status, not the pod, and until the watch delivers
+        the bound pod a scheduling cycle reading the cache would still see it Pending and unbound —
+        and place the next pod on capacity this one already holds. The assumed copy keeps the
+        cached resourceVersion, so the watch's MODIFIED (a newer version) replaces it."""
+        out = self.api.bind(pod_name, namespace, node_name)
+        inf = self._informers.get("Pod")
+        if inf is not None:
+            with inf.lock:
+                inf.assumed[(namespace, pod_name)] = node_name
+                cur = inf.store.get((namespace, pod_name))
+                assumed = _copy.deepcopy(cur) if cur is not None and not ko.pod_node_name(cur) else None
+            if assumed is not None:
+                inf.apply("MODIFIED", assumed)
+        return out
 
     def watch(self, kind: str, handler: Handler, replay: bool = True) -> Callable[[], None]:
         inf = self.informer(kind)

@@ -95,12 +95,15 @@ class InMemoryAPIServer:
         self.revision = 0
 
     # ---- watch ------------------------------------------------------------------------
-    def watch(self, kind: str, handler: Handler, replay: bool = True) -> Callable[[], None]:
+    def watch(self, kind: str, handler: Handler, replay: bool = True,
+              on_synced: Optional[Callable[[], None]] = None) -> Callable[[], None]:
         with self._lock:
             self._handlers.setdefault(kind, []).append(handler)
             existing = [fast_copy(o) for o in self._by_kind.get(kind, {}).values()] if replay else []
         for o in existing:
             handler("ADDED", o, None)
+        if on_synced is not None:
+            on_synced()
 
         def cancel() -> None:
             with self._lock:

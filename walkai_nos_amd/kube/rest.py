@@ -151,8 +151,14 @@ class RESTClient:
                 "target": {"apiVersion": "v1", "kind": "Node", "name": node_name}}
         return self._req("POST", self._path("Pod", pod_name, namespace, "binding"), body)
 
-    def watch(self, kind: str, handler: Callable[[str, Obj, Optional[Obj]], None], replay: bool = True) -> Callable[[], None]:
+    def watch(self, kind: str, handler: Callable[[str, Obj, Optional[Obj]], None], replay: bool = True,
+              on_synced: Optional[Callable[[], None]] = None) -> Callable[[], None]:
+        """Stream ``kind`` to ``handler`` from a watch thread: LIST (replayed as ADDED when
+        ``replay``), then WATCH from the list's resourceVersion, re-listing on ``410 Gone``.
+        ``on_synced`` is called once, on the watch thread, right after the first LIST has been
+        delivered — the informer's "has synced", ordered with every later event of the stream."""
         stop = threading.Event()
+        synced_once = threading.Event()
         self._watchers.append(stop)
         cache: Dict[Tuple[str, str], Obj] = {}
 
@@ -177,6 +183,9 @@ class RESTClient:
                         for k in [k for k in cache if k not in seen]:
                             gone = cache.pop(k)
                             handler("DELETED", gone, gone)
+                        if on_synced is not None and not synced_once.is_set():
+                            synced_once.set()
+                            on_synced()
                     resp = self._req("GET", self._path(kind), query={"watch": "1", "resourceVersion": rv,
                                                                      "allowWatchBookmarks": "true"},
                                      stream=True, timeout=300)

@@ -38,6 +38,7 @@ class Target:
     flags: List[str] = field(default_factory=list)
     libs: List[str] = field(default_factory=list)
     headers: List[str] = field(default_factory=list)
+    executable: bool = False   # a program (spawned by the agents), not a shared library
 
     @property
     def out(self) -> str:
@@ -78,7 +79,8 @@ class Target:
 
     def command(self) -> List[str]:
         srcs = [os.path.join(CSRC, s) for s in self.sources]
-        common = ["-O3", "-std=c++17", "-fPIC", "-shared", f"-I{ROCM}/include", f"-I{CSRC}"]
+        common = ["-O3", "-std=c++17", "-fPIC"] + ([] if self.executable else ["-shared"]) + \
+            [f"-I{ROCM}/include", f"-I{CSRC}"]
         if self.compiler == "hipcc":
             cc = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-Wno-unused-result",
                   "-Wno-unused-value"]
@@ -95,6 +97,9 @@ TARGETS: Sequence[Target] = (
     Target("libnos_barrier.so", ["rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
            libs=["rccl", "amdhip64"]),
     Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip"], "hipcc"),
+    # the agent's commit-barrier helper as a native program: no interpreter start-up on the flip path
+    Target("nos-gpuhelper", ["gpuhelper.cpp", "rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
+           libs=["rccl", "amdhip64"], executable=True),
 )
 
 

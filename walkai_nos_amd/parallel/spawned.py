@@ -88,14 +88,28 @@ class HelperRegistry:
 DEFAULT_REGISTRY = HelperRegistry()
 
 
-def run_helper(args: Sequence[str], timeout: float = 180.0, registry: Optional[HelperRegistry] = None) -> Dict[str, Any]:
-    """Run ``python -m walkai_nos_amd.cmd.gpuhelper <args>`` and return its JSON line."""
+NATIVE_HELPER = "nos-gpuhelper"
+
+
+def native_helper() -> Optional[str]:
+    """Path of the native commit-barrier helper (``csrc/gpuhelper.cpp``), when it is built and not
+    disabled with ``NOS_NATIVE_HELPER=0``."""
+    from ..ops import native
+    if os.environ.get("NOS_NATIVE_HELPER", "1") == "0" or not native.available(NATIVE_HELPER):
+        return None
+    return native.lib_path(NATIVE_HELPER)
+
+
+def run_helper(args: Sequence[str], timeout: float = 180.0, registry: Optional[HelperRegistry] = None,
+               program: Optional[str] = None) -> Dict[str, Any]:
+    """Run the helper — ``program`` (a native executable) or ``python -m walkai_nos_amd.cmd.gpuhelper``
+    — with ``args`` and return its JSON line."""
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     reg = registry or DEFAULT_REGISTRY
-    p = reg.spawn([sys.executable, "-m", "walkai_nos_amd.cmd.gpuhelper", *args], timeout, cwd=ROOT, env=env,
-                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cmd = [program, *args] if program else [sys.executable, "-m", "walkai_nos_amd.cmd.gpuhelper", *args]
+    p = reg.spawn(cmd, timeout, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     try:
         out, err = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
@@ -115,14 +129,18 @@ class SpawnedNodeBarrier(CommitBarrier):
 
     One vote per logical device of the re-enumerated device map (HIP ordinal order); the helper
     must see exactly that many HIP devices, so a partition that did not come up is a veto even if
-    every vote was 1."""
+    every vote was 1.  The RCCL backend runs the native ``nos-gpuhelper`` when it is built (no
+    interpreter start-up on the flip path), else the Python helper."""
 
     def __init__(self, n_devices: int, backend: str = "rccl", timeout: float = 180.0,
-                 registry: Optional[HelperRegistry] = None):
+                 registry: Optional[HelperRegistry] = None, native: Optional[bool] = None):
         self.n = n_devices
         self.backend = backend
         self.timeout = timeout
         self.registry = registry
+        self.program = native_helper() if backend == "rccl" and native is not False else None
+        if native and self.program is None:
+            raise RuntimeError(f"native helper {NATIVE_HELPER} is not built")
         self.last: Dict[str, Any] = {}
 
     def vote_all(self, votes: Sequence[bool]) -> bool:
@@ -130,12 +148,13 @@ class SpawnedNodeBarrier(CommitBarrier):
         t0 = time.perf_counter()
         try:
             res = run_helper(["barrier", "--votes", ",".join(map(str, v)), "--expect", str(self.n),
-                              "--backend", self.backend], self.timeout, self.registry)
+                              "--backend", self.backend], self.timeout, self.registry, self.program)
         except (RuntimeError, TimeoutError) as e:
             log.error("commit barrier helper: %s", e)
             self.last = {"error": str(e)}
             return False
         REGISTRY.phase_seconds.labels(phase="commit_barrier").observe(time.perf_counter() - t0)
+        res["wall_ms"] = round(1e3 * (time.perf_counter() - t0), 3)
         self.last = res
         if res.get("error"):
             log.error("commit barrier: %s", res["error"])
