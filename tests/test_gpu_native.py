@@ -258,3 +258,17 @@ def test_hbm_limit_shim_with_expandable_segments(gpu):
     assert "ENFORCED" in p.stdout and "NOT_ENFORCED" not in p.stdout, p.stdout
     peak = int(p.stdout.split("PEAK")[1].split()[0])
     assert 2**30 <= peak <= 2 * 2**30, peak  # the 1 GiB segment was charged through hipMemCreate
+
+
+def test_two_concurrent_slice_processes_have_disjoint_census(gpu):
+    """two pods run as two processes AT THE SAME TIME, each with the env Allocate()
+    gives its slice; the CUs each one's kernels land on (census taken while both loop) are the
+    slice's own and do not overlap, and both serve inferences in the common window."""
+    from walkai_nos_amd.dataplane.procs import run_pods
+    r = run_pods(["32cu.36gb", "64cu.72gb"], seconds=4.0, census=True, ready_timeout=240)
+    a, b = r["per_pod"]
+    assert sorted([a["hsa_cu_mask"], b["hsa_cu_mask"]]) == ["0:0-63", "0:64-95"], r
+    assert sorted([a["census_cus"], b["census_cus"]]) == [32, 64], r
+    assert r["census_pairs_overlapping"] == 0, r
+    assert a["inferences"] > 0 and b["inferences"] > 0, r
+    assert all(p["hbm"]["loaded"] and p["hbm"]["peak_bytes"] <= p["hbm"]["limit_bytes"] for p in r["per_pod"]), r

@@ -46,8 +46,26 @@ def set_slice_cus(n: Optional[int]) -> None:
     _slice.cus = n
 
 
+def env_mask_cus(mask: Optional[str] = None, device: int = 0) -> Optional[int]:
+    """CUs the process-wide ``HSA_CU_MASK`` (``<dev>:<ranges>[;<dev>:<ranges>]``, what the nos device
+    plugin's ``Allocate`` hands a container) leaves device ``device``; None when it does not mask it."""
+    mask = os.environ.get("HSA_CU_MASK", "") if mask is None else mask
+    for part in mask.split(";"):
+        dev, _, ranges = part.partition(":")
+        if not dev.strip().isdigit() or int(dev) != device or not ranges.strip():
+            continue
+        n = 0
+        for r in ranges.split(","):
+            lo, _, hi = r.strip().partition("-")
+            n += (int(hi) - int(lo) + 1) if hi else 1
+        return n
+    return None
+
+
 def slice_cus() -> int:
-    return getattr(_slice, "cus", None) or total_cus()
+    """CUs the current stream may use: the thread's slice, else the process's ``HSA_CU_MASK``
+    (a pod run as its own process), else the whole device."""
+    return getattr(_slice, "cus", None) or env_mask_cus() or total_cus()
 
 
 def set_slice_pin(mask: int) -> None:
