@@ -3,10 +3,12 @@
 
 Runs the flagship step (see :mod:`walkai_nos_amd.bench_core`): a node of N MI355X GPUs (one
 process per GPU under torchrun, RCCL over xGMI for the partition-commit barrier) serving a
-churning mix of 1/8, 1/2 and 1/1-GPU YOLOS-small inference pods through the nos control plane,
-one ``--quantum``-second serving quantum per step, every compute-partition flip charged as a
-``--flip-cost``-second outage of its GPU.  After the timed window a density phase saturates the
-node (8 CPX pods per GPU, then CU-mask slices beyond).  Rank 0 prints one JSON line.
+churning mix of 1/8, 1/2 and 1/1-GPU YOLOS-small inference pods through the nos control plane.
+One step = one quantum of ``--cluster-s`` seconds of cluster time replayed in ``--quantum`` wall
+seconds of GPU serving (pod lifetimes, planner thresholds and flip outages compressed alike; the
+GPU serves at its real rate); every compute-partition flip darkens its GPU for the measured flip
+cost.  After the timed window a density phase saturates the node (8 CPX pods per GPU, then CU-mask
+slices beyond).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -31,15 +33,20 @@ def main() -> int:
     ap.add_argument("--preroll", type=int, default=60,
                     help="control-plane-only steps before warmup, so timing starts in steady state")
     ap.add_argument("--quantum", type=float, default=0.5, help="wall seconds of serving per step")
-    ap.add_argument("--flip-cost", type=float, default=2.0,
-                    help="seconds a GPU serves nothing after a compute-partition flip")
+    ap.add_argument("--cluster-s", type=float, default=60.0, help="cluster seconds one step stands for")
+    ap.add_argument("--flip-cost", type=float, default=-1.0,
+                    help="cluster seconds a GPU serves nothing per compute-partition flip "
+                         "(default: the measured components, bench_core.FLIP_COST_COMPONENTS)")
+    ap.add_argument("--device-plugin", default="nos", choices=("nos", "amd"),
+                    help="nos: drains enforced by the partition plugin's device health; amd: no enforcement")
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
-    ap.add_argument("--depth", type=int, default=2, help="inferences in flight per pod stream")
+    ap.add_argument("--depth", type=int, default=1,
+                    help="inferences in flight per pod stream (1 = the reference demo's synchronous loop)")
     ap.add_argument("--pod-streams", type=int, default=1,
                     help="concurrent request streams per pod (1 = one inference at a time, as the reference demo)")
-    ap.add_argument("--lane-cus", type=int, default=64,
-                    help="a partition pod wider than this many CUs runs one batch-1 request loop per disjoint "
-                         "run of this many CUs (0 = one loop per pod)")
+    ap.add_argument("--lane-cus", type=int, default=0,
+                    help="opt-in: a partition pod wider than this many CUs runs one batch-1 request loop per "
+                         "disjoint run of this many CUs (0 = one loop per pod, as the reference demo)")
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--emulation", default=None, choices=("pinned", "spread", "landing"),
                     help="compute-partition emulation on the SPX device (default: spread; bench_core.EMULATION)")
@@ -66,9 +73,10 @@ def main() -> int:
     from walkai_nos_amd.bench_core import BenchConfig, run_bench
     cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
-                      preroll=args.preroll, quantum_s=args.quantum, flip_cost_s=args.flip_cost,
-                      policy=args.policy, depth=args.depth, density=not args.no_density,
-                      pod_streams=args.pod_streams, lane_cus=args.lane_cus)
+                      preroll=args.preroll, quantum_s=args.quantum, cluster_s=args.cluster_s,
+                      flip_cost_s=args.flip_cost, policy=args.policy, depth=args.depth,
+                      density=not args.no_density, pod_streams=args.pod_streams, lane_cus=args.lane_cus,
+                      device_plugin=args.device_plugin)
     if args.emulation:
         cfg.emulation = args.emulation
     res = run_bench(cfg)

@@ -243,7 +243,7 @@ def test_packing_config_maps_to_pack_params():
     cfg.validate()
     p = cfg.pack_params()
     assert (p.min_fill, p.drain_gain_after, p.spx_reserve) == (0.25, 120.0, False)
-    assert p.drain_gain == 0.625  # untouched knobs keep their defaults
+    assert p.drain_gain == 0.3 and p.min_stint == 120.0  # untouched knobs keep their defaults
     with pytest.raises(ValueError):
         GpuPartitionerConfig(packing={"minFil": 0.2}).validate()
     with pytest.raises(ValueError):
@@ -260,8 +260,24 @@ def test_pack_gain_drain_rotates_an_underused_gpu():
     pending = [({"spx_nps1": 1}, 700.0)]
     changed = plan_cluster_pack(models, pending, params=PackParams())
     assert changed["n0"].gpus[0].target == {"spx_nps1": 1}
-    assert plan_cluster_pack(models, pending, params=PackParams(drain_gain_after=0)) == {}
+    assert plan_cluster_pack(models, pending, params=PackParams(drain_gain_after=0, unserved_after=0)) == {}
     assert plan_cluster_pack(models, [({"spx_nps1": 1}, 100.0)], params=PackParams()) == {}
+
+
+def test_pack_fairness_drains_a_full_gpu_for_an_unserved_profile_after_its_stint():
+    # one GPU in CPX mode with all 8 partitions in use: the gain rule never drains it (the SPX queue
+    # would fill it no better), but no GPU serves SPX at all — after unserved_after x 1 GPU of
+    # waiting, and once the GPU has held CPX for min_stint, it is drained for SPX
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, new_node_model, plan_cluster_pack
+    node = xnode("n0", gpus=1, anns={"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8"})
+    models = {"n0": new_node_model("xcp", node)}
+    waited = [({"spx_nps1": 1}, 400.0)]
+    p = PackParams()
+    assert plan_cluster_pack(models, [({"spx_nps1": 1}, 200.0)], params=p) == {}          # not long enough
+    assert plan_cluster_pack(models, waited, params=p, mode_age=lambda n, g: 60.0) == {}  # stint not over
+    changed = plan_cluster_pack(models, waited, params=p, mode_age=lambda n, g: 600.0)
+    assert changed["n0"].gpus[0].target == {"spx_nps1": 1}
+    assert plan_cluster_pack(models, waited, params=PackParams(unserved_after=0), mode_age=lambda n, g: 600.0) == {}
 
 
 def test_multi_node_cluster_bench_tracks_flips_per_node():
@@ -275,7 +291,7 @@ def test_multi_node_cluster_bench_tracks_flips_per_node():
         assert all(isinstance(k, tuple) and k[0] in nb.cluster.nodes for k in nb.outage)
         nb.end_step()
     assert nb.flips > 0 and max(nb.util_samples) > 50.0
-    assert nb.gpu_steps == 40 * 6
+    assert nb.gpu_quanta == 40 * 6
 
 
 def test_pack_reserve_break_flips_a_reserved_idle_spx_gpu_for_a_full_queue():

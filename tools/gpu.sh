@@ -6,6 +6,7 @@
 #
 # steps:
 #   tests              pytest -m gpu (in one process)
+#   test_k             pytest -m gpu -k "$NOS_TEST_K"
 #   smoke              __graft_entry__.smoke()
 #   bench              bench.py as the driver runs it (--gpus 1 --steps 20 --warmup 5)
 #   bench_torch        bench.py on the PyTorch (hipBLASLt) backend, for comparison
@@ -51,6 +52,8 @@ pmc() {  # pmc <dir> <tag> <program...> -- <counters>: one counter pass, kernel 
 for s in "$@"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread ;;
+    test_k) step "test_${NOS_TEST_K:-x}" 600 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 \
+              --timeout-method thread -k "${NOS_TEST_K:-x}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
     bench_torch) step bench_torch 600 python bench.py --steps 20 --warmup 5 --backend torch --out "$OUT/bench_torch.json" ;;

@@ -73,12 +73,13 @@ class GpuPartitionerConfig(ManagerConfig):
     scoring: str = "fraction"
     #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
     #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds,
-    #: reserveBreakFill
+    #: reserveBreakFill, minStintSeconds, unservedAfterSeconds
     packing: Dict[str, Any] = field(default_factory=dict)
 
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
                     "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
-                    "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after",
+                    "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after", "minStintSeconds": "min_stint",
+                    "unservedAfterSeconds": "unserved_after",
                     "reserveBreakFill": "reserve_break_fill"}
 
     def pack_params(self) -> Any:

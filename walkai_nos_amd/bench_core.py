@@ -3,22 +3,32 @@
 Headline metric (BASELINE.json): *aggregate GPU utilization % + schedulable pods/node under a
 mixed fractional-GPU load*, on the workload the reference publishes numbers for (YOLOS-small
 batch-1 inference pods, ``demos/gpu-sharing-comparison``).  ``value`` is the aggregate inference
-rate the node sustains; utilisation and pods/node are reported next to it.
+rate the node sustains; allocation %, pods/node and per-profile service are reported next to it.
 
-One step = one **serving quantum** of ``quantum_s`` wall seconds:
+**Time model: a compressed replay of cluster time.**  One step = one *quantum* of
+``cluster_s`` (60) seconds of cluster time, replayed in ``quantum_s`` (0.5) wall seconds of GPU
+serving.  Every cluster-time duration is compressed by the same factor — pod lifetimes (2-6
+quanta, so the driver's 20 timed steps span 5 mean lifetimes), the planner's thresholds and every
+compute-partition flip's outage — while the GPU serves at its real rate, so inferences per wall
+second of the replay equal inferences per second of the cluster.  Per quantum:
 
-1. churn: pods whose served lifetime is over finish, new pods arrive (seeded Poisson process;
-   fractions 1/8, 1/2 and 1/1 GPU = ``amd.com/cpx_nps1``, ``dpx_nps1``, ``spx_nps1``);
-2. the *real* control plane (partitioner pod/node controllers with the flip-aware ``pack`` policy,
-   partition agents with their reporter/actuator handshake and commit barrier, the scheduler)
-   runs to quiescence on the in-memory API server;
-3. **every compute-partition flip is charged**: the flipped GPU serves nothing for
-   ``flip_cost_s`` (amd-smi switch + AMD device-plugin re-registration; the reference waits up to
-   a minute for the plugin, ``pkg/gpu/client.go:86-135``; 2 s by default, ``--flip-cost``), pods
-   on it neither serve nor age during the outage, and the GPU counts as unallocated;
-4. until the quantum ends, every running pod on this rank's GPU keeps its partition busy with
-   YOLOS-small inferences (fp32-accurate, batch 1, 800x1066; a HIP graph replay per inference on
-   a stream whose CU mask is the partition's CU set, ``depth`` inferences in flight per pod).
+1. churn: pods whose served lifetime is over finish, new pods arrive (seeded Poisson arrivals at
+   ``offered_load`` GPUs of demand per GPU; profiles 1/8, 1/2 and 1/1 GPU = ``amd.com/cpx_nps1``,
+   ``dpx_nps1``, ``spx_nps1`` drawn 50/30/20 in seeded stratified blocks);
+2. the *real* control plane runs for ``cluster_s`` on the virtual clock against the in-memory API
+   server: the partitioner (flip-aware ``pack`` policy), per node the partition agent (reporter,
+   actuator, commit barrier — RCCL across the bench's ranks) and the **nos partition device
+   plugin** whose health rule enforces drains (every partition of a GPU being re-partitioned is
+   Unhealthy, ``deviceplugin/partitions.py``), a kubelet that admits pods onto healthy devices
+   only, and a scheduler with kube-scheduler semantics (node allocatable minus requests; it knows
+   nothing about GPUs);
+3. **every flip is charged**: the flipped GPU serves nothing for ``flip_cost_s`` of cluster time
+   (the measured commit barrier + the amd-smi mode switch + the plugin's pushed update + the
+   probe round: :data:`FLIP_COST_COMPONENTS`); the dark part of a quantum is idle wall time in the
+   replay, pods on the GPU neither serve nor age meanwhile;
+4. for the rest of the quantum every running pod on this rank's GPU runs the reference demo's
+   loop: one YOLOS-small inference (fp32-accurate, batch 1, 800x1066; a HIP graph replay on a
+   stream whose CU mask is the partition's CU set) after another.
 
 Because the box is not root, compute-partition modes cannot be flipped on the real device; a
 CPX/QPX/DPX partition is emulated by an XCD-symmetric CU mask of the same CU count (32/64/128
@@ -86,6 +96,27 @@ def working_cus(cus: Optional[List[int]], pin: int, total_cus: int = 256) -> int
     return sum(1 for c in cus if (pin >> (c % XCDS)) & 1)
 
 
+#: One compute-partition flip, in cluster seconds, from its measured parts.  The GPU serves nothing
+#: from the amd-smi switch until the agent has committed and its pods can start:
+#:
+#: * ``commit_barrier_s`` — the node-atomic commit: the native helper's wall time (spawn, hipInit,
+#:   ncclCommInitAll, all-reduce, teardown), warm median (profiles/operator_gpu_report_r3.json);
+#: * ``probe_s`` — the probe-on-commit round after the flip (profiles/operator_gpu_report_r2.json);
+#: * ``plugin_push_s`` — the nos partition plugin's ListAndWatch push + allocatable patch (no plugin
+#:   restart; the reference waits up to 60 s for the NVIDIA plugin pod, ref pkg/gpu/client.go:86-135);
+#: * ``amdsmi_switch_s`` — the amd-smi compute-partition switch itself: NOT measurable here (the box
+#:   is not root, so the setter returns AMDSMI_STATUS_PERMISSION); 10 s is an estimate covering the
+#:   driver re-creating the partitions and the re-enumeration, flagged as such in BENCH.
+#:
+#: ``--flip-cost`` overrides the total; BENCH also reports the control plane's sensitivity to it.
+FLIP_COST_COMPONENTS = {"commit_barrier_s": 1.0, "probe_s": 0.39, "plugin_push_s": 0.05, "amdsmi_switch_s": 10.0}
+FLIP_COST_MEASURED = ("commit_barrier_s", "probe_s", "plugin_push_s")
+
+
+def default_flip_cost() -> float:
+    return round(sum(FLIP_COST_COMPONENTS.values()), 2)
+
+
 @dataclass
 class BenchConfig:
     gpus: int = 1
@@ -94,14 +125,15 @@ class BenchConfig:
     seed: int = 1234
     offered_load: float = 1.0            # offered GPU-equivalents per GPU (= capacity)
     quantum_s: float = 0.5               # wall seconds of serving per step
-    flip_cost_s: float = 2.0             # outage of a GPU per compute-partition flip
-    lifetime: Tuple[int, int] = (8, 24)  # served quanta per pod
+    cluster_s: float = 60.0              # cluster seconds one step stands for (the replay's compression)
+    flip_cost_s: float = -1.0            # cluster seconds a GPU is dark per flip (<0: FLIP_COST_COMPONENTS)
+    lifetime: Tuple[int, int] = (2, 6)   # served quanta per pod (uniform, stratified): mean 4 = 5 in 20 steps
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"
     graphs: bool = True
-    depth: int = 2                       # inferences in flight per pod stream
+    depth: int = 1                       # inferences in flight per pod stream (1 = the reference's loop)
     pod_streams: int = 1                 # concurrent request streams per pod (1 = the reference demo's loop)
-    lane_cus: int = 64                   # >0: a partition pod wider than this serves on disjoint CU runs of
+    lane_cus: int = 0                    # >0: a partition pod wider than this serves on disjoint CU runs of
                                          # this many CUs, one batch-1 request loop per run (0 = one loop)
     preroll: int = 60                    # control-plane-only steps before warmup (steady state)
     rank: int = 0
@@ -110,22 +142,44 @@ class BenchConfig:
     density: bool = True
     emulation: str = EMULATION           # compute-partition emulation: pinned | spread
     nodes: int = 1                       # cluster nodes of `gpus` GPUs (control-plane simulation only)
+    device_plugin: str = "nos"           # nos (drain enforced by device health) | amd (no drain enforcement)
+    pack: Optional[Dict[str, float]] = None  # PackParams overrides (field name -> value)
+
+    def __post_init__(self) -> None:
+        if self.flip_cost_s < 0:
+            self.flip_cost_s = default_flip_cost()
 
     @property
-    def outage_steps(self) -> int:
-        return int(math.ceil(self.flip_cost_s / self.quantum_s - 1e-9)) if self.flip_cost_s > 0 else 0
+    def flip_quanta(self) -> float:
+        """A flip's outage in quanta (fractional)."""
+        return self.flip_cost_s / self.cluster_s
+
+    @property
+    def mean_lifetime_quanta(self) -> float:
+        return (self.lifetime[0] + self.lifetime[1]) / 2
 
 
 class ChurnProcess:
-    """Deterministic pod arrival process (identical on every rank)."""
+    """Deterministic pod arrival process (identical on every rank): Poisson arrivals at the offered
+    load; profiles and lifetimes drawn from seeded shuffles of stratified blocks (every block of 10
+    arrivals holds the 50/30/20 mix exactly, every block of lifetimes each value once), so a short
+    window sees the mix it is configured with."""
 
     def __init__(self, cfg: BenchConfig):
         self.cfg = cfg
         self.rng = random.Random(cfg.seed)
         self.seq = 0
         mean_frac = sum((1.0 / COMPUTE_MODES[p.split("_")[0]]) * w for p, w in MIX)
-        mean_life = (cfg.lifetime[0] + cfg.lifetime[1]) / 2
-        self.rate = cfg.offered_load * cfg.gpus * cfg.nodes / (mean_frac * mean_life)
+        self.rate = cfg.offered_load * cfg.gpus * cfg.nodes / (mean_frac * cfg.mean_lifetime_quanta)
+        self._profiles: List[str] = []
+        self._lifetimes: List[int] = []
+
+    def _next_profile(self) -> str:
+        if not self._profiles:
+            block = [p for p, w in MIX for _ in range(int(round(10 * w)))]
+            self.rng.shuffle(block)
+            self._profiles = block
+        return self._profiles.pop()
 
     def arrivals(self) -> List[str]:
         # Poisson(rate) via inversion, seeded
@@ -135,22 +189,14 @@ class ChurnProcess:
             if p <= L:
                 break
             n += 1
-        out = []
-        for _ in range(n):
-            r, acc = self.rng.random(), 0.0
-            prof = MIX[-1][0]
-            for name, w in MIX:
-                acc += w
-                if r < acc:
-                    prof = name
-                    break
-            out.append(prof)
-        return out
+        return [self._next_profile() for _ in range(n)]
 
     def lifetime(self) -> int:
-        return self.rng.randint(*self.cfg.lifetime)
-
-
+        if not self._lifetimes:
+            block = list(range(self.cfg.lifetime[0], self.cfg.lifetime[1] + 1))
+            self.rng.shuffle(block)
+            self._lifetimes = block
+        return self._lifetimes.pop()
 
 
 def partition_xcds(profile: str, partition: int) -> Optional[List[int]]:
@@ -374,8 +420,8 @@ class DataPlane:
         for s in self.slots.values():
             s.drain()
 
-    def serve(self, keys: List[Any], deadline: float) -> int:
-        """Keep every listed slot busy until ``deadline``; returns the inferences enqueued.
+    def serve(self, keys: List[Any], deadline: float) -> Dict[Any, int]:
+        """Keep every listed slot busy until ``deadline``; returns the inferences enqueued per slot.
 
         A different set of compute modes than in the last quantum means the GPU was re-partitioned:
         every queued inference of the old layout finishes first (the agent only flips an idle GPU),
@@ -386,8 +432,8 @@ class DataPlane:
                 self.drains += 1
             self.drain_all()
             self._layout = layout
-        active = [self.slots[k] for k in keys]
-        n = 0
+        active = [(k, self.slots[k]) for k in keys]
+        n: Dict[Any, int] = {k: 0 for k in keys}
         while True:
             now = time.perf_counter()
             if now >= deadline:
@@ -396,11 +442,11 @@ class DataPlane:
                 time.sleep(deadline - now)
                 break
             progressed = False
-            for s in active:
+            for k, s in active:
                 s.reap()
                 if s.in_flight < s.capacity:
                     s.submit()
-                    n += 1
+                    n[k] += 1
                     progressed = True
             if not progressed:
                 time.sleep(0.0002)
@@ -473,42 +519,53 @@ class HwBusySampler:
 
 
 class NodeBench:
-    """The simulated node (real control plane) + the outage model + this rank's data plane. With
-    ``cfg.nodes > 1`` (control plane only, ``nos-simulate --nodes``) the cluster has that many nodes
-    and the outage model tracks every (node, GPU); the data plane serves the first node."""
+    """The simulated node (real control plane, nos partition device plugin, kube-scheduler
+    semantics) + the outage model + this rank's data plane. With ``cfg.nodes > 1`` (control plane
+    only, ``nos-simulate --nodes``) the cluster has that many nodes and the outage model tracks
+    every (node, GPU); the data plane serves the first node."""
 
     def __init__(self, cfg: BenchConfig, barrier_factory=None, gpu_data_plane: bool = True,
                  verify=None):
         from .sim.cluster import SimCluster
 
         self.cfg = cfg
-        self.cluster = SimCluster(n_nodes=cfg.nodes, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
+        from .controllers.partitioner.pod_controller import PackParams
+        self.cluster = SimCluster(n_nodes=cfg.nodes, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy,
+                                  device_plugin=cfg.device_plugin, pack=PackParams(**(cfg.pack or {})))
         self.sn = next(iter(self.cluster.nodes.values()))  # the node this rank's data plane serves
         if barrier_factory is not None or verify is not None:
             self._set_commit(barrier_factory, verify)
         self.churn = ChurnProcess(cfg)
         self.cluster.run(30)  # node initialisation (SPX everywhere)
-        self.live: Dict[str, int] = {}          # running pod -> served quanta left
-        self.outage: Dict[Tuple[str, int], int] = {}  # (node, GPU) -> quanta of outage left
+        self.live: Dict[str, float] = {}              # running pod -> served quanta left
+        self.profile_of: Dict[str, str] = {}          # pod -> requested profile
+        self.created: Dict[str, float] = {}           # pod -> cluster time it was created
+        self.bound_at: Dict[str, float] = {}          # pod -> cluster time it was bound
+        self.outage: Dict[Tuple[str, int], float] = {}  # (node, GPU) -> quanta of outage left
         self._flips_seen = {n: len(sn.smi.set_calls) for n, sn in self.cluster.nodes.items()}
+        self._binds_seen = 0
         self.reset_stats()
         self.data: Optional[DataPlane] = DataPlane(cfg) if gpu_data_plane else None
 
     def reset_stats(self) -> None:
         self.inferences = 0
         self.flips = 0
-        self.outage_gpu_steps = 0
-        self.gpu_steps = 0
+        self.outage_gpu_quanta = 0.0
+        self.gpu_quanta = 0
         self.util_samples: List[float] = []
         self.raw_util_samples: List[float] = []
         self.pods_samples: List[int] = []
         self.pending_samples: List[int] = []
         self.host_s = {"control": 0.0, "serve": 0.0}
         self.empty_steps = 0
+        self.profile_inferences: Dict[str, int] = collections.defaultdict(int)
+        self.profile_pods: Dict[str, set] = collections.defaultdict(set)        # pods that served in the window
+        self.tts: Dict[str, List[float]] = collections.defaultdict(list)        # bound in the window: wait (s)
+        self.dark_wall_s = 0.0
 
-    def dark(self, gpu: int, node: Optional[str] = None) -> bool:
-        """Is ``gpu`` of ``node`` (default: this rank's node) in a flip outage this quantum?"""
-        return self.outage.get((node or self.sn.name, gpu), 0) > 0
+    def dark(self, gpu: int, node: Optional[str] = None) -> float:
+        """Fraction of this quantum ``gpu`` of ``node`` (default: this rank's node) is dark (flip outage)."""
+        return min(1.0, max(0.0, self.outage.get((node or self.sn.name, gpu), 0.0)))
 
     def _set_commit(self, factory: Any, verify: Any) -> None:
         for c in self.sn.manager.controllers:
@@ -530,50 +587,60 @@ class NodeBench:
     def control_step(self) -> None:
         t0 = time.perf_counter()
         c = self.cluster
-        gpus_of = self.pod_gpus()
-        for name in list(self.live):
-            if any(self.outage.get(g, 0) > 0 for g in gpus_of.get(name, ())):
-                continue  # its GPU is dark: the pod neither serves nor ages
-            self.live[name] -= 1
-            if self.live[name] <= 0:
-                del self.live[name]
-                c.complete(name)
-                c.delete_pod(name)  # the owning controller garbage-collects finished pods
+        for name in [n for n, left in self.live.items() if left <= 1e-9]:
+            del self.live[name]
+            c.complete(name)
+            c.delete_pod(name)  # the owning controller garbage-collects finished pods
+        now = c.clock()
         for prof in self.churn.arrivals():
-            c.submit({f"amd.com/{prof}": 1}, name=f"p{self.churn.seq}")
+            name = f"p{self.churn.seq}"
+            c.submit({f"amd.com/{prof}": 1}, name=name)
+            self.profile_of[name] = prof
+            self.created[name] = now
             self.churn.seq += 1
-        c.run(60)
+        c.run(self.cfg.cluster_s)
+        c.clock.set(now + self.cfg.cluster_s)  # a quantum is cluster_s of cluster time, idle or not
         for nname, sn in c.nodes.items():
             calls = sn.smi.set_calls
             for kind, gpu, _ in calls[self._flips_seen[nname]:]:
                 self.flips += 1
                 for g in (range(self.cfg.gpus) if gpu is None else (gpu,)):
-                    self.outage[(nname, g)] = max(self.outage.get((nname, g), 0), self.cfg.outage_steps)
+                    self.outage[(nname, g)] = max(self.outage.get((nname, g), 0.0), self.cfg.flip_quanta)
             self._flips_seen[nname] = len(calls)
+        for t, name, _ in c.binds[self._binds_seen:]:
+            self.bound_at[name] = t
+            if name in self.created:
+                self.tts[self.profile_of.get(name, "?")].append(t - self.created[name])
+        self._binds_seen = len(c.binds)
         for p in c.running_pods():
             n = ko.name(p)
             if n not in self.live:
-                self.live[n] = self.churn.lifetime()
+                self.live[n] = float(self.churn.lifetime())
         frac = c.gpu_allocated_fraction()
-        dark = {k for k, v in self.outage.items() if v > 0}
         self.raw_util_samples.append(100.0 * sum(frac.values()) / max(1, len(frac)))
-        self.util_samples.append(100.0 * sum(v for k, v in frac.items() if k not in dark) / max(1, len(frac)))
+        self.util_samples.append(100.0 * sum(v * (1.0 - self.dark(g, n)) for (n, g), v in frac.items())
+                                 / max(1, len(frac)))
         self.pods_samples.append(len(c.running_pods()))
         self.pending_samples.append(len(c.pending_pods()))
-        self.gpu_steps += self.cfg.gpus * self.cfg.nodes
-        self.outage_gpu_steps += len(dark)
+        self.gpu_quanta += self.cfg.gpus * self.cfg.nodes
+        self.outage_gpu_quanta += sum(self.dark(g, n) for (n, g) in frac)
         self.host_s["control"] += time.perf_counter() - t0
 
     def end_step(self) -> None:
+        """Age every running pod by the part of the quantum its GPU was lit, then let outages run."""
+        gpus_of = self.pod_gpus()
+        for name in list(self.live):
+            lit = min((1.0 - self.dark(g, n) for (n, g) in gpus_of.get(name, ())), default=1.0)
+            if lit > 0:
+                self.profile_pods[self.profile_of.get(name, "?")].add(name)
+            self.live[name] -= lit
         for g in list(self.outage):
-            self.outage[g] -= 1
-            if self.outage[g] <= 0:
+            self.outage[g] -= 1.0
+            if self.outage[g] <= 1e-9:
                 del self.outage[g]
 
     def my_pods(self) -> List[Tuple[str, int]]:
         """(profile, partition index) of the pods served on this rank's GPU this quantum."""
-        if self.dark(self.cfg.rank):
-            return []
         out = []
         for devs in self.sn.kubelet.allocations.values():
             for r, dev_id in devs:
@@ -586,18 +653,63 @@ class NodeBench:
         return out
 
     def step(self, deadline: Optional[float] = None) -> int:
+        """One quantum: control plane, then the dark part of the quantum idle (a flip in progress),
+        then every pod of this rank's GPU served until ``deadline``."""
         t0 = time.perf_counter()
         deadline = deadline if deadline is not None else t0 + self.cfg.quantum_s
         self.control_step()
         keys = self.my_pods()
+        dark = self.dark(self.cfg.rank)
         if not keys:
             self.empty_steps += 1
         t1 = time.perf_counter()
-        n = self.data.serve(keys, deadline) if self.data is not None else 0
+        n: Dict[Any, int] = {}
+        if self.data is not None:
+            lit_from = deadline - (1.0 - dark) * self.cfg.quantum_s
+            if dark > 0:
+                self.data.drain_all()  # the flipped GPU ran nothing of the old layout past the flip
+                wait = lit_from - time.perf_counter()
+                if wait > 0:
+                    time.sleep(wait)
+                    self.dark_wall_s += wait
+            n = self.data.serve(keys if dark < 1.0 else [], deadline)
         self.host_s["serve"] += time.perf_counter() - t1
-        self.inferences += n
+        total = sum(n.values())
+        self.inferences += total
+        for k, v in n.items():
+            self.profile_inferences[str(k[0])] += v
         self.end_step()
-        return n
+        return total
+
+    def profile_report(self, window_s: float) -> Dict[str, Dict[str, Any]]:
+        """Per profile: inferences served in the window, pods that served, time-to-schedule of the
+        pods bound in the window (cluster seconds and mean pod lifetimes), waits of pods still
+        pending at the end."""
+        life_s = self.cfg.mean_lifetime_quanta * self.cfg.cluster_s
+        now = self.cluster.clock()
+        pending_age: Dict[str, List[float]] = collections.defaultdict(list)
+        for p in self.cluster.pending_pods():
+            n = ko.name(p)
+            if n in self.created:
+                pending_age[self.profile_of.get(n, "?")].append(now - self.created[n])
+        out: Dict[str, Dict[str, Any]] = {}
+        for prof, _ in MIX:
+            tts = sorted(self.tts.get(prof, []))
+            waits = sorted(pending_age.get(prof, []))
+            row: Dict[str, Any] = {"inferences": int(self.profile_inferences.get(prof, 0)),
+                                   "inf_per_s": round(self.profile_inferences.get(prof, 0) / max(1e-9, window_s), 2),
+                                   "pods_served": len(self.profile_pods.get(prof, ())),
+                                   "pods_bound": len(tts)}
+            if tts:
+                row["tts_s"] = {"p50": round(tts[len(tts) // 2], 1),
+                                "p99": round(tts[min(len(tts) - 1, int(0.99 * len(tts)))], 1),
+                                "max": round(tts[-1], 1)}
+                row["tts_lifetimes_p99"] = round(row["tts_s"]["p99"] / life_s, 2)
+            row["pending_at_end"] = len(waits)
+            if waits:
+                row["pending_wait_s_max"] = round(waits[-1], 1)
+            out[prof] = row
+        return out
 
     def close(self) -> None:
         if self.data is not None:
@@ -630,7 +742,7 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
         keys = [("cpx_nps1", sn.smi.resolve(d).partition_index) for devs in sn.kubelet.allocations.values()
                 for _, d in devs if sn.smi.resolve(d).gpu_index == cfg.rank]
         t0 = time.perf_counter()
-        n = data.serve(keys, t0 + serve_s)
+        n = sum(data.serve(keys, t0 + serve_s).values())
         data.drain_all()
         torch.cuda.synchronize()
         out["xcp"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
@@ -662,7 +774,7 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
             wanted = {(variant, s.id): cus_of(s, slices, 256) for s in slices if s.id in mine}
             data.add_slots(wanted)
             t0 = time.perf_counter()
-            n = data.serve(list(wanted), t0 + serve_s)
+            n = sum(data.serve(list(wanted), t0 + serve_s).values())
             data.drain_all()
             torch.cuda.synchronize()
             out[variant]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
@@ -686,6 +798,33 @@ def inference_latency(data: Optional[DataPlane]) -> Dict[str, Dict[str, float]]:
             v = sorted(v)
             out[mode] = {"n": len(v), "mean": round(sum(v) / len(v), 3), "p50": round(v[len(v) // 2], 3),
                          "p99": round(v[min(len(v) - 1, int(0.99 * len(v)))], 3)}
+    return out
+
+
+def _mean(v: List[float]) -> float:
+    return sum(v) / max(1, len(v))
+
+
+def flip_cost_report(cfg: BenchConfig) -> Dict[str, Any]:
+    out: Dict[str, Any] = {"total_s": cfg.flip_cost_s, "per_quantum": round(cfg.flip_quanta, 4)}
+    if abs(cfg.flip_cost_s - default_flip_cost()) < 1e-9:
+        out["components_s"] = dict(FLIP_COST_COMPONENTS)
+        out["measured"] = list(FLIP_COST_MEASURED)
+        out["estimated"] = [k for k in FLIP_COST_COMPONENTS if k not in FLIP_COST_MEASURED]
+    else:
+        out["components_s"] = "overridden by --flip-cost"
+    return out
+
+
+def flip_sensitivity(cfg: BenchConfig, costs=(2.0, 5.0, 10.0, 30.0), steps: Optional[int] = None) -> Dict[str, Any]:
+    """The control plane alone (no GPU) over the same seeded window for several flip costs: how much
+    allocation the cost of a flip takes (``control_only``, priced with the measured mode rates)."""
+    import dataclasses
+    out: Dict[str, Any] = {}
+    for fc in costs:
+        c = dataclasses.replace(cfg, flip_cost_s=fc, rank=0, world=1)
+        r = control_only(c, steps if steps is not None else cfg.warmup + cfg.steps, skip=cfg.warmup)
+        out[f"{fc:g}s"] = {k: r[k] for k in ("util_pct", "flips", "time_in_flip_pct", "inf_per_s_model")}
     return out
 
 
@@ -732,7 +871,9 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     elapsed = time.perf_counter() - t0
     hw_busy = busy.stop()
     on_gpu = dist.get_backend() == "nccl" if distributed else True
-    stats = torch.tensor([elapsed, float(nb.inferences), hw_busy if hw_busy is not None else -1.0],
+    profs = [p for p, _ in MIX]
+    stats = torch.tensor([elapsed, float(nb.inferences), hw_busy if hw_busy is not None else -1.0]
+                         + [float(nb.profile_inferences.get(p, 0)) for p in profs],
                          dtype=torch.float64, device=f"cuda:{nb.data.device}" if on_gpu else "cpu")
     if distributed:
         t = stats[:1].clone()
@@ -741,18 +882,24 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
         elapsed, total_inf = float(t.item()), float(s[0].item())
         hw_busy = round(float(s[1].item()) / cfg.world, 1) if hw_busy is not None else None
+        for i, p in enumerate(profs):
+            nb.profile_inferences[p] = int(s[2 + i].item())
     else:
         total_inf = float(nb.inferences)
     latency = inference_latency(nb.data)
+    per_profile = nb.profile_report(elapsed)
+    barrier_8dev = node_barrier_probe(cfg) if cfg.rank == 0 else None
     density = density_phase(cfg, nb.data) if cfg.density else {}
     nb.close()
     value = total_inf / elapsed
-    util = sum(nb.util_samples) / max(1, len(nb.util_samples))
-    raw = sum(nb.raw_util_samples) / max(1, len(nb.raw_util_samples))
-    pods = sum(nb.pods_samples) / max(1, len(nb.pods_samples))
+    util = _mean(nb.util_samples)
+    raw = _mean(nb.raw_util_samples)
+    pods = _mean(nb.pods_samples)
     from .models.workload.yolos import YolosSmall
     from .ops import kernels as K
     flops = YolosSmall().flops_per_inference(cfg.hw)
+    sens = flip_sensitivity(cfg) if cfg.rank == 0 else {}
+    life_s = cfg.mean_lifetime_quanta * cfg.cluster_s
     return {
         "metric": "aggregate GPU utilization % + schedulable pods/node, mixed fractional-GPU load",
         "value": round(value, 3),
@@ -775,27 +922,37 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "hw_busy_source": "amd-smi gfx_activity, sampled every 100 ms in the timed window" if hw_busy is not None
         else f"unavailable: {busy.error}",
         "hw_power_clock": busy.power_summary(),
-        "inference_latency_ms": latency,
         "pods_per_node": round(pods, 2),
         "pods_per_gpu": round(pods / cfg.gpus, 2),
+        "per_profile": per_profile,
+        "inference_latency_ms": latency,
+        "pending_pods_mean": round(_mean(nb.pending_samples), 2),
+        "pending_pods_max": max(nb.pending_samples) if nb.pending_samples else 0,
+        "window": {"quanta": cfg.steps, "cluster_s_per_quantum": cfg.cluster_s, "wall_s_per_quantum": cfg.quantum_s,
+                   "compression": round(cfg.cluster_s / cfg.quantum_s, 1),
+                   "mean_pod_lifetime_quanta": cfg.mean_lifetime_quanta,
+                   "pod_lifetimes_in_window": round(cfg.steps / cfg.mean_lifetime_quanta, 2),
+                   "mean_pod_lifetime_cluster_s": life_s},
+        "flip_cost": flip_cost_report(cfg),
+        "flips": nb.flips,
+        "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
+        "dark_wall_s": round(nb.dark_wall_s, 3),
+        "flip_cost_sensitivity": sens,
+        "commit_barrier_node": barrier_8dev,
         "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},
         "density": density,
-        "pending_pods_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
-        "pending_pods_max": max(nb.pending_samples) if nb.pending_samples else 0,
-        "flip_cost_s": cfg.flip_cost_s,
-        "flips": nb.flips,
-        "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),
-        "quantum_s": cfg.quantum_s,
         "achieved_tflops": round(value * flops / 1e12, 2),
         "host_ms_per_step": {k: round(1000.0 * v / cfg.steps, 2) for k, v in nb.host_s.items()},
         "layout_drains": nb.data.drains if nb.data is not None else 0,
         "empty_steps": nb.empty_steps,
+        "admission_failures": nb.cluster.admission_failures,
         "baseline_ref": BASELINE_LABEL,
         "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
                    "parallelism": f"fractional-gpu xcp partitions, {cfg.gpus} GPU node",
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
                    "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
+                   "device_plugin": cfg.device_plugin, "scheduler": "kube-scheduler semantics (allocatable)",
                    "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
                    "pod_streams": cfg.pod_streams, "lane_cus": cfg.lane_cus,
                    "partition_emulation": cfg.emulation,
@@ -803,38 +960,64 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     }
 
 
-def control_only(cfg: BenchConfig, steps: int) -> Dict[str, Any]:
-    """The control plane + outage model alone (no GPU): allocation, flips and queue over ``steps``
-    quanta after the preroll.  ``inf_per_s_model`` prices the served partition-quanta with the
-    measured per-mode full-GPU rates (``profiles/kbench_r2_modes_lanes64_splitk_rule.json``)."""
+def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
+    """The node-atomic commit barrier over every GPU this process can see, timed once after the
+    window (never inside it): the native helper spawned as the partition agent spawns it, one
+    communicator over all devices. On the driver's 8-GPU node this measures the 8-device clique."""
+    try:
+        from .ops import native
+        from .parallel.spawned import NATIVE_HELPER, SpawnedNodeBarrier
+        if not native.available(NATIVE_HELPER):
+            return {"error": "native helper not built"}
+        import torch
+        n = torch.cuda.device_count()
+        b = SpawnedNodeBarrier(n, backend="rccl", native=True, timeout=120.0)
+        ok = b.vote_all([True] * n)
+        out = {"devices": n, "committed": ok}
+        out.update({k: b.last.get(k) for k in ("wall_ms", "hip_init_ms", "comm_init_ms", "allreduce_ms",
+                                                "destroy_ms", "error") if b.last.get(k) is not None})
+        return out
+    except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench
+        return {"error": str(e)[:200]}
+
+
+def control_only(cfg: BenchConfig, steps: int, skip: int = 0) -> Dict[str, Any]:
+    """The control plane + outage model alone (no GPU): allocation, flips, queue and per-profile
+    time-to-schedule over ``steps`` quanta after the preroll (the first ``skip`` of them are warm-up,
+    not counted).  ``inf_per_s_model`` prices the served partition-quanta with the measured
+    one-loop-per-pod mode rates (``profiles/kbench_r2_modes_tiles256.json``)."""
     nb = NodeBench(cfg, gpu_data_plane=False)
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
-    nb.reset_stats()
-    # SPX and DPX pods serve as 64-CU request lanes (cfg.lane_cus); profiles/kbench_r2_modes_lanes64_splitk_rule.json
-    rate = {"spx": 437.9, "dpx": 445.2, "qpx": 438.9, "cpx": 389.2}
+    rate = {"spx": 358.2, "dpx": 429.3, "qpx": 440.4, "cpx": 376.2}
     served = 0.0
-    for _ in range(steps):
+    for i in range(steps):
+        if i == skip:
+            nb.reset_stats()
+            served = 0.0
         nb.control_step()
         for g in range(cfg.gpus):
-            if nb.dark(g):
-                continue
+            lit = 1.0 - nb.dark(g)
             for devs in nb.sn.kubelet.allocations.values():
                 for r, d in devs:
                     p = extract_profile_name(r)
                     if p is not None and nb.sn.smi.resolve(d).gpu_index == g:
                         m = p.split("_")[0]
-                        served += rate[m] / COMPUTE_MODES[m] * cfg.quantum_s
+                        served += rate[m] / COMPUTE_MODES[m] * cfg.quantum_s * lit
+                        nb.profile_inferences[p] += int(rate[m] / COMPUTE_MODES[m] * cfg.quantum_s * lit)
         nb.end_step()
-    return {"policy": cfg.policy, "gpus": cfg.gpus, "steps": steps, "flip_cost_s": cfg.flip_cost_s,
-            "util_pct": round(sum(nb.util_samples) / max(1, len(nb.util_samples)), 2),
-            "util_incl_outage_pct": round(sum(nb.raw_util_samples) / max(1, len(nb.raw_util_samples)), 2),
-            "flips": nb.flips, "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),
-            "pending_mean": round(sum(nb.pending_samples) / max(1, len(nb.pending_samples)), 2),
+    n = steps - skip
+    return {"policy": cfg.policy, "gpus": cfg.gpus, "steps": n, "flip_cost_s": cfg.flip_cost_s,
+            "util_pct": round(_mean(nb.util_samples), 2),
+            "util_incl_outage_pct": round(_mean(nb.raw_util_samples), 2),
+            "flips": nb.flips, "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
+            "pending_mean": round(_mean(nb.pending_samples), 2),
             "pending_max": max(nb.pending_samples) if nb.pending_samples else 0,
-            "pods_per_gpu": round(sum(nb.pods_samples) / max(1, len(nb.pods_samples)) / cfg.gpus, 2),
-            "inf_per_s_model": round(served / (steps * cfg.quantum_s), 1)}
+            "pods_per_gpu": round(_mean(nb.pods_samples) / cfg.gpus, 2),
+            "inf_per_s_model": round(served / (n * cfg.quantum_s), 1),
+            "admission_failures": nb.cluster.admission_failures,
+            "per_profile": nb.profile_report(n * cfg.quantum_s)}
 
 
 def smoke_step() -> None:
@@ -846,7 +1029,7 @@ def smoke_step() -> None:
     assert r.tflops > 0
     cfg = BenchConfig(gpus=1, steps=1, warmup=0, graphs=False)
     nb = NodeBench(cfg, barrier_factory=None, gpu_data_plane=False)
-    for _ in range(8):  # a few quanta of churn, so pods are scheduled and running
+    for _ in range(4):  # a few quanta of churn, so pods are scheduled and running
         nb.control_step()
         nb.end_step()
     from .models.workload.yolos import YolosSmall, demo_input

@@ -169,9 +169,15 @@ class PackParams:
     drain_backlog: float = 2.0      # ... if its profile's queue would fill at least this many GPUs
     spx_reserve: bool = True        # keep idle SPX GPUs for recent whole-GPU demand (multi-GPU)
     reserve_decay: float = 0.5      # EMA decay of the whole-GPU demand estimate per planning pass
-    drain_gain: float = 0.625       # drain a busy GPU whose used fraction is this much below the
-    drain_gain_after: float = 600.0  # ... fill a profile waiting this long would give it (0 = off)
+    drain_gain: float = 0.3         # drain a busy GPU whose used fraction is this much below the
+    drain_gain_after: float = 180.0  # ... fill a profile waiting this long would give it (0 = off)
     reserve_break_fill: float = 2.0  # a queue filling this many GPUs takes a reserved idle SPX GPU
+    min_stint: float = 120.0        # seconds: a GPU keeps a mode at least this long before it may be
+                                    # drained for another (refilled from its own queue meanwhile)
+    unserved_after: float = 300.0   # seconds (x GPUs of the cluster): a profile no GPU serves (none in its mode, none draining
+                                    # to it) whose oldest pod waited this long gets a GPU drained for
+                                    # it regardless of gain (0 = off) — the fairness that makes a
+                                    # single GPU cycle through the modes its pods ask for
 
 
 def _mode_of(gpu: Any) -> Optional[str]:
@@ -181,7 +187,8 @@ def _mode_of(gpu: Any) -> Optional[str]:
 
 def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[str, int], float]],
                       incoming: Optional[Mapping[str, int]] = None, params: Optional[PackParams] = None,
-                      spx_demand: float = 0.0) -> Dict[str, NodeModel]:
+                      spx_demand: float = 0.0,
+                      mode_age: Optional[Callable[[str, int], float]] = None) -> Dict[str, NodeModel]:
     """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
     reference's "first node that can change wins").
 
@@ -206,12 +213,23 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
        oldest pod has waited ``drain_gain_after`` and whose queue would fill a GPU at least
        ``drain_gain`` more than the pods now holding one (a single-GPU node otherwise serves one
        profile for as long as its pods keep arriving), with no idle GPU to take gets one busy
-       GPU **drained** for it: the least-used GPU in another mode gets the new spec now, is no
-       longer offered to new pods (``PartitionedGPU.target``; the scheduler skips GPUs whose spec
-       mode differs from their current mode), and the agent flips it when its last pod leaves.
-       Without this a single GPU that never goes idle would starve every other profile forever.
+       GPU **drained** for it: the least-used GPU in another mode that has held its mode for at
+       least ``min_stint`` (``mode_age``; a GPU just flipped first serves — and refills — its own
+       queue) gets the new spec now, is no longer offered to new pods (``PartitionedGPU.target``;
+       the nos partition device plugin reports every partition of a GPU being re-partitioned
+       Unhealthy, so neither kube-scheduler nor kubelet can place a pod there), and the agent flips
+       it when its last pod leaves.  Without this a single GPU that never goes idle would starve
+       every other profile forever;
+    6. **fairness**: a profile that no GPU serves — none in its mode, none draining towards it — and
+       whose oldest pod has waited ``unserved_after`` x (GPUs in the cluster) gets a GPU drained for
+       it without the gain
+       condition (still the least-used GPU past ``min_stint``).  On a multi-GPU node the GPUs settle
+       into modes that match the demand and this rarely fires; on a single GPU it is what makes the
+       GPU cycle through the modes its queue asks for, each mode serving (and refilling) for at
+       least ``min_stint``.
 
-    ``pending`` = [(requested profiles, age in seconds)], oldest first."""
+    ``pending`` = [(requested profiles, age in seconds)], oldest first; ``mode_age(node, gpu)`` =
+    seconds since that GPU's mode last changed (None: unknown, treated as old)."""
     params = params or PackParams()
     current = {n: m.clone() for n, m in models.items()}
     changed: Dict[str, NodeModel] = {}
@@ -317,6 +335,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
     # 5. drain a busy GPU for a profile that has waited too long (backlog rule), or whose waiting
     #    demand would use the GPU much better than the few pods holding it now (gain rule)
     draining_to = {next(iter(g.target)) for m in current.values() for g in m.gpus if g.target}
+    served = {_mode_of(g) for m in current.values() for g in m.gpus} | draining_to
     used_of = (lambda g: g.used_fraction(lambda q: round(1.0 / frac(q)))) if w is not None else \
         (lambda g: float(sum(g.used.values())))
     for p in sorted(demand, key=lambda q: -oldest.get(q, 0.0)):
@@ -324,13 +343,19 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
             continue
         backlog = demand[p] >= params.drain_backlog - 1e-9 and oldest.get(p, 0.0) >= params.drain_after
         gain_ok = params.drain_gain_after > 0 and oldest.get(p, 0.0) >= params.drain_gain_after
-        if not backlog and not gain_ok:
+        # the fairness wait scales with the node count of GPUs: the more GPUs, the sooner one goes
+        # idle on its own and is handed to the waiting profile by rule 3 — a drain is the last resort
+        starved = params.unserved_after > 0 and p not in served and \
+            oldest.get(p, 0.0) >= params.unserved_after * max(1, total_gpus)
+        if not backlog and not gain_ok and not starved:
             continue
         fill = min(demand[p], 1.0)
         cands = [(used_of(g), name, g) for name in sorted(current) for g in current[name].gpus
-                 if g.target is None and not g.is_idle() and _mode_of(g) != p]
-        if not backlog:
+                 if g.target is None and not g.is_idle() and _mode_of(g) != p
+                 and (mode_age is None or params.min_stint <= 0 or mode_age(name, g.index) >= params.min_stint)]
+        if not backlog and not starved:
             cands = [c for c in cands if w is not None and fill - c[0] >= params.drain_gain - 1e-9]
+
         if not cands:
             continue
         _, name, g = min(cands, key=lambda c: (c[0], c[1], c[2].index))
@@ -342,6 +367,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         g.target = trial.geometry()
         changed[name] = current[name]
         draining_to.add(p)
+        served.add(p)
     return changed
 
 
@@ -422,6 +448,7 @@ class PodController:
         self.policy = policy
         self.pack = pack or PackParams()
         self._first_seen: Dict[str, float] = {}   # pending pod uid -> first time the planner saw it
+        self._mode_since: Dict[Tuple[str, int], Tuple[Optional[str], float]] = {}  # (node, gpu) -> (mode, since)
         self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
@@ -521,6 +548,18 @@ class PodController:
                 return False
         return True
 
+    def _mode_ages(self, models: Mapping[str, NodeModel], now: float) -> Callable[[str, int], float]:
+        """Track when each GPU's reported mode last changed (first sight counts as long ago)."""
+        for name, m in models.items():
+            for g in getattr(m, "gpus", []):
+                mode = _mode_of(g)
+                prev = self._mode_since.get((name, g.index))
+                if prev is None:
+                    self._mode_since[(name, g.index)] = (mode, float("-inf"))
+                elif prev[0] != mode:
+                    self._mode_since[(name, g.index)] = (mode, now)
+        return lambda name, idx: now - self._mode_since.get((name, idx), (None, float("-inf")))[1]
+
     def _update_spx_demand(self, nodes: List[Dict[str, Any]], pending: List[Tuple[Dict[str, int], float]]) -> None:
         """EMA of whole-GPU demand: SPX partitions in use plus SPX pods waiting."""
         used = 0
@@ -549,8 +588,10 @@ class PodController:
         while the revision is unchanged (no pod, node or annotation changed) the same request would
         plan on identical inputs and reach the same answer, so the requeues of a waiting plan key
         return that answer without re-planning. Only with a client that exposes ``revision`` (the
-        in-memory API server) and without a batch window (whose deadline depends on the clock)."""
-        rev = getattr(self.client, "revision", None) if self.batch_timeout <= 0 else None
+        in-memory API server), without a batch window (whose deadline depends on the clock) and not
+        for the ``pack`` policy, whose starve/drain rules depend on how long pods have waited and
+        GPUs have held their mode: the same inputs plan differently a minute later."""
+        rev = getattr(self.client, "revision", None) if self.batch_timeout <= 0 and self.policy != "pack" else None
         if rev is not None:
             seen, results = self._idle
             if seen == rev and req in results:
@@ -618,7 +659,8 @@ class PodController:
                     incoming[p] = incoming.get(p, 0) + q
             pend = self.pending_with_age()
             self._update_spx_demand(nodes, pend)
-            changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand)
+            changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand,
+                                        self._mode_ages(models, now))
             need = requested
         elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}

@@ -1,0 +1,220 @@
+"""nos partition device plugin: MI355X compute partitions as ``amd.com/<mode>_<nps>`` devices,
+with the drain enforced where kubelet and kube-scheduler can see it.
+
+Why nos serves partitions itself.  On MIG the reference never needs a drain: a geometry can change
+around used devices (ref ``pkg/gpu/mig/gpu.go:99-112``) and the agent deletes only free devices
+(ref ``internal/controllers/migagent/actuator.go:225``).  An MI355X mode flip destroys every
+partition of the GPU, so it needs the GPU empty: the partitioner's ``pack`` policy writes the new
+spec for a busy GPU (its *drain target*) and expects that no new pod lands there.  kube-scheduler
+only counts node allocatable, and with the AMD device plugin every free partition of that GPU stays
+allocatable — new pods keep landing on it and the drain never ends.
+
+So the devices of this plugin carry the drain: **every partition of a GPU that is being
+re-partitioned is advertised ``Unhealthy``** — the node's spec annotations ask this GPU for a
+different geometry than its status reports (draining while partitions are in use, or about to
+flip) — and so is every partition of a GPU that left the device map.  kubelet never hands an
+unhealthy partition to a new container, and node allocatable counts healthy partitions only.
+
+Why *used* partitions too, not just the free ones.  kube-scheduler sees free = allocatable minus
+the requests of the pods bound to the node.  Withholding only the free partitions looks exact, but
+it races: when a pod on the draining GPU finishes, its request leaves the scheduler's sum at once
+while the plugin withholds the freed partition only on its next sync — with pods of that profile
+queued, the scheduler binds one immediately, kubelet admits it onto the freed (still healthy)
+partition, and under a standing queue the GPU never drains.  With every partition of the GPU
+unhealthy there is nothing to race for: a finished pod frees a request and an unhealthy device, so
+the next pod can only be admitted onto another GPU.  The price: while a GPU drains, the scheduler
+undercounts the node's free partitions *of that GPU's mode* by the partitions still in use there
+(none on a single-GPU node; the planner drains the least-used GPU).  Running containers are not
+affected by the health of their devices.
+
+The partition agent also patches the node's ``status.allocatable`` with the healthy counts right
+after each sync (kubelet's own node status sync runs every 10 s): between the partitioner writing a
+drain spec and the agent's sync a pod bound to the GPU's last free partitions would be rejected at
+admission; the agent reacts to the spec annotation within one watch event.
+
+When the agent flips the GPU and reports the new status, the spec matches again and the new
+partitions are advertised healthy — pushed through ``ListAndWatch`` (a new resource name registers
+one more plugin), no plugin restart.  The same pure function (:func:`partition_view`) drives the
+gRPC plugin on a node and the simulator's kubelet, so the drain the benchmark relies on is this
+production rule, not a simulator shortcut.
+
+``GetPreferredAllocation`` packs a request onto the GPU with the most partitions in use (idle GPUs
+stay idle for future flips); ``Allocate`` returns ``/dev/kfd`` and the partition's own render node
+(from the device map) — a CPX container sees exactly its partition.
+"""
+from __future__ import annotations
+
+import logging
+from collections import defaultdict
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, Iterable, List, Mapping, Set
+
+from .. import constant
+from ..device.protos import dp
+from ..models import annotation as ann
+from .server import DEVICE_PLUGIN_DIR, KUBELET_SOCKET, DeviceState, PluginManager, PluginServer, \
+    preferred_same_gpu
+
+log = logging.getLogger("nos.deviceplugin.partitions")
+
+LOST = "gpu left the device map"
+
+
+def reconfiguring_gpus(annotations: Mapping[str, str]) -> frozenset:
+    """GPUs whose spec annotations ask for a different geometry than their status reports (a GPU
+    without spec annotations is not being changed)."""
+    status, spec = ann.parse_node_annotations(dict(annotations or {}))
+    want: Dict[int, Dict[str, int]] = defaultdict(dict)
+    have: Dict[int, Dict[str, int]] = defaultdict(dict)
+    for a in spec:
+        want[a.index][a.profile] = want[a.index].get(a.profile, 0) + a.quantity
+    for a in status:
+        if a.quantity > 0:
+            have[a.index][a.profile] = have[a.index].get(a.profile, 0) + a.quantity
+    return frozenset(g for g, w in want.items() if {p: q for p, q in w.items() if q > 0} != have.get(g, {}))
+
+
+def draining_gpus(annotations: Mapping[str, str]) -> frozenset:
+    """Re-partitioning GPUs that still have partitions in use (they flip once their pods leave)."""
+    status, _ = ann.parse_node_annotations(dict(annotations or {}))
+    busy = {a.index for a in status if a.is_used() and a.quantity > 0}
+    return frozenset(g for g in reconfiguring_gpus(annotations) if g in busy)
+
+
+def resource_of(device: Any) -> str:
+    return f"{constant.AMD_RESOURCE_PREFIX}{device.compute_mode.lower()}_{device.memory_mode.lower()}"
+
+
+@dataclass(frozen=True)
+class PartitionDevice:
+    id: str
+    resource: str
+    gpu_index: int
+    partition_index: int
+    render_minor: int
+    healthy: bool
+    reason: str = ""
+    bdf: str = ""
+
+
+def partition_view(device_map: Any, withheld_gpus: Iterable[int], used_ids: Set[str],
+                   lost: Iterable[PartitionDevice] = ()) -> Dict[str, List[PartitionDevice]]:
+    """resource name -> the partitions to advertise, with their health (see the module docstring).
+    ``lost``: devices of GPUs that left the map since the last view, kept listed as unhealthy."""
+    withheld = frozenset(withheld_gpus)
+    out: Dict[str, List[PartitionDevice]] = defaultdict(list)
+    for d in device_map.devices:
+        r = resource_of(d)
+        held = d.gpu_index in withheld
+        why = ("gpu re-partitioning (in use, draining)" if d.device_id in used_ids else "gpu re-partitioning") \
+            if held else ""
+        out[r].append(PartitionDevice(d.device_id, r, d.gpu_index, d.partition_index, d.render_minor,
+                                      not held, why, d.bdf.lower()))
+    present = {d.id for ds in out.values() for d in ds}
+    for d in lost:
+        if d.id not in present:
+            out[d.resource].append(PartitionDevice(d.id, d.resource, d.gpu_index, d.partition_index, d.render_minor,
+                                                   False, LOST, d.bdf))
+    return {r: sorted(v, key=lambda x: (x.gpu_index, x.partition_index, x.id)) for r, v in out.items()}
+
+
+def preferred_partitions(view: List[PartitionDevice], must: List[str], available: List[str], size: int,
+                         withheld: Iterable[int] = ()) -> List[str]:
+    """GetPreferredAllocation for one container: one GPU, the most-used one first (GPUs being
+    re-partitioned are unhealthy, so kubelet never offers them)."""
+    gpu_of = {d.id: d.gpu_index for d in view}
+    total: Dict[int, int] = {}
+    for d in view:
+        total[d.gpu_index] = total.get(d.gpu_index, 0) + 1
+    return preferred_same_gpu(must, available, size, gpu_of, total, set(withheld))
+
+
+class PartitionState:
+    """The node-side inputs of the view: device map (amd-smi), node annotations (the partitioner's
+    spec, the reporter's status) and the partitions kubelet has allocated."""
+
+    def __init__(self, device_map: Callable[[], Any], annotations: Callable[[], Mapping[str, str]],
+                 used_ids: Callable[[], Set[str]]):
+        self._map = device_map
+        self._annotations = annotations
+        self._used = used_ids
+        self._last: Dict[str, PartitionDevice] = {}   # devices of the previous view, by id
+        self._lost: Dict[str, PartitionDevice] = {}   # devices of GPUs that left the map
+
+    def view(self) -> Dict[str, List[PartitionDevice]]:
+        try:
+            anns = self._annotations()
+        except Exception as e:  # noqa: BLE001 - without the spec nothing is known to be draining
+            log.warning("node annotations unavailable: %s", e)
+            anns = {}
+        try:
+            used = set(self._used())
+        except Exception as e:  # noqa: BLE001 - usage only labels the reason
+            log.warning("kubelet allocations unavailable: %s", e)
+            used = set()
+        withheld = reconfiguring_gpus(anns)
+        m = self._map()
+        bdfs = {g.bdf.lower() for g in m.gpus}
+        for d in self._last.values():
+            if d.bdf not in bdfs:
+                self._lost[d.id] = d
+        self._lost = {i: d for i, d in self._lost.items() if d.bdf not in bdfs}  # back on the bus
+        v = partition_view(m, withheld, used, self._lost.values())
+        self._last = {d.id: d for ds in v.values() for d in ds if d.bdf in bdfs}
+        return v
+
+
+class PartitionDevicePlugin(PluginServer):
+    """One ``amd.com/<mode>_<nps>`` resource of the node's compute partitions."""
+
+    def __init__(self, resource_name: str, state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
+                 poll_interval: float = 1.0):
+        super().__init__(resource_name, socket_dir, poll_interval, prefix="nos-xcp-")
+        self.state = state
+
+    def _devices(self) -> List[PartitionDevice]:
+        return self.state.view().get(self.resource_name, [])
+
+    def device_states(self) -> List[DeviceState]:
+        return [(d.id, d.healthy) for d in self._devices()]
+
+    def GetPreferredAllocation(self, req, ctx):
+        view = self._devices()
+        withheld = {d.gpu_index for d in view if not d.healthy}
+        resp = dp.PreferredAllocationResponse()
+        for cr in req.container_requests:
+            ids = preferred_partitions(view, list(cr.must_include_deviceIDs), list(cr.available_deviceIDs),
+                                       int(cr.allocation_size), withheld)
+            resp.container_responses.add(deviceIDs=ids)
+        return resp
+
+    def Allocate(self, req, ctx):
+        import grpc
+        by_id = {d.id: d for d in self._devices()}
+        resp = dp.AllocateResponse()
+        for cr in req.container_requests:
+            car = resp.container_responses.add()
+            nodes = []
+            for did in cr.devicesIDs:
+                d = by_id.get(did)
+                if d is None or not d.healthy:
+                    msg = f"partition {did} is not allocatable ({'unknown' if d is None else d.reason})"
+                    if ctx is not None:
+                        ctx.abort(grpc.StatusCode.FAILED_PRECONDITION, msg)
+                    raise KeyError(msg)
+                if d.render_minor >= 0:
+                    nodes.append(f"/dev/dri/renderD{d.render_minor}")
+            car.envs["NOS_PARTITION_IDS"] = ",".join(cr.devicesIDs)
+            car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
+            for n in sorted(set(nodes)):
+                car.devices.add(container_path=n, host_path=n, permissions="rw")
+        return resp
+
+
+def partition_plugin_manager(state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
+                             kubelet_socket: str = KUBELET_SOCKET, **kw: Any) -> PluginManager:
+    """A :class:`PluginManager` over the partition view: one plugin per resource name present (a
+    flip to a mode never served before registers its resource on the next sync)."""
+    return PluginManager(None, socket_dir=socket_dir, kubelet_socket=kubelet_socket,
+                         resources=lambda: sorted(state.view()),
+                         factory=lambda r: PartitionDevicePlugin(r, state, socket_dir), **kw)

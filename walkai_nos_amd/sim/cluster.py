@@ -51,68 +51,117 @@ DP_LABEL_KEY, DP_LABEL_VALUE = constant.DEFAULT_DEVICE_PLUGIN_LABEL.split("=")
 
 
 class SimDevicePlugin:
-    """xcp: one device per logical partition of each GPU (AMD device plugin, mixed naming);
-    cumask: one device per slice of the slice store (the nos device plugin)."""
+    """The device plugin of one simulated node, as kubelet sees it: ``advertised`` (every device id
+    per resource) and ``healthy`` (the ids kubelet may allocate; node allocatable counts these).
 
-    def __init__(self, smi: FakeAmdSmi, store: Optional[MemorySliceStore] = None):
+    * xcp, ``plugin="nos"`` (default) — the nos partition device plugin's own view
+      (:class:`~walkai_nos_amd.deviceplugin.partitions.PartitionState`: device map + node
+      annotations + allocated ids): free partitions of a GPU being re-partitioned are Unhealthy,
+      which is what enforces the pack policy's drain; updates are pushed (``refresh``);
+    * xcp, ``plugin="amd"`` — the AMD k8s-device-plugin: every logical device healthy, re-read only
+      when its pod is restarted (``reregister``); no drain enforcement;
+    * cumask — one device per slice of the slice store (the nos slice plugin)."""
+
+    def __init__(self, smi: FakeAmdSmi, store: Optional[MemorySliceStore] = None, plugin: str = "nos",
+                 annotations: Optional[Callable[[], Dict[str, str]]] = None,
+                 used: Optional[Callable[[], set]] = None):
         self.smi = smi
         self.store = store
+        self.plugin = plugin
         self.advertised: Dict[str, List[str]] = {}
+        self.healthy: Dict[str, List[str]] = {}
         self.registrations = 0
+        self.state = None
+        if store is None and plugin == "nos":
+            from ..deviceplugin.partitions import PartitionState
+            self.state = PartitionState(smi.device_map, annotations or (lambda: {}), used or (lambda: set()))
         self.reregister()
 
-    def current(self) -> Dict[str, List[str]]:
-        out: Dict[str, List[str]] = defaultdict(list)
+    def current(self) -> Dict[str, List[Tuple[str, bool]]]:
+        out: Dict[str, List[Tuple[str, bool]]] = defaultdict(list)
         if self.store is not None:
             for g, slices in sorted(self.store.load().items()):
                 for s in slices:
-                    out[slice_resource(s.profile)].append(s.id)
+                    out[slice_resource(s.profile)].append((s.id, True))
             return dict(out)
+        if self.state is not None:
+            return {r: [(d.id, d.healthy) for d in ds] for r, ds in self.state.view().items()}
         for d in self.smi.logical_devices():
-            out[f"amd.com/{d.compute_mode.lower()}_{d.memory_mode.lower()}"].append(d.device_id)
+            out[f"amd.com/{d.compute_mode.lower()}_{d.memory_mode.lower()}"].append((d.device_id, True))
         return dict(out)
 
+    def refresh(self) -> bool:
+        """Re-read the view (a pushed ListAndWatch update); True if anything kubelet sees changed.
+        The AMD plugin only re-reads when it is restarted."""
+        if self.store is None and self.state is None:
+            return False
+        return self._load()
+
+    def _load(self) -> bool:
+        cur = self.current()
+        adv = {r: [i for i, _ in v] for r, v in cur.items()}
+        ok = {r: [i for i, h in v if h] for r, v in cur.items()}
+        changed = adv != self.advertised or ok != self.healthy
+        self.advertised, self.healthy = adv, ok
+        return changed
+
     def reregister(self) -> None:
-        self.advertised = self.current()
+        self._load()
         self.registrations += 1
+
+    def withheld_gpus(self) -> frozenset:
+        return frozenset(self.smi.gpu_index_of(i) for r, ids in self.advertised.items()
+                         for i in set(ids) - set(self.healthy.get(r, ())))
 
 
 class SimKubelet:
-    """Device accounting for one node: allocatable from the device plugin, allocations per pod."""
+    """Device accounting for one node: allocatable = healthy devices of the plugin, allocations
+    per pod (admission picks healthy, unallocated devices through the plugin's preferred
+    allocation)."""
 
     def __init__(self, node_name: str, plugin: SimDevicePlugin, smi: FakeAmdSmi):
         self.node_name = node_name
         self.plugin = plugin
         self.smi = smi
         self.allocations: Dict[Tuple[str, str], List[Tuple[str, str]]] = {}
+        self.admission_failures = 0
 
     def used_ids(self) -> Dict[str, str]:
         return {i: r for devs in self.allocations.values() for r, i in devs}
 
-    def free_devices(self, resource: str, skip_gpus: frozenset = frozenset()) -> List[str]:
+    def free_devices(self, resource: str) -> List[str]:
         used = self.used_ids()
-        return [i for i in self.plugin.advertised.get(resource, []) if i not in used
-                and (not skip_gpus or self.smi.gpu_index_of(i) not in skip_gpus)]
+        return [i for i in self.plugin.healthy.get(resource, []) if i not in used]
 
-    def can_fit(self, req: Dict[str, int], skip_gpus: frozenset = frozenset()) -> bool:
-        return all(len(self.free_devices(r, skip_gpus)) >= q for r, q in req.items() if is_managed(r))
+    def can_fit(self, req: Dict[str, int]) -> bool:
+        return all(len(self.free_devices(r)) >= q for r, q in req.items() if is_managed(r))
 
-    def allocate(self, pod_key: Tuple[str, str], req: Dict[str, int],
-                 skip_gpus: frozenset = frozenset()) -> List[Tuple[str, str]]:
-        """GetPreferredAllocation semantics: pack onto the GPU that already has the most partitions
-        in use, so whole GPUs stay idle for future mode flips (fragmentation control)."""
+    def allocate(self, pod_key: Tuple[str, str], req: Dict[str, int]) -> List[Tuple[str, str]]:
+        """Admission: ``GetPreferredAllocation`` semantics — one GPU, the one with the most
+        partitions in use (whole GPUs stay idle for future mode flips), withheld GPUs last."""
+        from ..deviceplugin.server import preferred_same_gpu
         out: List[Tuple[str, str]] = []
+        used = self.used_ids()
+        withheld = self.plugin.withheld_gpus()
         for r, q in req.items():
             if not is_managed(r):
                 continue
-            free = self.free_devices(r, skip_gpus)
-            used_per_gpu: Dict[int, int] = defaultdict(int)
-            for i in self.used_ids():
-                used_per_gpu[self.smi.gpu_index_of(i)] += 1
-            free.sort(key=lambda i: (-used_per_gpu[self.smi.gpu_index_of(i)], self.smi.gpu_index_of(i), i))
+            free = self.free_devices(r)
             if len(free) < q:
                 raise RuntimeError(f"not enough {r} on {self.node_name}")
-            out.extend((r, i) for i in free[:q])
+            gpu_of = {i: self.smi.gpu_index_of(i) for i in self.plugin.advertised.get(r, [])}
+            total: Dict[int, int] = defaultdict(int)
+            for i in self.plugin.advertised.get(r, []):
+                total[gpu_of[i]] += 1
+            # "in use" per GPU counts every resource's allocations (the busiest GPU of the node)
+            in_use: Dict[int, int] = defaultdict(int)
+            for i in used:
+                in_use[self.smi.gpu_index_of(i)] += 1
+            avail_by_gpu: Dict[int, int] = defaultdict(int)
+            for i in free:
+                avail_by_gpu[gpu_of[i]] += 1
+            busy_total = {g: avail_by_gpu[g] + in_use[g] for g in total}
+            out.extend((r, i) for i in preferred_same_gpu([], free, q, gpu_of, busy_total, set(withheld)))
         self.allocations[pod_key] = out
         return out
 
@@ -120,10 +169,17 @@ class SimKubelet:
         self.allocations.pop(pod_key, None)
 
     def resource_client(self) -> StaticResourceClient:
+        # PodResources GetAllocatableResources lists every registered device, healthy or not
         return StaticResourceClient(lambda: [(r, i) for devs in self.allocations.values() for r, i in devs],
                                     lambda: [(r, i) for r, ids in self.plugin.advertised.items() for i in ids])
 
     def allocatable(self) -> Dict[str, str]:
+        out = {"cpu": "256", "memory": "2048Gi", "pods": "250"}
+        for r, ids in self.plugin.healthy.items():
+            out[r] = str(len(ids))
+        return out
+
+    def capacity(self) -> Dict[str, str]:
         out = {"cpu": "256", "memory": "2048Gi", "pods": "250"}
         for r, ids in self.plugin.advertised.items():
             out[r] = str(len(ids))
@@ -140,79 +196,63 @@ class SimNode:
     dp_counter: Any = field(default_factory=lambda: itertools.count(1))
 
 
-def draining_gpus(node: Optional[Dict[str, Any]]) -> frozenset:
-    """GPUs whose spec asks for a different geometry than the one they report while partitions
-    are in use: they wait for their pods to leave before the agent flips them, so no new pod may
-    land on their free partitions (the pack policy's drain, ``plan_cluster_pack`` step 5)."""
-    if node is None:
-        return frozenset()
-    from ..models import annotation as ann
-    status, spec = ann.parse_node_annotations(ko.annotations(node))
-    want: Dict[int, Dict[str, int]] = defaultdict(lambda: defaultdict(int))
-    have: Dict[int, Dict[str, int]] = defaultdict(lambda: defaultdict(int))
-    busy = set()
-    for a in spec:
-        want[a.index][a.profile] += a.quantity
-    for a in status:
-        have[a.index][a.profile] += a.quantity
-        if a.is_used() and a.quantity > 0:
-            busy.add(a.index)
-    return frozenset(g for g in busy if g in want and dict(want[g]) != dict(have[g]))
-
-
-class SimScheduler:
-    """Binds pending pods (first-fit over nodes ordered most-allocated first) or marks them
-    Unschedulable — the signal the partitioner reacts to."""
+class KubeScheduler:
+    """kube-scheduler semantics for ``default-scheduler`` pods: it knows nothing about GPUs,
+    partitions or drains — only node **allocatable** (what the device plugins report healthy, via
+    kubelet) minus the requests of the non-terminal pods bound to the node (NodeResourcesFit), the
+    default filters (``quota/filters.py``: NodeUnschedulable, NodeSelector, NodeAffinity,
+    TaintToleration) and MostAllocated scoring.  A pod that fits nowhere gets
+    ``PodScheduled=False/Unschedulable`` — the signal the partitioner reacts to.  The device a pod
+    gets on its node is kubelet's choice (``SimKubelet.allocate``), not the scheduler's."""
 
     KEY = Request("schedule-all")
 
-    def __init__(self, api_: InMemoryAPIServer, nodes: Dict[str, SimNode], on_bind: Callable[[Dict[str, Any], str], None]):
+    def __init__(self, api_: InMemoryAPIServer, nodes: Dict[str, SimNode], on_bind: Callable[[Dict[str, Any], str], None],
+                 scheduler_name: str = "default-scheduler"):
         self.api = api_
         self.nodes = nodes
         self.on_bind = on_bind
+        self.scheduler_name = scheduler_name
         self.bound = 0
 
     def reconcile(self, req: Request) -> Result:
-        pods = [p for p in self.api.list("Pod", field_selector="status.phase=Pending", copy=False)
-                if not podutil.is_scheduled(p)
-                and p["spec"].get("schedulerName", "default-scheduler") == "default-scheduler"]
-        pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
+        pods = self.api.list("Pod", copy=False)
+        pending = [p for p in pods if ko.pod_phase(p) == "Pending" and not podutil.is_scheduled(p)
+                   and p["spec"].get("schedulerName", "default-scheduler") == self.scheduler_name]
+        if not pending:
+            return Result()
+        pending.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
         node_objs = {n.name: self.api.get("Node", n.name) for n in self.nodes.values()}
-        draining = {name: draining_gpus(o) for name, o in node_objs.items()}
-        # per pass: free-device counts per (node, resource), recomputed only for a node that just
-        # took a pod, and filter verdicts per (node, scheduling constraints) — pods of one shape share
-        # them (the pass was O(pods x nodes x devices) at 64 nodes)
-        free: Dict[Tuple[str, str], int] = {}
-        verdict: Dict[Tuple[str, str], bool] = {}
-
-        def fits(n: SimNode, reqs: Dict[str, int]) -> bool:
-            for r, q in reqs.items():
-                if not is_managed(r):
-                    continue
-                k = (n.name, r)
-                if k not in free:
-                    free[k] = len(n.kubelet.free_devices(r, draining[n.name]))
-                if free[k] < q:
-                    return False
-            return True
-
-        def passes(p: Dict[str, Any], shape: str, n: SimNode) -> bool:
-            k = (n.name, shape)
-            if k not in verdict:
-                verdict[k] = filter_node(p, node_objs[n.name])[0]
-            return verdict[k]
-        unplaceable = set()  # (shape, request) that fit no node in this pass: free devices only shrink
+        free: Dict[str, Dict[str, int]] = {}
+        for name, o in node_objs.items():
+            free[name] = {r: v for r, v in res.from_k8s(ko.node_allocatable(o)).items() if is_managed(r)}
         for p in pods:
-            reqs = res.compute_pod_request(p)
+            nn = ko.pod_node_name(p)
+            if nn in free and not podutil.is_terminated(p):
+                for r, v in res.compute_pod_request(p).items():
+                    if is_managed(r):
+                        free[nn][r] = free[nn].get(r, 0) - v
+        verdict: Dict[Tuple[str, str], bool] = {}
+        unplaceable = set()
+        for p in pending:
+            reqs = {r: q for r, q in res.compute_pod_request(p).items() if is_managed(r)}
             spec = p["spec"]
             shape = repr((spec.get("nodeSelector"), spec.get("tolerations"), spec.get("affinity"),
                           spec.get("nodeName")))
-            rkey = (shape, tuple(sorted((r, q) for r, q in reqs.items() if is_managed(r))))
+            rkey = (shape, tuple(sorted(reqs.items())))
             target = None
             if rkey not in unplaceable:
-                order = sorted(self.nodes.values(), key=lambda n: (-len(n.kubelet.allocations), n.name))
-                target = next((n for n in order if passes(p, shape, n) and fits(n, reqs)), None)
-                if target is None:
+                cands = []
+                for name in sorted(free):
+                    k = (name, shape)
+                    if k not in verdict:
+                        verdict[k] = filter_node(p, node_objs[name])[0]
+                    if verdict[k] and all(free[name].get(r, 0) >= q for r, q in reqs.items()):
+                        cands.append(name)
+                if cands:
+                    # MostAllocated: the node with the least free GPU capacity left
+                    target = min(cands, key=lambda n: (sum(v for v in free[n].values() if v > 0), n))
+                else:
                     unplaceable.add(rkey)
             if target is None:
                 if not podutil.is_unschedulable(p):
@@ -225,24 +265,48 @@ class SimScheduler:
                         pass
                 continue
             try:
-                self.api.bind(ko.name(p), ko.namespace(p), target.name)
+                self.api.bind(ko.name(p), ko.namespace(p), target)
             except (Conflict, NotFound):
                 continue
             self.bound += 1
-            self.on_bind(p, target.name, draining[target.name])
-            for k in [k for k in free if k[0] == target.name]:
-                del free[k]
+            for r, q in reqs.items():
+                free[target][r] = free[target].get(r, 0) - q
+            self.on_bind(p, target)
         return Result()
+
+
+SimScheduler = KubeScheduler  # the simulator's scheduler is plain kube-scheduler semantics
+
+
+class _PushedPluginUpdate:
+    """The actuator's device-plugin hook with the nos partition plugin: no pod restart, the
+    plugin re-reads the device map and pushes the new devices (``PluginManager.restart``)."""
+
+    def __init__(self, cluster: "SimCluster", sn: SimNode):
+        self.cluster = cluster
+        self.sn = sn
+        self.pushes = 0
+
+    def restart(self, node: str, timeout: float = 60.0) -> None:
+        self.pushes += 1
+        self.sn.plugin.refresh()
+        self.cluster._refresh_node_status(self.sn)
 
 
 class SimCluster:
     def __init__(self, n_nodes: int = 1, gpus_per_node: int = 8, model: str = "MI355X",
                  kind: str = api.PARTITIONING_KIND_XCP, refresh_interval: float = 10.0,
                  batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None,
-                 scoring: str = "fraction", policy: str = "fifo", elastic_quota: bool = False):
+                 scoring: str = "fraction", policy: str = "fifo", elastic_quota: bool = False,
+                 device_plugin: str = "nos", pack: Any = None):
+        """``device_plugin``: ``nos`` (the nos partition plugin: drains enforced through device
+        health) or ``amd`` (the AMD k8s-device-plugin, restarted after flips: no drain enforcement)."""
+        if device_plugin not in ("nos", "amd"):
+            raise ValueError(f"unknown device plugin {device_plugin!r}")
         self.clock = clock or SimClock()
         self.api = InMemoryAPIServer(clock=self.clock)
         self.kind = kind
+        self.device_plugin = device_plugin
         self.gpus_per_node = gpus_per_node
         self.nodes: Dict[str, SimNode] = {}
         self.pod_seq = itertools.count()
@@ -250,12 +314,19 @@ class SimCluster:
         # control plane
         self.partitioner_mgr = Manager(self.api, clock=self.clock)
         self.pod_controllers, _ = setup_partitioner(self.partitioner_mgr, kinds=(kind,), batch_timeout=batch_timeout,
-                                                    batch_idle=batch_idle, scoring=scoring, policy=policy)
+                                                    batch_idle=batch_idle, scoring=scoring, policy=policy, pack=pack)
+        # kubelet (one controller for every simulated node): device plugin updates -> node status
+        self.kubelet_mgr = Manager(self.api, clock=self.clock)
+        self.kubelet_mgr.new_controller("sim-kubelet", self._kubelet_sync,
+                                        [Watch("Node", mapper=lambda o: [Request(ko.name(o))]),
+                                         Watch("Pod", mapper=lambda o: [Request(ko.pod_node_name(o))]
+                                               if ko.pod_node_name(o) else [])])
         self.scheduler_mgr = Manager(self.api, clock=self.clock)
         self.scheduler = SimScheduler(self.api, self.nodes, self._on_bind)
         self.scheduler_mgr.new_controller("sim-scheduler", self.scheduler.reconcile,
                                           [Watch("Pod", mapper=lambda o: [SimScheduler.KEY]),
                                            Watch("Node", mapper=lambda o: [SimScheduler.KEY])])
+        self.admission_failures = 0
         self.api.watch("Pod", self._on_pod_event, replay=False)
         self.quota_mgr: Optional[Manager] = None
         self.nos_scheduler = None
@@ -272,8 +343,17 @@ class SimCluster:
     def add_node(self, name: str, n_gpus: int, model: str, refresh_interval: float) -> SimNode:
         smi = FakeAmdSmi(n_gpus=n_gpus, model=model)
         store = MemorySliceStore() if self.kind == api.PARTITIONING_KIND_CUMASK else None
-        plugin = SimDevicePlugin(smi, store)
+        holder: Dict[str, SimKubelet] = {}
+
+        def node_annotations() -> Dict[str, str]:
+            try:
+                return ko.annotations(self.api.get("Node", name))
+            except NotFound:
+                return {}
+        plugin = SimDevicePlugin(smi, store, plugin=self.device_plugin, annotations=node_annotations,
+                                 used=lambda: set(holder["k"].used_ids()) if "k" in holder else set())
         kubelet = SimKubelet(name, plugin, smi)
+        holder["k"] = kubelet
         labels = {api.LABEL_GPU_PARTITIONING: self.kind, constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}",
                   constant.LABEL_AMD_GPU_COUNT: str(n_gpus), constant.LABEL_AMD_GPU_VRAM: "288G",
                   constant.LABEL_AMD_GPU_CU_COUNT: "256"}
@@ -282,8 +362,11 @@ class SimCluster:
         sn = SimNode(name, smi, plugin, kubelet, mgr)
         self.nodes[name] = sn
         self._create_dp_pod(sn)
-        dp = DevicePluginClient(self.api, namespace=DP_NAMESPACE, poll_interval=0.5, sleep=lambda s: self.clock.advance(s),
-                                clock=self.clock)
+        if store is None and self.device_plugin == "nos":
+            dp: Any = _PushedPluginUpdate(self, sn)  # the agent's PluginManager.restart(): a pushed update
+        else:
+            dp = DevicePluginClient(self.api, namespace=DP_NAMESPACE, poll_interval=0.5,
+                                    sleep=lambda s: self.clock.advance(s), clock=self.clock)
         if store is not None:
             sc = SlicingClient(kubelet.resource_client(), smi)
             setup_slice_agent(mgr, name, sc, store, device_plugin=dp, barrier_factory=lambda n: LocalBarrier(n),
@@ -315,12 +398,41 @@ class SimCluster:
             self.nodes[node].kubelet.release(ko.key(pod))
 
     def _refresh_node_status(self, sn: SimNode) -> None:
-        alloc = sn.kubelet.allocatable()
-        self.api.patch("Node", sn.name, {"status": {"allocatable": alloc, "capacity": alloc}})
+        """Publish the node's allocatable (healthy devices) and capacity (all devices) when they
+        changed (the partition agent's eager allocatable patch; kubelet's node status sync)."""
+        alloc, cap = sn.kubelet.allocatable(), sn.kubelet.capacity()
+        try:
+            cur = self.api.get("Node", sn.name).get("status", {})
+        except NotFound:
+            return
+        if cur.get("allocatable") == alloc and cur.get("capacity") == cap:
+            return
+        # a merge patch keeps keys it does not mention: resources that disappeared are nulled
+        gone = lambda old, new: {k: None for k in (old or {}) if k not in new}  # noqa: E731
+        self.api.patch("Node", sn.name, {"status": {"allocatable": {**gone(cur.get("allocatable"), alloc), **alloc},
+                                                    "capacity": {**gone(cur.get("capacity"), cap), **cap}}})
+
+    def _kubelet_sync(self, req: Request) -> Result:
+        sn = self.nodes.get(req.name)
+        if sn is not None:
+            sn.plugin.refresh()
+            self._refresh_node_status(sn)
+        return Result()
 
     def _on_bind(self, pod: Dict[str, Any], node: str, skip_gpus: frozenset = frozenset()) -> None:
-        """kubelet side of a binding: allocate devices (preferred allocation) and start the pod."""
-        self.nodes[node].kubelet.allocate(ko.key(pod), res.compute_pod_request(pod), skip_gpus)
+        """kubelet side of a binding: admission allocates healthy devices (the plugin's preferred
+        allocation) and starts the pod; a pod whose devices are not available is rejected
+        (``UnexpectedAdmissionError``, phase Failed), as kubelet does."""
+        sn = self.nodes[node]
+        sn.plugin.refresh()
+        try:
+            sn.kubelet.allocate(ko.key(pod), res.compute_pod_request(pod))
+        except RuntimeError as e:
+            self.admission_failures += 1
+            log.warning("admission of %s on %s failed: %s", ko.name(pod), node, e)
+            self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Failed", "reason": "UnexpectedAdmissionError",
+                                                            "message": str(e)}}, ko.namespace(pod))
+            return
         self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Running"}}, ko.namespace(pod))
         self.binds.append((self.clock(), ko.key(pod)[1], node))
 
@@ -345,7 +457,8 @@ class SimCluster:
     # -- driving ------------------------------------------------------------------------
     def managers(self) -> List[Manager]:
         extra = [self.quota_mgr] if self.quota_mgr is not None else []
-        return [self.scheduler_mgr, self.partitioner_mgr] + extra + [n.manager for n in self.nodes.values()]
+        return [self.kubelet_mgr, self.scheduler_mgr, self.partitioner_mgr] + extra + \
+            [n.manager for n in self.nodes.values()]
 
     def run(self, horizon: float = 30.0) -> float:
         return run_until_idle(self.managers(), self.clock, horizon=horizon)
