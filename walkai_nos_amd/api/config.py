@@ -129,7 +129,20 @@ class AgentConfig(ManagerConfig):
 
 @dataclass
 class MigAgentConfig(AgentConfig):
-    """Partition agent configuration (kind kept from the reference for config compatibility)."""
+    """Partition agent configuration (kind kept from the reference for config compatibility).
+
+    ``devicePlugin``: ``nos`` (default) — the agent serves the compute partitions itself
+    (``deviceplugin/partitions.py``) and enforces drains through device health; ``amd`` — the AMD
+    k8s-device-plugin serves them and is restarted after a flip (no drain enforcement: a GPU the
+    partitioner drains keeps receiving pods on its free partitions)."""
+    devicePlugin: str = "nos"
+    devicePluginDir: str = "/var/lib/kubelet/device-plugins"
+    publishAllocatable: bool = True         # patch node status.allocatable right after each plugin sync
+
+    def validate(self) -> None:
+        super().validate()
+        if self.devicePlugin not in ("nos", "amd"):
+            raise ValueError("devicePlugin must be 'nos' or 'amd'")
 
 
 @dataclass

@@ -6,6 +6,11 @@ node has at least one compute-partition-capable GPU and runs the start-up reconc
 (:meth:`Actuator.startup`: a plan journalled but not committed before a crash is rolled forward);
 then runs the reporter and the actuator sharing a :class:`SharedState`.
 
+Compute partitions are served by the agent's own nos partition device plugin (``devicePlugin:
+nos``, default): a GPU the partitioner drains has every partition reported Unhealthy, so no new pod
+lands on it, and a flip is pushed to kubelet through ListAndWatch instead of restarting a plugin
+pod (``devicePlugin: amd`` keeps the AMD k8s-device-plugin + restart path, without drains).
+
 The agent process never initialises HIP: the RCCL commit barrier (one communicator over every
 logical device of the re-enumerated node, 64 in CPX on 8 GPUs) and the probe-on-commit kernels run
 in spawned helper processes (``cmd/gpuhelper.py``) that exit before the next flip.
@@ -13,6 +18,7 @@ in spawned helper processes (``cmd/gpuhelper.py``) that exit before the next fli
 from __future__ import annotations
 
 import logging
+import os
 import sys
 
 from .. import constant
@@ -22,6 +28,8 @@ from ..device.amdsmi import new_backend
 from ..device.deviceplugin_client import DevicePluginClient
 from ..device.partition_client import PartitionClient
 from ..device.podresources import PodResourcesClient
+from ..kube.runtime import Watch
+from ..utils.predicates import AnnotationsChanged, ExcludeDelete, MatchingName
 from ..utils.util import get_env_or_panic
 from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
 
@@ -33,6 +41,23 @@ def node_barrier_factory(registry, backend: str = "rccl"):
     passes one vote per device of the re-enumerated map)."""
     from ..parallel.spawned import SpawnedNodeBarrier
     return lambda n: SpawnedNodeBarrier(n, backend=backend, registry=registry)
+
+
+def nos_partition_plugin(client, node: str, smi, resources, cfg):
+    """The nos partition device plugin of this node: its view (device map, the node's spec/status
+    annotations, kubelet's allocated ids), one gRPC plugin per ``amd.com/<mode>_<nps>`` resource,
+    and the hook the actuator calls after a flip."""
+    from ..deviceplugin.partitions import AllocatablePublisher, PartitionPluginHook, PartitionState, \
+        partition_plugin_manager
+    from ..kube import objects as ko
+
+    def used_ids():
+        return {d.device_id for d in resources.get_used_devices()}
+    state = PartitionState(smi.device_map, lambda: ko.annotations(client.get("Node", node)), used_ids)
+    plugins = partition_plugin_manager(state, socket_dir=cfg.devicePluginDir,
+                                       kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"))
+    publisher = AllocatablePublisher(client, node) if cfg.publishAllocatable else None
+    return PartitionPluginHook(plugins, state, publisher), plugins
 
 
 def main(argv=None) -> int:
@@ -48,8 +73,14 @@ def main(argv=None) -> int:
         return 1
     resources = PodResourcesClient(cfg.podResourcesSocket)
     pc = PartitionClient(resources, smi)
-    dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
     mgr = make_manager(client, cfg, "partitionagent")
+    plugins = None
+    if cfg.devicePlugin == "nos":
+        dp, plugins = nos_partition_plugin(client, node, smi, resources, cfg)
+        mgr.new_controller("nos-partition-plugin", dp.reconcile,
+                           [Watch("Node", [ExcludeDelete(), MatchingName(node), AnnotationsChanged()])])
+    else:
+        dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
     from ..parallel.spawned import HelperRegistry
     helpers = HelperRegistry()
     bf = node_barrier_factory(helpers) if cfg.commitBarrier == "rccl" else None
@@ -65,7 +96,14 @@ def main(argv=None) -> int:
     from ..exporters.gpu_metrics import GpuMetricsPoller
     GpuMetricsPoller(smi, node).register(mgr)
     serve_endpoints(mgr, cfg)
-    return run_until_signal(mgr)
+    stop = None
+    if plugins is not None:
+        import threading
+        from ..deviceplugin.server import run_forever
+        stop = threading.Event()
+        threading.Thread(target=run_forever, args=(plugins, 2.0, stop), name="nos-partition-plugins",
+                         daemon=True).start()
+    return run_until_signal(mgr, stop) if stop is not None else run_until_signal(mgr)
 
 
 if __name__ == "__main__":

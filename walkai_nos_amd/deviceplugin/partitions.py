@@ -47,7 +47,7 @@ from __future__ import annotations
 import logging
 from collections import defaultdict
 from dataclasses import dataclass
-from typing import Any, Callable, Dict, Iterable, List, Mapping, Set
+from typing import Any, Callable, Dict, Iterable, List, Mapping, Optional, Set
 
 from .. import constant
 from ..device.protos import dp
@@ -218,3 +218,61 @@ def partition_plugin_manager(state: PartitionState, socket_dir: str = DEVICE_PLU
     return PluginManager(None, socket_dir=socket_dir, kubelet_socket=kubelet_socket,
                          resources=lambda: sorted(state.view()),
                          factory=lambda r: PartitionDevicePlugin(r, state, socket_dir), **kw)
+
+
+class AllocatablePublisher:
+    """Patches the node's ``status.allocatable`` with the healthy partition counts of a view (the
+    partition agent's eager update: kubelet's own node status sync runs every 10 s, and a scheduler
+    reading a stale allocatable would bind pods that kubelet then rejects at admission)."""
+
+    def __init__(self, client: Any, node: str):
+        self.client = client
+        self.node = node
+        self.patches = 0
+
+    def publish(self, view: Mapping[str, List[PartitionDevice]]) -> bool:
+        want = {r: str(sum(1 for d in ds if d.healthy)) for r, ds in view.items()}
+        try:
+            cur = (self.client.get("Node", self.node).get("status") or {}).get("allocatable") or {}
+        except Exception as e:  # noqa: BLE001 - kubelet's own sync still gets there
+            log.warning("node %s unavailable for the allocatable update: %s", self.node, e)
+            return False
+        # partition resources no longer served drop to 0 (kubelet keeps a registered resource at 0)
+        for r in cur:
+            if r.startswith(constant.AMD_RESOURCE_PREFIX) and r not in want and _is_partition_resource(r):
+                want[r] = "0"
+        if all(cur.get(r) == v for r, v in want.items()):
+            return False
+        self.client.patch("Node", self.node, {"status": {"allocatable": want}})
+        self.patches += 1
+        return True
+
+
+def _is_partition_resource(r: str) -> bool:
+    from ..models.xcp.profile import is_xcp_resource
+    return is_xcp_resource(r)
+
+
+class PartitionPluginHook:
+    """The partition agent's device-plugin hook (``Actuator._reregister`` calls ``restart``): sync
+    the plugins — a pushed ListAndWatch update, no pod restart — and publish the allocatable."""
+
+    def __init__(self, manager: PluginManager, state: PartitionState,
+                 publisher: Optional[AllocatablePublisher] = None):
+        self.manager = manager
+        self.state = state
+        self.publisher = publisher
+
+    def restart(self, node: str = "", timeout: float = 60.0) -> None:
+        try:
+            self.manager.sync()
+        finally:
+            if self.publisher is not None:
+                self.publisher.publish(self.state.view())
+
+    def reconcile(self, req: Any) -> Any:
+        """Controller entry point: the node's annotations changed (a new spec = a drain starts, a new
+        status = a flip committed)."""
+        from ..kube.runtime import Result
+        self.restart()
+        return Result()

@@ -138,7 +138,7 @@ class RESTClient:
 
     def patch(self, kind: str, name: str, patch: Obj, namespace: str = "") -> Obj:
         sub = ""
-        if set(patch) == {"status"} and kind in ("Pod", "ElasticQuota", "CompositeElasticQuota"):
+        if set(patch) == {"status"} and kind in ("Pod", "Node", "ElasticQuota", "CompositeElasticQuota"):
             sub = "status"
         return self._req("PATCH", self._path(kind, name, namespace, sub), patch,
                          content_type="application/merge-patch+json")
