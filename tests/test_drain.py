@@ -249,3 +249,43 @@ def test_partition_agent_wiring_publishes_allocatable_on_a_drain():
         finally:
             plugins.stop()
             reg.stop()
+
+
+def test_slice_plugin_render_nodes_health_and_kubelet_restart():
+    """The CU-mask slice plugin: render node of a slice's GPU from the device map (not /dev/dri
+    order), Unhealthy when its GPU leaves the map, re-served and re-registered after a kubelet
+    restart (sockets wiped, kubelet.sock recreated)."""
+    from walkai_nos_amd.device.slicing_client import MemorySliceStore
+    from walkai_nos_amd.deviceplugin.server import PluginManager
+    from walkai_nos_amd.models.slicing.cumask import Slice
+    smi = FakeAmdSmi(n_gpus=2)
+    dm = smi.device_map()
+    b0, b1 = dm.gpus[0].bdf, dm.gpus[1].bdf
+    store = MemorySliceStore()
+    store.save({0: [Slice(f"{b0}::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9)],
+                1: [Slice(f"{b1}::s0", "32cu.36gb", [0, 1, 2, 3], 36 * 10**9)]})
+    with tempfile.TemporaryDirectory() as d:
+        reg = RegistrationServer(os.path.join(d, "kubelet.sock")).start()
+        # a wrong directory-order fallback: the device map must win
+        mgr = PluginManager(store, {0: "/dev/dri/renderD999", 1: "/dev/dri/renderD998"}, socket_dir=d,
+                            kubelet_socket=reg.socket, device_map=smi.device_map, register_backoff=0.01)
+        try:
+            mgr.sync()
+            plug = mgr.plugins["amd.com/gpu-32cu.36gb"]
+            a = dp.AllocateRequest()
+            a.container_requests.add(devicesIDs=[f"{b1}::s0"])
+            r = plug.Allocate(a, None).container_responses[0]
+            assert [x.host_path for x in r.devices] == ["/dev/kfd", f"/dev/dri/renderD{dm.devices[1].render_minor}"]
+            assert plug.device_states() == [(f"{b0}::s0", True), (f"{b1}::s0", True)]
+            smi._gpus.pop(1)
+            smi.enumerate(reinit=True)
+            assert plug.device_states() == [(f"{b0}::s0", True), (f"{b1}::s0", False)]
+            reg.stop()
+            for f in os.listdir(d):
+                os.unlink(os.path.join(d, f))
+            reg2 = RegistrationServer(os.path.join(d, "kubelet.sock")).start()
+            mgr.sync()
+            assert [r.resource_name for r in reg2.registered] == ["amd.com/gpu-32cu.36gb"] and plug.serving()
+            reg2.stop()
+        finally:
+            mgr.stop()

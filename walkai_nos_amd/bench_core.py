@@ -144,6 +144,7 @@ class BenchConfig:
     nodes: int = 1                       # cluster nodes of `gpus` GPUs (control-plane simulation only)
     device_plugin: str = "nos"           # nos (drain enforced by device health) | amd (no drain enforcement)
     pack: Optional[Dict[str, float]] = None  # PackParams overrides (field name -> value)
+    arrivals: str = "steady"             # steady (constant rate, seeded phase) | poisson
 
     def __post_init__(self) -> None:
         if self.flip_cost_s < 0:
@@ -173,6 +174,7 @@ class ChurnProcess:
         self.rate = cfg.offered_load * cfg.gpus * cfg.nodes / (mean_frac * cfg.mean_lifetime_quanta)
         self._profiles: List[str] = []
         self._lifetimes: List[int] = []
+        self._acc: Optional[float] = None
 
     def _next_profile(self) -> str:
         if not self._profiles:
@@ -182,13 +184,21 @@ class ChurnProcess:
         return self._profiles.pop()
 
     def arrivals(self) -> List[str]:
-        # Poisson(rate) via inversion, seeded
-        n, p, L = 0, 1.0, math.exp(-self.rate)
-        while True:
-            p *= self.rng.random()
-            if p <= L:
-                break
-            n += 1
+        if self.cfg.arrivals == "poisson":
+            # Poisson(rate) via inversion, seeded
+            n, p, L = 0, 1.0, math.exp(-self.rate)
+            while True:
+                p *= self.rng.random()
+                if p <= L:
+                    break
+                n += 1
+        else:
+            # constant rate (a load generator submitting pods at a steady pace), seeded phase
+            if self._acc is None:
+                self._acc = self.rng.random()
+            self._acc += self.rate
+            n = int(self._acc)
+            self._acc -= n
         return [self._next_profile() for _ in range(n)]
 
     def lifetime(self) -> int:

@@ -41,8 +41,10 @@ def main(argv=None) -> int:
     store = ConfigMapSliceStore(client, node)
     sc = SlicingClient(PodResourcesClient(cfg.podResourcesSocket), smi)
     mgr = make_manager(client, cfg, "sliceagent")
+    # render nodes and slice health come from the device map (a slice whose GPU left the map is
+    # Unhealthy); the sysfs listing is only the fallback for a map without render minors
     plugins = PluginManager(store, render_nodes_from_sysfs(), cu_count=gpus[0].cu_count or 256,
-                            shim_path=cfg.hbmLimitShimPath)
+                            shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map)
 
     class Notify:
         def restart(self, node_name, timeout=60):

@@ -188,7 +188,8 @@ def _mode_of(gpu: Any) -> Optional[str]:
 def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[str, int], float]],
                       incoming: Optional[Mapping[str, int]] = None, params: Optional[PackParams] = None,
                       spx_demand: float = 0.0,
-                      mode_age: Optional[Callable[[str, int], float]] = None) -> Dict[str, NodeModel]:
+                      mode_age: Optional[Callable[[str, int], float]] = None,
+                      last_served: Optional[Mapping[str, float]] = None) -> Dict[str, NodeModel]:
     """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
     reference's "first node that can change wins").
 
@@ -301,7 +302,8 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
             fill = min(d, 1.0)
             if fill + 1e-9 < params.min_fill and not starving:
                 continue
-            key = (1 if starving else 0, fill, oldest.get(p, 0.0))
+            # starving profiles: the longest wait first (FIFO across profiles); otherwise the fullest
+            key = (1, oldest.get(p, 0.0), fill) if starving else (0, fill, oldest.get(p, 0.0))
             if best is None or key > best[0]:
                 best = (key, p)
         if best is None:
@@ -338,7 +340,11 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
     served = {_mode_of(g) for m in current.values() for g in m.gpus} | draining_to
     used_of = (lambda g: g.used_fraction(lambda q: round(1.0 / frac(q)))) if w is not None else \
         (lambda g: float(sum(g.used.values())))
-    for p in sorted(demand, key=lambda q: -oldest.get(q, 0.0)):
+    # round robin: the profile served least recently (no GPU in its mode for longest) drains first,
+    # then the oldest waiting pod — oldest-first alone lets the profiles with the longest queues
+    # take turn after turn while a shorter queue's pods keep waiting
+    order = sorted(demand, key=lambda q: ((last_served or {}).get(q, float("-inf")), -oldest.get(q, 0.0)))
+    for p in order:
         if p in draining_to:
             continue
         backlog = demand[p] >= params.drain_backlog - 1e-9 and oldest.get(p, 0.0) >= params.drain_after
@@ -449,6 +455,7 @@ class PodController:
         self.pack = pack or PackParams()
         self._first_seen: Dict[str, float] = {}   # pending pod uid -> first time the planner saw it
         self._mode_since: Dict[Tuple[str, int], Tuple[Optional[str], float]] = {}  # (node, gpu) -> (mode, since)
+        self._last_served: Dict[str, float] = {}  # profile -> last time a GPU was in its mode
         self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
@@ -547,6 +554,15 @@ class PodController:
             if sum(m.free().get(p, 0) for m in models.values()) < q:
                 return False
         return True
+
+    def _served(self, models: Mapping[str, NodeModel], now: float) -> Dict[str, float]:
+        """Last time each profile had a GPU in its mode (the round robin of the drain rules)."""
+        for m in models.values():
+            for g in getattr(m, "gpus", []):
+                mode = _mode_of(g)
+                if mode is not None:
+                    self._last_served[mode] = now
+        return dict(self._last_served)
 
     def _mode_ages(self, models: Mapping[str, NodeModel], now: float) -> Callable[[str, int], float]:
         """Track when each GPU's reported mode last changed (first sight counts as long ago)."""
@@ -660,7 +676,7 @@ class PodController:
             pend = self.pending_with_age()
             self._update_spx_demand(nodes, pend)
             changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand,
-                                        self._mode_ages(models, now))
+                                        self._mode_ages(models, now), self._served(models, now))
             need = requested
         elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}
