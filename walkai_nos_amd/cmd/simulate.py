@@ -1,9 +1,14 @@
 """Run the whole nos control plane on the in-process cluster and print utilisation / density per
 step (the ``kind``-cluster scenario of BASELINE.json config 1, no GPU needed).
 
-Uses the bench's outage model: every compute-partition flip darkens its GPU for ``--flip-cost``
-seconds (``--quantum`` seconds per step), during which it counts as unallocated and its pods
-neither serve nor age; ``util_pct`` is that effective allocation."""
+``--scenario churn`` (default) uses the bench's model: one step = ``--cluster-s`` seconds of
+cluster time; every compute-partition flip darkens its GPU for ``--flip-cost`` seconds (default:
+the measured components), during which it counts as unallocated and its pods neither serve nor
+age; ``util_pct`` is that effective allocation; per-profile time-to-schedule is reported.
+
+``--scenario erq``: Elastic Resource Quota on an xcp node under churn (``sim/erq.py``): team A
+borrows team B's idle share, team B reclaims it through nos-scheduler preemption; reports the
+reclaim latency and each team's ``used`` against its ``min``."""
 from __future__ import annotations
 
 import argparse
@@ -23,14 +28,24 @@ def main(argv=None) -> int:
     ap.add_argument("--load", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
-    ap.add_argument("--flip-cost", type=float, default=2.0)
-    ap.add_argument("--quantum", type=float, default=0.5)
+    ap.add_argument("--flip-cost", type=float, default=-1.0, help="seconds per flip (default: measured components)")
+    ap.add_argument("--cluster-s", type=float, default=60.0, help="cluster seconds per step")
     ap.add_argument("--preroll", type=int, default=60)
+    ap.add_argument("--scenario", default="churn", choices=("churn", "erq"))
     ap.add_argument("--quiet", action="store_true", help="print only the summary line")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
+    if args.scenario == "erq":
+        from ..sim.erq import run_erq_churn
+        r = run_erq_churn(gpus=args.gpus, epochs=args.epochs, seed=args.seed, cluster_s=args.cluster_s)
+        samples = r.pop("samples")
+        if not args.quiet:
+            for x in samples:
+                print(json.dumps(x))
+        print(json.dumps(r))
+        return 0
     nb = NodeBench(BenchConfig(gpus=args.gpus, nodes=args.nodes, offered_load=args.load, seed=args.seed,
-                               policy=args.policy, flip_cost_s=args.flip_cost, quantum_s=args.quantum),
+                               policy=args.policy, flip_cost_s=args.flip_cost, cluster_s=args.cluster_s),
                    gpu_data_plane=False)
     for _ in range(args.preroll):
         nb.control_step()
@@ -48,8 +63,9 @@ def main(argv=None) -> int:
                       "mean_util_pct": round(sum(nb.util_samples) / len(nb.util_samples), 2),
                       "mean_pods_per_node": round(sum(nb.pods_samples) / len(nb.pods_samples) / args.nodes, 2),
                       "pending_mean": round(sum(nb.pending_samples) / len(nb.pending_samples), 2),
-                      "pending_max": max(nb.pending_samples), "flips": nb.flips, "flip_cost_s": args.flip_cost,
-                      "time_in_flip_pct": round(100.0 * nb.outage_gpu_steps / max(1, nb.gpu_steps), 2),
+                      "pending_max": max(nb.pending_samples), "flips": nb.flips, "flip_cost_s": nb.cfg.flip_cost_s,
+                      "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
+                      "per_profile": nb.profile_report(args.epochs * nb.cfg.quantum_s),
                       "control_plane_ms_per_epoch": round(1000 * dt / args.epochs, 2)}))
     return 0
 

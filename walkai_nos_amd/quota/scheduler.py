@@ -21,6 +21,7 @@ with the same extension points:
 from __future__ import annotations
 
 import logging
+import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -123,14 +124,18 @@ def _neg_ts(p: Dict[str, Any]) -> str:
 
 class NosScheduler:
     def __init__(self, client: Any, calculator: Optional[GpuMemoryCalculator] = None,
-                 on_bind: Optional[Callable[[Dict[str, Any], str], None]] = None, scheduler_name: str = SCHEDULER_NAME):
+                 on_bind: Optional[Callable[[Dict[str, Any], str], None]] = None, scheduler_name: str = SCHEDULER_NAME,
+                 clock: Callable[[], float] = time.time):
         self.client = client
         self.calc = calculator or GpuMemoryCalculator()
         self.plugin = CapacityScheduling(self.calc)
         self.on_bind = on_bind
         self.scheduler_name = scheduler_name
+        self.clock = clock
         self.bound = 0
         self.preempted = 0
+        self._preempted_for: Dict[str, float] = {}  # preemptor -> when its first victims were evicted
+        self.reclaim_latency_s: List[float] = []    # preemption -> preemptor bound
 
     KEY = Request("nos-scheduler-cycle")
 
@@ -205,6 +210,10 @@ class NosScheduler:
             state.node_free[node] = res.subtract(state.node_free[node], req_)
             state.node_pods[node].append(pod)
             self.bound += 1
+            t = self._preempted_for.pop(_pkey(pod), None)
+            if t is not None:
+                self.reclaim_latency_s.append(self.clock() - t)
+                REGISTRY.phase_seconds.labels(phase="quota_reclaim").observe(self.clock() - t)
             if self.on_bind is not None:
                 self.on_bind(pod, node)
         return Result(requeue_after=1.0) if retry else Result()
@@ -221,6 +230,7 @@ class NosScheduler:
         if best is None:
             return False
         _, node, victims = best
+        self._preempted_for.setdefault(_pkey(pod), self.clock())
         for v in victims:
             try:
                 self.client.delete("Pod", ko.name(v), ko.namespace(v))
@@ -238,7 +248,7 @@ class NosScheduler:
 
 def setup_nos_scheduler(mgr: Manager, calculator: Optional[GpuMemoryCalculator] = None,
                         on_bind: Optional[Callable[[Dict[str, Any], str], None]] = None) -> NosScheduler:
-    s = NosScheduler(mgr.client, calculator, on_bind)
+    s = NosScheduler(mgr.client, calculator, on_bind, clock=mgr.clock)
     to_cycle = lambda o: [NosScheduler.KEY]  # noqa: E731
     mgr.new_controller("nos-scheduler", s.reconcile,
                        [Watch("Pod", mapper=to_cycle), Watch("Node", mapper=to_cycle),
