@@ -1,5 +1,11 @@
 // nos-gpuhelper: the partition agent's short-lived GPU helper as a native executable.
 //
+//   nos-gpuhelper barrier --votes 1,1,0,... [--expect N] [--backend xgmi|rccl]
+//
+// ``xgmi`` (default): a ring of peer-to-peer token writes over xGMI (csrc/p2p_barrier.hip) — every
+// device executes, every link of the ring carries its token; ``rccl``: one ncclCommInitAll clique
+// and a grouped 4-byte all-reduce (csrc/rccl_barrier.cpp).
+//
 // The agent never initialises HIP itself (a KFD context in the agent would make every later mode
 // switch fail with "busy"), so each node-atomic commit runs in a child process spawned after the
 // flips. The Python helper (walkai_nos_amd/cmd/gpuhelper.py) spent 0.7 s starting an interpreter
@@ -7,9 +13,7 @@
 // (profiles/operator_gpu_report_r2.json); this executable starts in milliseconds and reports where
 // the rest goes, phase by phase:
 //
-//   nos-gpuhelper barrier --votes 1,1,0,... [--expect N]
-//
-// prints ONE JSON line: n (votes), seen (HIP devices), sum, and the wall milliseconds of
+// Either way it prints ONE JSON line: n (votes), seen (HIP devices), sum, and the wall milliseconds of
 // hip_init (hipInit + device count), comm_init (ncclCommInitAll over every device), allreduce (one
 // grouped 4-byte sum), destroy, total. A device count different from --expect (or from the number
 // of votes) is a veto: a partition that did not come up after the flip. RCCL init tunables that
@@ -30,6 +34,8 @@ const char* nos_barrier_last_error();
 int nos_barrier_init_all(int ndev, const int* devlist, void** handle);
 int nos_barrier_allreduce_all(void* handle, const int32_t* votes, int32_t* result);
 int nos_barrier_destroy_all(void* handle);
+const char* nos_p2p_last_error();
+int nos_p2p_barrier(int n, const int32_t* votes, int32_t* sum, int32_t* intact);
 }
 
 namespace {
@@ -65,7 +71,7 @@ void tune_rccl_env() {
   for (auto& p : kv) setenv(p[0], p[1], /*overwrite=*/0);
 }
 
-int barrier(const std::vector<int32_t>& votes, int expect) {
+int barrier(const std::vector<int32_t>& votes, int expect, const std::string& backend) {
   auto t0 = Clock::now();
   tune_rccl_env();
   std::string err;
@@ -82,6 +88,16 @@ int barrier(const std::vector<int32_t>& votes, int expect) {
   } else if (seen != want || seen != int(votes.size())) {
     err = "helper sees " + std::to_string(seen) + " HIP devices, the device map has " + std::to_string(want) +
           " (" + std::to_string(votes.size()) + " votes)";
+  } else if (backend == "xgmi") {
+    auto t1 = Clock::now();
+    int32_t intact = 0;
+    int rc = nos_p2p_barrier(seen, votes.data(), &sum, &intact);
+    comm_init = 0;
+    allreduce = ms_since(t1);
+    if (rc != 0)
+      err = std::string("p2p ring: ") + nos_p2p_last_error();
+    else if (intact != seen)
+      err = std::to_string(seen - intact) + " token(s) did not arrive intact over the ring";
   } else {
     std::vector<int> devs(seen);
     for (int i = 0; i < seen; ++i) devs[i] = i;
@@ -106,8 +122,10 @@ int barrier(const std::vector<int32_t>& votes, int expect) {
     }
   }
   std::printf("{\"n\": %zu, \"seen\": %d, \"sum\": %d, \"hip_init_ms\": %.3f, \"comm_init_ms\": %.3f, "
-              "\"allreduce_ms\": %.3f, \"destroy_ms\": %.3f, \"total_ms\": %.3f, \"native\": true",
-              votes.size(), seen, err.empty() ? sum : 0, hip_init, comm_init, allreduce, destroy, ms_since(t0));
+              "\"allreduce_ms\": %.3f, \"destroy_ms\": %.3f, \"total_ms\": %.3f, \"native\": true, "
+              "\"backend\": \"%s\"",
+              votes.size(), seen, err.empty() ? sum : 0, hip_init, comm_init, allreduce, destroy, ms_since(t0),
+              backend.c_str());
   if (!err.empty()) std::printf(", \"error\": \"%s\"", json_escape(err).c_str());
   std::printf("}\n");
   std::fflush(stdout);
@@ -115,7 +133,7 @@ int barrier(const std::vector<int32_t>& votes, int expect) {
 }
 
 int usage() {
-  std::fprintf(stderr, "usage: nos-gpuhelper barrier --votes 1,1,0 [--expect N]\n");
+  std::fprintf(stderr, "usage: nos-gpuhelper barrier --votes 1,1,0 [--expect N] [--backend xgmi|rccl]\n");
   return 2;
 }
 }  // namespace
@@ -126,6 +144,7 @@ int main(int argc, char** argv) {
   if (cmd != "barrier") return usage();
   std::vector<int32_t> votes;
   int expect = -1;
+  std::string backend = "xgmi";
   for (int i = 2; i < argc; ++i) {
     std::string a = argv[i];
     if (a == "--votes" && i + 1 < argc) {
@@ -141,11 +160,12 @@ int main(int argc, char** argv) {
     } else if (a == "--expect" && i + 1 < argc) {
       expect = std::atoi(argv[++i]);
     } else if (a == "--backend" && i + 1 < argc) {
-      ++i;  // accepted for command-line compatibility with the Python helper (always rccl here)
+      backend = argv[++i];
+      if (backend != "xgmi" && backend != "rccl") return usage();
     } else {
       return usage();
     }
   }
   if (votes.empty()) return usage();
-  return barrier(votes, expect);
+  return barrier(votes, expect, backend);
 }

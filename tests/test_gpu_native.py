@@ -73,6 +73,21 @@ def test_rccl_commit_barrier_single_rank(gpu):
         b.close()
 
 
+def test_xgmi_p2p_commit_barrier_in_the_native_helper(gpu):
+    """The agent's default commit barrier: the native helper writes each device's vote over the
+    P2P ring and reads it back; a no-vote and a device-count mismatch veto; well under a second."""
+    from walkai_nos_amd.parallel.spawned import SpawnedNodeBarrier
+    import torch
+    n = torch.cuda.device_count()
+    b = SpawnedNodeBarrier(n, backend="xgmi", native=True, timeout=120.0)
+    assert b.vote_all([True] * n) is True, b.last
+    assert b.last["backend"] == "xgmi" and b.last["sum"] == n and "error" not in b.last
+    assert b.last["wall_ms"] < 1000.0, b.last
+    assert b.vote_all([False] + [True] * (n - 1)) is False
+    assert b.last["sum"] == n - 1 and "error" not in b.last       # the no-vote arrived, and vetoed
+    assert SpawnedNodeBarrier(n + 1, backend="xgmi", native=True).vote_all([True] * (n + 1)) is False
+
+
 def test_hbm_limit_shim_enforces_budget(gpu):
     shim = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
     code = ("import torch\n"

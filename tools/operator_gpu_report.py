@@ -4,7 +4,8 @@
   and a timed re-enumeration (the step every flip pays);
 * the spawned commit-barrier helper: wall time of a vote including process spawn, HIP init and
   ncclCommInitAll over every logical device, and its own phase split (the agent pays this per
-  commit because a flip changes the device set) — native executable vs the Python helper;
+  commit because a flip changes the device set) — the xGMI P2P token ring vs the RCCL
+  communicator, native executable vs the Python helper;
 * the spawned probe round on every logical device;
 * amd-smi power / clock / activity at rest.
 
@@ -39,16 +40,17 @@ def main() -> int:
     # the commit barrier per helper flavour: native executable with the init tunables (the agent's
     # default), native with RCCL's default init, and the round-2 Python helper; a first call on a
     # fresh box pays cold file-cache costs, so every flavour runs 4 times (1 vetoed)
-    flavours = {"native_tuned": ({}, True), "native_rccl_defaults": ({"NOS_BARRIER_KEEP_NCCL_ENV": "1"}, True),
-                "python": ({}, False)}
+    flavours = {"native_xgmi": ({}, True, "xgmi"), "native_rccl": ({}, True, "rccl"),
+                "native_rccl_defaults": ({"NOS_BARRIER_KEEP_NCCL_ENV": "1"}, True, "rccl"),
+                "python_rccl": ({}, False, "rccl")}
     out["commit_barrier"] = {}
-    for name, (env, native) in flavours.items():
+    for name, (env, native, backend) in flavours.items():
         votes = []
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
             for ok in (True, True, True, False):
-                b = SpawnedNodeBarrier(n, backend="rccl", native=native)
+                b = SpawnedNodeBarrier(n, backend=backend, native=native)
                 t0 = time.perf_counter()
                 res = b.vote_all([ok] * n)
                 votes.append({"votes_ok": ok, "result": res, "wall_ms": round(1e3 * (time.perf_counter() - t0), 1),

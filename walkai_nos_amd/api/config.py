@@ -114,7 +114,7 @@ class AgentConfig(ManagerConfig):
     devicePluginLabel: str = constant.DEFAULT_DEVICE_PLUGIN_LABEL
     devicePluginNamespace: str = ""
     podResourcesSocket: str = constant.DEFAULT_POD_RESOURCES_SOCKET
-    commitBarrier: str = "rccl"             # rccl | none
+    commitBarrier: str = "xgmi"             # xgmi (P2P token ring) | rccl (communicator all-reduce) | none
     probeOnCommit: bool = True
 
     def validate(self) -> None:
@@ -123,8 +123,8 @@ class AgentConfig(ManagerConfig):
             raise ValueError("reportConfigIntervalSeconds must be greater than 0")
         if self.amdSmiBackend not in ("native", "fake"):
             raise ValueError("amdSmiBackend must be 'native' or 'fake'")
-        if self.commitBarrier not in ("rccl", "none"):
-            raise ValueError("commitBarrier must be 'rccl' or 'none'")
+        if self.commitBarrier not in ("xgmi", "rccl", "none"):
+            raise ValueError("commitBarrier must be 'xgmi', 'rccl' or 'none'")
 
 
 @dataclass

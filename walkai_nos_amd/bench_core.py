@@ -972,8 +972,9 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
 
 def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
     """The node-atomic commit barrier over every GPU this process can see, timed once after the
-    window (never inside it): the native helper spawned as the partition agent spawns it, one
-    communicator over all devices. On the driver's 8-GPU node this measures the 8-device clique."""
+    window (never inside it), spawned as the partition agent spawns it: the xGMI P2P token ring
+    (the agent's default) and the RCCL communicator. On the driver's 8-GPU node this measures the
+    8-device ring and clique."""
     try:
         from .ops import native
         from .parallel.spawned import NATIVE_HELPER, SpawnedNodeBarrier
@@ -981,11 +982,13 @@ def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
             return {"error": "native helper not built"}
         import torch
         n = torch.cuda.device_count()
-        b = SpawnedNodeBarrier(n, backend="rccl", native=True, timeout=120.0)
-        ok = b.vote_all([True] * n)
-        out = {"devices": n, "committed": ok}
-        out.update({k: b.last.get(k) for k in ("wall_ms", "hip_init_ms", "comm_init_ms", "allreduce_ms",
-                                                "destroy_ms", "error") if b.last.get(k) is not None})
+        out: Dict[str, Any] = {"devices": n}
+        for backend in ("xgmi", "rccl"):
+            b = SpawnedNodeBarrier(n, backend=backend, native=True, timeout=120.0)
+            r = {"committed": b.vote_all([True] * n)}
+            r.update({k: b.last.get(k) for k in ("wall_ms", "hip_init_ms", "comm_init_ms", "allreduce_ms",
+                                                  "destroy_ms", "error") if b.last.get(k) is not None})
+            out[backend] = r
         return out
     except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench
         return {"error": str(e)[:200]}

@@ -36,7 +36,7 @@ from .common import base_parser, make_client, make_manager, run_until_signal, se
 log = logging.getLogger("nos.partitionagent")
 
 
-def node_barrier_factory(registry, backend: str = "rccl"):
+def node_barrier_factory(registry, backend: str = "xgmi"):
     """Commit barrier per commit: a spawned helper voting over ``n`` logical devices (the actuator
     passes one vote per device of the re-enumerated map)."""
     from ..parallel.spawned import SpawnedNodeBarrier
@@ -83,7 +83,7 @@ def main(argv=None) -> int:
         dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
     from ..parallel.spawned import HelperRegistry
     helpers = HelperRegistry()
-    bf = node_barrier_factory(helpers) if cfg.commitBarrier == "rccl" else None
+    bf = node_barrier_factory(helpers, cfg.commitBarrier) if cfg.commitBarrier != "none" else None
     probe = None
     if cfg.probeOnCommit:
         from ..controllers.agent.probe import ProbeRunner, device_map_targets

@@ -129,8 +129,11 @@ class SpawnedNodeBarrier(CommitBarrier):
 
     One vote per logical device of the re-enumerated device map (HIP ordinal order); the helper
     must see exactly that many HIP devices, so a partition that did not come up is a veto even if
-    every vote was 1.  The RCCL backend runs the native ``nos-gpuhelper`` when it is built (no
-    interpreter start-up on the flip path), else the Python helper."""
+    every vote was 1.  Backends: ``xgmi`` — a ring of peer-to-peer token writes over xGMI
+    (``csrc/p2p_barrier.hip``); ``rccl`` — an ncclCommInitAll clique and a grouped all-reduce
+    (``csrc/rccl_barrier.cpp``); both run in the native ``nos-gpuhelper`` when it is built (no
+    interpreter start-up on the flip path; ``rccl`` falls back to the Python helper); ``local``
+    sums on the CPU (tests)."""
 
     def __init__(self, n_devices: int, backend: str = "rccl", timeout: float = 180.0,
                  registry: Optional[HelperRegistry] = None, native: Optional[bool] = None):
@@ -138,9 +141,9 @@ class SpawnedNodeBarrier(CommitBarrier):
         self.backend = backend
         self.timeout = timeout
         self.registry = registry
-        self.program = native_helper() if backend == "rccl" and native is not False else None
-        if native and self.program is None:
-            raise RuntimeError(f"native helper {NATIVE_HELPER} is not built")
+        self.program = native_helper() if backend in ("rccl", "xgmi") and native is not False else None
+        if (native or backend == "xgmi") and self.program is None:
+            raise RuntimeError(f"native helper {NATIVE_HELPER} is not built (needed for the {backend} barrier)")
         self.last: Dict[str, Any] = {}
 
     def vote_all(self, votes: Sequence[bool]) -> bool:
