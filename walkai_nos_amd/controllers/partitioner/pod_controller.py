@@ -359,8 +359,16 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         cands = [(used_of(g), name, g) for name in sorted(current) for g in current[name].gpus
                  if g.target is None and not g.is_idle() and _mode_of(g) != p
                  and (mode_age is None or params.min_stint <= 0 or mode_age(name, g.index) >= params.min_stint)]
-        if not backlog and not starved:
-            cands = [c for c in cands if w is not None and fill - c[0] >= params.drain_gain - 1e-9]
+        if not backlog:
+            # a candidate qualifies through the gain rule, or through fairness — which weighs
+            # waiting work: a GPU keeps serving its own profile while that queue holds more
+            # GPU-seconds of waiting (demand x oldest wait) than the starved one does; turn-by-turn
+            # alternation would give a whole-GPU queue one pod per cycle and a 1/8 queue eight,
+            # whatever their demand
+            pressure = lambda q: demand.get(q, 0.0) * oldest.get(q, 0.0)  # noqa: E731
+            gain_fits = lambda c: gain_ok and w is not None and fill - c[0] >= params.drain_gain - 1e-9  # noqa: E731
+            fair_fits = lambda c: starved and pressure(_mode_of(c[2])) <= pressure(p)  # noqa: E731
+            cands = [c for c in cands if gain_fits(c) or fair_fits(c)]
 
         if not cands:
             continue
