@@ -100,7 +100,8 @@ def working_cus(cus: Optional[List[int]], pin: int, total_cus: int = 256) -> int
 #: from the amd-smi switch until the agent has committed and its pods can start:
 #:
 #: * ``commit_barrier_s`` — the node-atomic commit: the native helper's wall time (spawn, hipInit,
-#:   ncclCommInitAll, all-reduce, teardown), warm median (profiles/operator_gpu_report_r3.json);
+#:   the xGMI P2P token ring, exit), warm median 0.33 s (profiles/operator_gpu_report_r3.json; the
+#:   RCCL communicator variant takes 2.9-3.4 s, almost all of it ncclCommInitAll + destroy);
 #: * ``probe_s`` — the probe-on-commit round after the flip (profiles/operator_gpu_report_r2.json);
 #: * ``plugin_push_s`` — the nos partition plugin's ListAndWatch push + allocatable patch (no plugin
 #:   restart; the reference waits up to 60 s for the NVIDIA plugin pod, ref pkg/gpu/client.go:86-135);
@@ -109,7 +110,7 @@ def working_cus(cus: Optional[List[int]], pin: int, total_cus: int = 256) -> int
 #:   driver re-creating the partitions and the re-enumeration, flagged as such in BENCH.
 #:
 #: ``--flip-cost`` overrides the total; BENCH also reports the control plane's sensitivity to it.
-FLIP_COST_COMPONENTS = {"commit_barrier_s": 1.0, "probe_s": 0.39, "plugin_push_s": 0.05, "amdsmi_switch_s": 10.0}
+FLIP_COST_COMPONENTS = {"commit_barrier_s": 0.33, "probe_s": 0.39, "plugin_push_s": 0.05, "amdsmi_switch_s": 10.0}
 FLIP_COST_MEASURED = ("commit_barrier_s", "probe_s", "plugin_push_s")
 
 
