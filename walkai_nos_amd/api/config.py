@@ -79,7 +79,7 @@ class GpuPartitionerConfig(ManagerConfig):
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
                     "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
                     "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after", "minStintSeconds": "min_stint",
-                    "unservedAfterSeconds": "unserved_after",
+                    "unservedAfterSeconds": "unserved_after", "replanEverySeconds": "replan_every",
                     "reserveBreakFill": "reserve_break_fill"}
 
     def pack_params(self) -> Any:

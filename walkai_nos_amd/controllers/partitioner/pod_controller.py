@@ -174,6 +174,7 @@ class PackParams:
     reserve_break_fill: float = 2.0  # a queue filling this many GPUs takes a reserved idle SPX GPU
     min_stint: float = 120.0        # seconds: a GPU keeps a mode at least this long before it may be
                                     # drained for another (refilled from its own queue meanwhile)
+    replan_every: float = 10.0      # seconds: an unchanged cluster is re-planned at most this often (0 = always)
     unserved_after: float = 300.0   # seconds (x GPUs of the cluster): a profile no GPU serves (none in its mode, none draining
                                     # to it) whose oldest pod waited this long gets a GPU drained for
                                     # it regardless of gain (0 = off) — the fairness that makes a
@@ -612,10 +613,14 @@ class PodController:
         while the revision is unchanged (no pod, node or annotation changed) the same request would
         plan on identical inputs and reach the same answer, so the requeues of a waiting plan key
         return that answer without re-planning. Only with a client that exposes ``revision`` (the
-        in-memory API server), without a batch window (whose deadline depends on the clock) and not
-        for the ``pack`` policy, whose starve/drain rules depend on how long pods have waited and
-        GPUs have held their mode: the same inputs plan differently a minute later."""
-        rev = getattr(self.client, "revision", None) if self.batch_timeout <= 0 and self.policy != "pack" else None
+        in-memory API server) and without a batch window (whose deadline depends on the clock). The
+        ``pack`` policy's starve/stint/drain rules depend on how long pods have waited and GPUs have
+        held their mode, so its memo also keys on the clock in ``PackParams.replan_every`` buckets:
+        an unchanged cluster is re-planned at most that often (thresholds are acted on at most one
+        bucket late)."""
+        rev = getattr(self.client, "revision", None) if self.batch_timeout <= 0 else None
+        if rev is not None and self.policy == "pack":
+            rev = (rev, int(self.clock() // max(1e-9, self.pack.replan_every))) if self.pack.replan_every > 0 else None
         if rev is not None:
             seen, results = self._idle
             if seen == rev and req in results:
@@ -623,6 +628,8 @@ class PodController:
         res = self._reconcile(req)
         if rev is not None:
             after = getattr(self.client, "revision", None)
+            if isinstance(rev, tuple):
+                after = (after, rev[1])
             if after == rev:
                 seen, results = self._idle
                 if seen != rev:
