@@ -444,6 +444,8 @@ class DataPlane:
             self.drain_all()
             self._layout = layout
         active = [(k, self.slots[k]) for k in keys]
+        if self.cfg.depth <= 1 and active:
+            return self._serve_loops(active, deadline)
         n: Dict[Any, int] = {k: 0 for k in keys}
         while True:
             now = time.perf_counter()
@@ -462,6 +464,44 @@ class DataPlane:
             if not progressed:
                 time.sleep(0.0002)
         return n
+
+    def _serve_loops(self, active: List[Tuple[Any, "Slot"]], deadline: float) -> Dict[Any, int]:
+        """The reference demo's loop (``client/main.py:23-25``), one per pod lane, each on its own
+        thread: start one inference, wait for it (a blocking event wait, the GIL released), record
+        its GPU time, start the next — until ``deadline``. A polling loop over every pod would leave
+        each GPU idle for a poll interval after every inference; a thread per loop resubmits as
+        soon as its inference is done, as a pod's own process would."""
+        import torch
+
+        from .ops import kernels as K
+        counts: Dict[Any, List[int]] = {k: [] for k, _ in active}
+
+        def run(key: Any, slot: "Slot", lane: "_Lane") -> None:
+            K.set_slice_cus(lane.n_cus)
+            K.set_slice_pin(slot.pin)
+            done = 0
+            with torch.no_grad(), torch.cuda.stream(lane.stream):
+                while time.perf_counter() < deadline:
+                    st = torch.cuda.Event(enable_timing=True)
+                    st.record(lane.stream)
+                    if lane.graph is not None:
+                        lane.graph.replay()
+                    else:
+                        lane.out = slot.model(lane.x)
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record(lane.stream)
+                    ev.synchronize()
+                    slot.latency_ms.append(st.elapsed_time(ev))
+                    done += 1
+            counts[key].append(done)
+
+        threads = [threading.Thread(target=run, args=(k, s, lane), daemon=True, name=f"pod-{k}")
+                   for k, s in active for lane in s.lanes]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        return {k: sum(v) for k, v in counts.items()}
 
     def close(self) -> None:
         """Release graphs, model replicas and CU-masked streams before interpreter teardown (a
