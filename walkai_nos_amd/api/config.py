@@ -111,6 +111,7 @@ class GpuPartitionerConfig(ManagerConfig):
 class AgentConfig(ManagerConfig):
     reportConfigIntervalSeconds: float = 10.0
     amdSmiBackend: str = "native"           # native | fake
+    fakeGpus: int = 8                       # GPUs of the fake backend (development clusters, e2e tests)
     devicePluginLabel: str = constant.DEFAULT_DEVICE_PLUGIN_LABEL
     devicePluginNamespace: str = ""
     podResourcesSocket: str = constant.DEFAULT_POD_RESOURCES_SOCKET
@@ -123,6 +124,8 @@ class AgentConfig(ManagerConfig):
             raise ValueError("reportConfigIntervalSeconds must be greater than 0")
         if self.amdSmiBackend not in ("native", "fake"):
             raise ValueError("amdSmiBackend must be 'native' or 'fake'")
+        if self.fakeGpus <= 0:
+            raise ValueError("fakeGpus must be greater than 0")
         if self.commitBarrier not in ("xgmi", "rccl", "none"):
             raise ValueError("commitBarrier must be 'xgmi', 'rccl' or 'none'")
 

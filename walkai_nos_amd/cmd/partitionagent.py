@@ -66,7 +66,7 @@ def main(argv=None) -> int:
     cfg = load_config_file(args.config, "MigAgentConfig") if args.config else MigAgentConfig()
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node",))
-    smi = new_backend(cfg.amdSmiBackend)
+    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)
     gpus = smi.list_gpus()
     if not gpus:
         log.error("no AMD GPU found on node %s", node)

@@ -33,7 +33,7 @@ def main(argv=None) -> int:
     cfg = load_config_file(args.config, "GpuAgentConfig") if args.config else GpuAgentConfig()
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node", "ConfigMap"))
-    smi = new_backend(cfg.amdSmiBackend)
+    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)
     if any_partitioned_gpu(smi):
         log.error("CU-mask slicing needs every GPU in SPX mode; use the partition agent on this node")
         return 1

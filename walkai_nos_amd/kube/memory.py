@@ -86,6 +86,7 @@ class InMemoryAPIServer:
         self._objs: Dict[Tuple[str, str, str], Obj] = {}
         self._by_kind: Dict[str, Dict[Tuple[str, str, str], Obj]] = {}  # kind index of _objs
         self._rv = itertools.count(1)
+        self.last_resource_version = 0
         self._handlers: Dict[str, List[Handler]] = {}
         self.clock = clock
         # request counters, useful for tests / benchmarks
@@ -125,6 +126,11 @@ class InMemoryAPIServer:
         for h in handlers:
             h(etype, o, prev)
 
+    def _next_rv(self) -> str:
+        """The next resourceVersion (caller holds the lock)."""
+        self.last_resource_version = next(self._rv)
+        return str(self.last_resource_version)
+
     # ---- CRUD -------------------------------------------------------------------------
     @staticmethod
     def _k(kind: str, ns: str, name: str) -> Tuple[str, str, str]:
@@ -145,7 +151,7 @@ class InMemoryAPIServer:
             k = self._k(kind, md.get("namespace", ""), md["name"])
             if k in self._objs:
                 raise AlreadyExists(f"{kind} {k[1]}/{k[2]} already exists")
-            md["resourceVersion"] = str(next(self._rv))
+            md["resourceVersion"] = self._next_rv()
             md.setdefault("uid", str(uuid.uuid4()))
             md.setdefault("creationTimestamp", ko.now_rfc3339(self.clock()))
             md.setdefault("labels", md.get("labels") or {})
@@ -200,7 +206,7 @@ class InMemoryAPIServer:
             if new == old:
                 # a no-op write neither bumps the resourceVersion nor emits a watch event
                 return fast_copy(old)
-            md["resourceVersion"] = str(next(self._rv))
+            md["resourceVersion"] = self._next_rv()
             self._objs[k] = new
             self._by_kind.setdefault(kind, {})[k] = new
             out, prev = fast_copy(new), fast_copy(old)
@@ -240,6 +246,9 @@ class InMemoryAPIServer:
                 raise NotFound(f"{kind} {namespace}/{name} not found")
             self._by_kind.get(kind, {}).pop(k, None)
             self.stats["delete"] += 1
+            # the DELETED event carries the deletion's own resourceVersion, as the API server's does
+            o = fast_copy(o)
+            o["metadata"]["resourceVersion"] = self._next_rv()
         self._emit(kind, "DELETED", o, None)
 
     # ---- subresources -------------------------------------------------------------------
