@@ -23,6 +23,7 @@
 #include <cstdint>
 #include <string>
 
+#include "epilogue.h"
 #include "pin.h"
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -131,6 +132,18 @@ __device__ __forceinline__ void compute_stage(f32x16 (&acc)[WM / 32][WN / 32], c
   }
 }
 
+// two values of one column in adjacent rows (idx, idx + N): the plane split on packed pairs
+__device__ __forceinline__ void store_pair(float v0, float v1, size_t idx, int N, float* __restrict__ C,
+                                           __bf16* __restrict__ Cp, size_t c_plane) {
+  if (C) C[idx] = v0, C[idx + N] = v1;
+  if (Cp) {
+    nos_bf2 pl[3];
+    nos_split3_pair(nos_f2{v0, v1}, pl);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Cp[q * c_plane + idx] = pl[q].x, Cp[q * c_plane + idx + N] = pl[q].y;
+  }
+}
+
 __device__ __forceinline__ void store_one(float v, size_t idx, float* __restrict__ C, __bf16* __restrict__ Cp,
                                           size_t c_plane) {
   if (C) C[idx] = v;
@@ -154,7 +167,10 @@ __device__ __forceinline__ void epi_values(const f32x16& acc, float (&v)[16], in
   for (int r = 0; r < 16; ++r) v[r] = acc[r] + bv;
   if (epi & EPI_GELU) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
+    for (int r = 0; r < 16; r += 2) {
+      const nos_f2 g = nos_gelu2(nos_f2{v[r], v[r + 1]});
+      v[r] = g.x, v[r + 1] = g.y;
+    }
   }
   if (epi & EPI_RES) {
     float rv[16];
@@ -187,8 +203,10 @@ __device__ __forceinline__ void store_tile(const f32x16 (&acc)[TM][TN], int r0, 
       epi_values(acc[a][b], v, r0 + 32 * a, col, hf, bv, R, R2, r2_rows, M, N, epi);
       // full 32-row blocks (all but the last row of tiles) store without per-element predicates
       if (r0 + 32 * a + 32 <= M) {
+        // registers r, r+1 (r even) are rows acc_row(r) and acc_row(r) + 1
 #pragma unroll
-        for (int r = 0; r < 16; ++r) store_one(v[r], size_t(r0 + 32 * a + acc_row(r, hf)) * N + col, C, Cp, c_plane);
+        for (int r = 0; r < 16; r += 2)
+          store_pair(v[r], v[r + 1], size_t(r0 + 32 * a + acc_row(r, hf)) * N + col, N, C, Cp, c_plane);
       } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -481,7 +499,10 @@ __device__ __forceinline__ void store_tile16(const f32x4 (&acc)[TM][TN], int r0,
       for (int i = 0; i < 4; ++i) v[i] = acc[a][b][i] + bv;
       if (epi & EPI_GELU) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = 0.5f * v[i] * (1.f + erff(v[i] * 0.70710678118654752f));
+        for (int i = 0; i < 4; i += 2) {
+          const nos_f2 g = nos_gelu2(nos_f2{v[i], v[i + 1]});
+          v[i] = g.x, v[i + 1] = g.y;
+        }
       }
       if (epi & EPI_RES) {
         float rv[4];
@@ -499,7 +520,7 @@ __device__ __forceinline__ void store_tile16(const f32x4 (&acc)[TM][TN], int r0,
       }
       if (rb + 4 <= M) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) store_one(v[i], size_t(rb + i) * N + col, C, Cp, c_plane);
+        for (int i = 0; i < 4; i += 2) store_pair(v[i], v[i + 1], size_t(rb + i) * N + col, N, C, Cp, c_plane);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
