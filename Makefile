@@ -4,7 +4,7 @@ IMG ?= ghcr.io/walkai/nos-mi355x:0.1.0
 CLIENT_IMG ?= ghcr.io/walkai/nos-mi355x-client:0.1.0
 NAMESPACE ?= nos-system
 
-.PHONY: all native test test-gpu lint sanitize bench bench-8 smoke simulate kbench docker-build docker-push \
+.PHONY: all native test test-gpu lint sanitize bench bench-8 smoke simulate devcluster kbench docker-build docker-push \
         deploy undeploy install-crds helm-install helm-uninstall kind-up clean
 
 all: native test
@@ -39,6 +39,9 @@ kbench: native     ## per-slice kernel microbenchmark (attention / GEMM / LayerN
 
 simulate:          ## in-memory cluster simulation of the control plane (no GPU)
 	$(PYTHON) -m walkai_nos_amd.cmd.simulate --gpus 8 --epochs 50
+
+devcluster:        ## the partitioner and partition agents as local processes over a REST API server (no Kubernetes)
+	$(PYTHON) -m walkai_nos_amd.cmd.devcluster --nodes 2 --gpus 1 --demo
 
 docker-build:
 	docker build -f docker/Dockerfile -t $(IMG) .
