@@ -287,3 +287,36 @@ def test_two_concurrent_slice_processes_have_disjoint_census(gpu):
     assert r["census_pairs_overlapping"] == 0, r
     assert a["inferences"] > 0 and b["inferences"] > 0, r
     assert all(p["hbm"]["loaded"] and p["hbm"]["peak_bytes"] <= p["hbm"]["limit_bytes"] for p in r["per_pod"]), r
+
+
+def test_agent_process_serves_the_real_gpu(gpu):
+    """The partition agent BINARY on this box's real GPUs (native amd-smi, read-only: no flip is
+    asked for): it reports the current layout, its nos device plugin registers the real partitions
+    with a kubelet, admission through the plugin's Allocate hands out /dev/kfd and the partition's
+    own render node, and the agent process never loads the HIP runtime."""
+    import tempfile
+
+    from walkai_nos_amd.cmd.devcluster import DevCluster
+    from walkai_nos_amd.device.amdsmi import NativeAmdSmi
+    smi = NativeAmdSmi()
+    n = len(smi.list_gpus())
+    mode, nps = smi.get_compute_partition(0), smi.get_memory_partition(0)
+    profile = f"{mode.lower()}_{nps.lower()}"
+    per_gpu = {"SPX": 1, "DPX": 2, "QPX": 4, "CPX": 8}[mode]
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=n, amd_smi_backend="native")
+        try:
+            c.start()
+            k = c.kubelets["node-0"]
+            res = f"amd.com/{profile}"
+            c.run_until(lambda: len(k.healthy(res)) == n * per_gpu and c.allocatable("node-0", profile) == n * per_gpu,
+                        90, f"{res} to be served")
+            c.submit("p0", profile)
+            c.run_until(lambda: c.phase("p0") == "Running", 60, "the pod to be admitted")
+            paths = k.allocations[("default", "p0")]
+            assert paths[0] == "/dev/kfd" and any(p.startswith("/dev/dri/renderD") for p in paths), paths
+            assert all(os.path.exists(p) for p in paths), paths
+            maps = open(f"/proc/{c.procs['partitionagent-node-0'].pid}/maps").read()
+            assert "libamdhip64" not in maps
+        finally:
+            c.stop()

@@ -58,11 +58,12 @@ def fast_partitioner_config(**packing: float) -> GpuPartitionerConfig:
 class DevCluster:
     def __init__(self, root: str, nodes: int = 1, gpus: int = 1,
                  partitioner: Optional[GpuPartitionerConfig] = None, report_interval: float = 1.0,
-                 bookmark_every: float = 5.0):
+                 bookmark_every: float = 5.0, amd_smi_backend: str = "fake"):
         self.root = root
         self.n_nodes, self.gpus = nodes, gpus
         self.partitioner_cfg = partitioner or fast_partitioner_config()
         self.report_interval = report_interval
+        self.amd_smi_backend = amd_smi_backend   # native: the agents drive this machine's real GPUs
         self.facade = APIFacade(bookmark_every=bookmark_every)
         self.procs: Dict[str, subprocess.Popen] = {}
         self.logs: Dict[str, str] = {}
@@ -86,7 +87,7 @@ class DevCluster:
         for n in names:
             k = self.kubelets[n]
             cfg = MigAgentConfig(healthProbeBindAddress="0", metricsBindAddress="0",
-                                 reportConfigIntervalSeconds=self.report_interval, amdSmiBackend="fake",
+                                 reportConfigIntervalSeconds=self.report_interval, amdSmiBackend=self.amd_smi_backend,
                                  fakeGpus=self.gpus, podResourcesSocket=k.podres_socket, commitBarrier="none",
                                  probeOnCommit=False, devicePlugin="nos", devicePluginDir=k.dir)
             self._spawn(f"partitionagent-{n}", "walkai_nos_amd.cmd.partitionagent", cfg, "MigAgentConfig",

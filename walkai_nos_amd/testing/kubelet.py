@@ -38,6 +38,7 @@ class FakeKubelet:
         self.readers: Dict[str, Tuple[str, threading.Thread]] = {}
         self.used: Dict[Tuple[str, str], Tuple[str, str]] = {}   # (ns, pod) -> (resource, id)
         self.admission_failures: List[Tuple[Tuple[str, str], str]] = []
+        self.allocations: Dict[Tuple[str, str], List[str]] = {}  # (ns, pod) -> host device paths
         self.lock = threading.Lock()
         self.podres_socket = os.path.join(root, "pod-resources.sock")
         self.podres = PodResourcesServer(self.podres_socket, self._used, self._alloc).start()
@@ -115,6 +116,7 @@ class FakeKubelet:
             return None
         with self.lock:
             self.used[key] = (res, free[0])
+            self.allocations[key] = [d.host_path for d in resp.container_responses[0].devices]
         self.client.patch("Pod", key[1], {"status": {"phase": "Running"}}, key[0])
         return free[0]
 
