@@ -131,3 +131,41 @@ def test_devcluster_demo_runs_to_completion():
                            env=dict(os.environ, PYTHONPATH=REPO))
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         assert "the whole-GPU pod runs on node-" in r.stdout and "every pod finished" in r.stdout
+
+
+def test_quota_processes_borrow_and_reclaim():
+    """nos-operator and nos-scheduler as processes too: team A borrows team B's idle guaranteed
+    share (a second whole GPU), team B's pod then reclaims it — nos-scheduler preempts A's
+    over-quota pod and binds B's, the operator keeps `used` and the in/over-quota labels current."""
+    from walkai_nos_amd.api import v1alpha1 as api
+
+    def quota(ns):
+        return {"apiVersion": api.API_VERSION, "kind": api.KIND_ELASTIC_QUOTA,
+                "metadata": {"name": f"q-{ns}", "namespace": ns},
+                "spec": {"min": {api.RESOURCE_GPU_MEMORY: "288"}}}
+
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=2, gpus=1, quota=True)
+        try:
+            c.start()
+            c.run_until(lambda: all(c.allocatable(n, "spx_nps1") == 1 for n in c.kubelets), 30, "both GPUs served")
+            for ns in ("team-a", "team-b"):
+                c.client.create(quota(ns))
+            for name in ("a1", "a2"):
+                c.submit(name, "spx_nps1", namespace="team-a", scheduler_name="nos-scheduler")
+            c.run_until(lambda: all(c.phase(n, "team-a") == "Running" for n in ("a1", "a2")), 60,
+                        "team A's two whole-GPU pods (one borrowed)")
+
+            def caps():
+                return sorted(ko.labels(p).get(api.LABEL_CAPACITY_INFO, "") for p in c.client.list("Pod", "team-a"))
+            c.run_until(lambda: caps() == [api.CAPACITY_IN_QUOTA, api.CAPACITY_OVER_QUOTA], 30, "capacity labels")
+            c.submit("b1", "spx_nps1", namespace="team-b", scheduler_name="nos-scheduler")
+            c.run_until(lambda: c.phase("b1", "team-b") == "Running", 90, "team B's reclaiming pod")
+            assert len(c.client.list("Pod", "team-a")) == 1       # the over-quota pod was preempted
+
+            def used(ns):
+                q = c.client.get(api.KIND_ELASTIC_QUOTA, f"q-{ns}", ns)
+                return (q.get("status", {}).get("used") or {}).get(api.RESOURCE_GPU_MEMORY)
+            c.run_until(lambda: used("team-a") == "288" and used("team-b") == "288", 30, "quota status")
+        finally:
+            c.stop()

@@ -21,7 +21,24 @@ def base_parser(description: str) -> argparse.ArgumentParser:
     ap.add_argument("--config", default="", help="ComponentConfig file (config.nos.nebuly.com/v1alpha1)")
     ap.add_argument("--kubeconfig", default=os.environ.get("KUBECONFIG", ""), help="kubeconfig (default: in-cluster)")
     ap.add_argument("--log-level", "--zap-log-level", dest="log_level", default="info")
+    # controller-runtime's manager flags; when given they override the config file ("0" disables a server)
+    ap.add_argument("--metrics-bind-address", dest="metrics_bind_address", default=None)
+    ap.add_argument("--health-probe-bind-address", dest="health_probe_bind_address", default=None)
+    ap.add_argument("--leader-elect", dest="leader_elect", default=None, choices=("true", "false"))
     return ap
+
+
+def apply_manager_flags(cfg: ManagerConfig, args: argparse.Namespace) -> ManagerConfig:
+    """Command-line manager flags over the component's config (the reference's binaries take the same
+    three flags, ``cmd/*/*.go``)."""
+    if getattr(args, "metrics_bind_address", None) is not None:
+        cfg.metricsBindAddress = args.metrics_bind_address
+    if getattr(args, "health_probe_bind_address", None) is not None:
+        cfg.healthProbeBindAddress = args.health_probe_bind_address
+    if getattr(args, "leader_elect", None) is not None:
+        cfg.leaderElection.leaderElect = args.leader_elect == "true"
+    cfg.validate()
+    return cfg
 
 
 def setup_logging(level: str) -> None:

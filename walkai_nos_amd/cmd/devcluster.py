@@ -5,8 +5,10 @@ kubeconfig; creates fake MI355X nodes; runs ``nos-gpupartitioner`` and one ``nos
 per node (fake amd-smi inside each agent) as separate processes against that kubeconfig; and plays
 the parts a cluster would — one kubelet per node (``testing/kubelet.py``: plugin registration,
 ListAndWatch, admission through the plugin's ``Allocate``, PodResources) and kube-scheduler
-(``sim.cluster.KubeScheduler``: allocatable minus requests). The reference's equivalent developer
-loop is a kind cluster (``hack/kind/cluster.yaml``) with the operator deployed into it.
+(``sim.cluster.KubeScheduler``: allocatable minus requests). With ``--quota`` it also runs
+``nos-operator`` and ``nos-scheduler`` (Elastic Resource Quotas; pods opt in with
+``schedulerName: nos-scheduler``). The reference's equivalent developer loop is a kind cluster
+(``hack/kind/cluster.yaml``) with the operator deployed into it.
 
     nos-devcluster --nodes 2 --gpus 1 --demo        # submit sample pods and print what happens
     nos-devcluster --nodes 1 --gpus 8               # then create pods through the kubeconfig it prints
@@ -58,12 +60,13 @@ def fast_partitioner_config(**packing: float) -> GpuPartitionerConfig:
 class DevCluster:
     def __init__(self, root: str, nodes: int = 1, gpus: int = 1,
                  partitioner: Optional[GpuPartitionerConfig] = None, report_interval: float = 1.0,
-                 bookmark_every: float = 5.0, amd_smi_backend: str = "fake"):
+                 bookmark_every: float = 5.0, amd_smi_backend: str = "fake", quota: bool = False):
         self.root = root
         self.n_nodes, self.gpus = nodes, gpus
         self.partitioner_cfg = partitioner or fast_partitioner_config()
         self.report_interval = report_interval
         self.amd_smi_backend = amd_smi_backend   # native: the agents drive this machine's real GPUs
+        self.quota = quota                       # also run nos-operator and nos-scheduler (Elastic Resource Quotas)
         self.facade = APIFacade(bookmark_every=bookmark_every)
         self.procs: Dict[str, subprocess.Popen] = {}
         self.logs: Dict[str, str] = {}
@@ -92,20 +95,26 @@ class DevCluster:
                                  probeOnCommit=False, devicePlugin="nos", devicePluginDir=k.dir)
             self._spawn(f"partitionagent-{n}", "walkai_nos_amd.cmd.partitionagent", cfg, "MigAgentConfig",
                         {constant.ENV_NODE_NAME: n})
+        if self.quota:
+            quiet = ["--metrics-bind-address", "0", "--health-probe-bind-address", "0", "--leader-elect", "false"]
+            self._spawn("nos-operator", "walkai_nos_amd.cmd.nosoperator", None, "", {}, quiet)
+            self._spawn("nos-scheduler", "walkai_nos_amd.cmd.nosscheduler", None, "", {}, quiet)
         self.scheduler = KubeScheduler(self.client, {n: SimpleNamespace(name=n) for n in names},
                                        on_bind=self._on_bind)
         return self
 
-    def _spawn(self, name: str, module: str, cfg: Any, kind: str, env: Dict[str, str]) -> None:
-        path = os.path.join(self.root, f"{name}.yaml")
-        with open(path, "w") as f:
-            f.write(dump_config(cfg, kind))
+    def _spawn(self, name: str, module: str, cfg: Any, kind: str, env: Dict[str, str],
+               extra: Optional[List[str]] = None) -> None:
+        argv = [sys.executable, "-m", module, "--kubeconfig", self.kubeconfig] + list(extra or [])
+        if cfg is not None:
+            path = os.path.join(self.root, f"{name}.yaml")
+            with open(path, "w") as f:
+                f.write(dump_config(cfg, kind))
+            argv += ["--config", path]
         self.logs[name] = os.path.join(self.root, f"{name}.log")
         e = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""), **env)
         with open(self.logs[name], "w") as out:
-            self.procs[name] = subprocess.Popen([sys.executable, "-m", module, "--config", path,
-                                                 "--kubeconfig", self.kubeconfig],
-                                                stdout=out, stderr=subprocess.STDOUT, env=e, cwd=self.root)
+            self.procs[name] = subprocess.Popen(argv, stdout=out, stderr=subprocess.STDOUT, env=e, cwd=self.root)
 
     def stop(self) -> None:
         for p in self.procs.values():
@@ -142,6 +151,7 @@ class DevCluster:
         for k in self.kubelets.values():
             k.sync()
         self.scheduler.reconcile(KubeScheduler.KEY)
+        self._kubelet_pods()
         now = time.time()
         for (ns, name), t0 in list(self.started.items()):
             try:
@@ -153,6 +163,19 @@ class DevCluster:
             if rt is not None and now - t0 >= float(rt):
                 self.started.pop((ns, name), None)
                 self.kubelets[ko.pod_node_name(pod)].finish(ns, name)
+
+    def _kubelet_pods(self) -> None:
+        """What each kubelet sees of its pods: pods another scheduler (nos-scheduler) bound here are
+        admitted; devices of pods deleted (finished, evicted, preempted) are released."""
+        pods = {(ko.namespace(p), ko.name(p)): p for p in self.client.list("Pod")}
+        for node, k in self.kubelets.items():
+            for key in [key for key in k.used if key not in pods]:
+                with k.lock:
+                    k.used.pop(key, None)
+                self.started.pop(key, None)
+            for key, p in pods.items():
+                if ko.pod_node_name(p) == node and ko.pod_phase(p) == "Pending" and key not in k.used:
+                    self._on_bind(p, node)
 
     def run_until(self, cond: Callable[[], bool], timeout: float, what: str, period: float = 0.2) -> None:
         deadline = time.time() + timeout
@@ -170,8 +193,9 @@ class DevCluster:
     def phase(self, name: str, namespace: str = "default") -> str:
         return ko.pod_phase(self.client.get("Pod", name, namespace))
 
-    def submit(self, name: str, profile: str, runtime_s: Optional[float] = None, namespace: str = "default"):
-        pod = ko.new_pod(name, namespace, requests={f"amd.com/{profile}": 1})
+    def submit(self, name: str, profile: str, runtime_s: Optional[float] = None, namespace: str = "default",
+               scheduler_name: str = "default-scheduler"):
+        pod = ko.new_pod(name, namespace, requests={f"amd.com/{profile}": 1}, scheduler_name=scheduler_name)
         if runtime_s is not None:
             pod["metadata"]["annotations"][RUNTIME_ANNOTATION] = str(runtime_s)
         return self.client.create(pod)
@@ -205,12 +229,13 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--gpus", type=int, default=1, help="fake MI355X GPUs per node")
     ap.add_argument("--dir", default="", help="working directory (kubeconfig, configs, logs); default: a temp dir")
     ap.add_argument("--demo", action="store_true", help="submit sample pods, print the layouts, exit")
+    ap.add_argument("--quota", action="store_true", help="also run nos-operator and nos-scheduler")
     ap.add_argument("--log-level", default="info")
     a = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO))
     root = a.dir or tempfile.mkdtemp(prefix="nos-devcluster-")
     os.makedirs(root, exist_ok=True)
-    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus).start()
+    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus, quota=a.quota).start()
     print(f"nos dev cluster: {a.nodes} node(s) x {a.gpus} GPU(s); KUBECONFIG={c.kubeconfig}; logs in {root}",
           flush=True)
     try:

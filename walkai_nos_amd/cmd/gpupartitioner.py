@@ -12,7 +12,8 @@ import sys
 from ..api.config import GpuPartitionerConfig, load_config_file
 from ..controllers.partitioner.setup import setup_partitioner
 from ..models.xcp.known_configs import load_known_geometries_file, set_known_geometries
-from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+from .common import (apply_manager_flags, base_parser, make_client, make_manager, run_until_signal,
+                     serve_endpoints, setup_logging)
 
 log = logging.getLogger("nos.gpupartitioner")
 
@@ -21,6 +22,7 @@ def main(argv=None) -> int:
     args = base_parser("nos GPU partitioner").parse_args(argv)
     setup_logging(args.log_level)
     cfg = load_config_file(args.config, "GpuPartitionerConfig") if args.config else GpuPartitionerConfig()
+    apply_manager_flags(cfg, args)
     if cfg.knownMigGeometriesFile:
         set_known_geometries(load_known_geometries_file(cfg.knownMigGeometriesFile))
         log.info("loaded known geometries from %s", cfg.knownMigGeometriesFile)

@@ -10,7 +10,8 @@ import sys
 from ..api.config import CapacitySchedulingArgs, GpuPartitionerConfig, load_config_file
 from ..quota.gpu_memory import GpuMemoryCalculator
 from ..quota.scheduler import setup_nos_scheduler
-from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+from .common import (apply_manager_flags, base_parser, make_client, make_manager, run_until_signal,
+                     serve_endpoints, setup_logging)
 
 
 def main(argv=None) -> int:
@@ -22,6 +23,7 @@ def main(argv=None) -> int:
     mcfg = GpuPartitionerConfig()
     mcfg.leaderElection.leaderElect = True
     mcfg.leaderElection.resourceName = "nos-scheduler.nebuly.com"
+    apply_manager_flags(mcfg, args)
     mgr = make_manager(client, mcfg, "nos-scheduler")
     setup_nos_scheduler(mgr, GpuMemoryCalculator(sargs.nvidiaGpuResourceMemoryGB))
     serve_endpoints(mgr, mcfg)

@@ -31,7 +31,8 @@ from ..device.podresources import PodResourcesClient
 from ..kube.runtime import Watch
 from ..utils.predicates import AnnotationsChanged, ExcludeDelete, MatchingName
 from ..utils.util import get_env_or_panic
-from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+from .common import (apply_manager_flags, base_parser, make_client, make_manager, run_until_signal,
+                     serve_endpoints, setup_logging)
 
 log = logging.getLogger("nos.partitionagent")
 
@@ -64,6 +65,7 @@ def main(argv=None) -> int:
     args = base_parser("nos partition agent").parse_args(argv)
     setup_logging(args.log_level)
     cfg = load_config_file(args.config, "MigAgentConfig") if args.config else MigAgentConfig()
+    apply_manager_flags(cfg, args)
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node",))
     smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)

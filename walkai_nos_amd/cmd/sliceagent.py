@@ -18,7 +18,8 @@ from ..device.podresources import PodResourcesClient
 from ..device.slicing_client import ConfigMapSliceStore, SlicingClient
 from ..deviceplugin.server import PluginManager, render_nodes_from_sysfs, run_forever
 from ..utils.util import get_env_or_panic
-from .common import base_parser, make_client, make_manager, run_until_signal, serve_endpoints, setup_logging
+from .common import (apply_manager_flags, base_parser, make_client, make_manager, run_until_signal,
+                     serve_endpoints, setup_logging)
 
 log = logging.getLogger("nos.sliceagent")
 
@@ -31,6 +32,7 @@ def main(argv=None) -> int:
     args = base_parser("nos CU-mask slice agent").parse_args(argv)
     setup_logging(args.log_level)
     cfg = load_config_file(args.config, "GpuAgentConfig") if args.config else GpuAgentConfig()
+    apply_manager_flags(cfg, args)
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node", "ConfigMap"))
     smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)
