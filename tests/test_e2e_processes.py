@@ -169,3 +169,35 @@ def test_quota_processes_borrow_and_reclaim():
             c.run_until(lambda: used("team-a") == "288" and used("team-b") == "288", 30, "quota status")
         finally:
             c.stop()
+
+
+def test_slice_agent_process_serves_cu_mask_slices():
+    """A cumask node: the partitioner plans CU-mask slices for pending slice pods, the slice agent
+    process materialises them in its slice store and its device plugin serves them; kubelet's
+    Allocate hands each pod the HSA_CU_MASK of disjoint CU rows and its HBM budget."""
+    from walkai_nos_amd.api import v1alpha1 as api
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=1, kind=api.PARTITIONING_KIND_CUMASK)
+        try:
+            c.start()
+            k = c.kubelets[NODE]
+            c.submit("s0", "gpu-64cu.72gb")
+            c.submit("s1", "gpu-64cu.72gb")
+            c.submit("m0", "gpu-36gb")
+            c.run_until(lambda: all(c.phase(n) == "Running" for n in ("s0", "s1", "m0")), 90,
+                        "the three slice pods to run")
+            masks = [k.envs[("default", n)].get("HSA_CU_MASK", "") for n in ("s0", "s1")]
+            assert all(m.startswith("0:") for m in masks) and masks[0] != masks[1], masks
+
+            def cus(m):
+                out = set()
+                for part in m.split(":", 1)[1].split(","):
+                    lo, _, hi = part.partition("-")
+                    out |= set(range(int(lo), int(hi or lo) + 1))
+                return out
+            a, b = cus(masks[0]), cus(masks[1])
+            assert len(a) == len(b) == 64 and not (a & b)
+            limits = [int(k.envs[("default", n)]["NOS_HBM_LIMIT_BYTES"]) for n in ("s0", "s1", "m0")]
+            assert limits[0] == limits[1] == 72 * 10**9 and limits[2] == 36 * 10**9
+        finally:
+            c.stop()

@@ -192,3 +192,16 @@ def test_slice_reporter_groups_slices_and_excludes_whole_gpu_resource():
     rv = srv.get("Node", "node-s")["metadata"]["resourceVersion"]
     rep.reconcile(Request("node-s"))
     assert srv.get("Node", "node-s")["metadata"]["resourceVersion"] == rv
+
+
+def test_pack_policy_plans_cumask_nodes_oldest_first():
+    """The partitioner's default policy is ``pack`` (compute partitions); on a cumask node it must
+    still plan slices (found by the process-level test: the pack planner assumed partition GPUs)."""
+    from walkai_nos_amd.controllers.partitioner.setup import policy_for
+    assert policy_for("cumask", "pack") == "fifo" and policy_for("xcp", "pack") == "pack"
+    c = SimCluster(n_nodes=1, gpus_per_node=1, kind="cumask", policy="pack")
+    c.run(30)
+    c.submit({"amd.com/gpu-64cu.72gb": 1}, name="s0")
+    c.submit({"amd.com/gpu-36gb": 1}, name="m0")
+    c.run(120)
+    assert {ko.name(p) for p in c.running_pods()} == {"s0", "m0"}

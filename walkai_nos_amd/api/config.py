@@ -117,6 +117,7 @@ class AgentConfig(ManagerConfig):
     podResourcesSocket: str = constant.DEFAULT_POD_RESOURCES_SOCKET
     commitBarrier: str = "xgmi"             # xgmi (P2P token ring) | rccl (communicator all-reduce) | none
     probeOnCommit: bool = True
+    devicePluginDir: str = "/var/lib/kubelet/device-plugins"  # kubelet's plugin dir (kubelet.sock + our sockets)
 
     def validate(self) -> None:
         super().validate()
@@ -139,7 +140,6 @@ class MigAgentConfig(AgentConfig):
     k8s-device-plugin serves them and is restarted after a flip (no drain enforcement: a GPU the
     partitioner drains keeps receiving pods on its free partitions)."""
     devicePlugin: str = "nos"
-    devicePluginDir: str = "/var/lib/kubelet/device-plugins"
     publishAllocatable: bool = True         # patch node status.allocatable right after each plugin sync
 
     def validate(self) -> None:

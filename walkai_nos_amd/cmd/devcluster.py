@@ -2,7 +2,8 @@
 
 Starts the in-memory API server behind its REST facade (``kube/apiserver.py``) and writes a
 kubeconfig; creates fake MI355X nodes; runs ``nos-gpupartitioner`` and one ``nos-partitionagent``
-per node (fake amd-smi inside each agent) as separate processes against that kubeconfig; and plays
+per node (fake amd-smi inside each agent; ``--kind cumask``: ``nos-sliceagent``) as separate
+processes against that kubeconfig; and plays
 the parts a cluster would — one kubelet per node (``testing/kubelet.py``: plugin registration,
 ListAndWatch, admission through the plugin's ``Allocate``, PodResources) and kube-scheduler
 (``sim.cluster.KubeScheduler``: allocatable minus requests). With ``--quota`` it also runs
@@ -31,7 +32,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 from .. import constant
 from ..api import v1alpha1 as api
-from ..api.config import GpuPartitionerConfig, MigAgentConfig, dump_config
+from ..api.config import GpuAgentConfig, GpuPartitionerConfig, MigAgentConfig, dump_config
 from ..kube import objects as ko
 from ..kube.apiserver import APIFacade
 from ..kube.rest import from_kubeconfig
@@ -43,8 +44,8 @@ RUNTIME_ANNOTATION = "nos.nebuly.com/dev-runtime-seconds"
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def node_labels(gpus: int, model: str = "MI355X") -> Dict[str, str]:
-    return {api.LABEL_GPU_PARTITIONING: api.PARTITIONING_KIND_XCP,
+def node_labels(gpus: int, model: str = "MI355X", kind: str = api.PARTITIONING_KIND_XCP) -> Dict[str, str]:
+    return {api.LABEL_GPU_PARTITIONING: kind,
             constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}", constant.LABEL_AMD_GPU_COUNT: str(gpus),
             constant.LABEL_AMD_GPU_VRAM: "288G", constant.LABEL_AMD_GPU_CU_COUNT: "256"}
 
@@ -60,13 +61,15 @@ def fast_partitioner_config(**packing: float) -> GpuPartitionerConfig:
 class DevCluster:
     def __init__(self, root: str, nodes: int = 1, gpus: int = 1,
                  partitioner: Optional[GpuPartitionerConfig] = None, report_interval: float = 1.0,
-                 bookmark_every: float = 5.0, amd_smi_backend: str = "fake", quota: bool = False):
+                 bookmark_every: float = 5.0, amd_smi_backend: str = "fake", quota: bool = False,
+                 kind: str = api.PARTITIONING_KIND_XCP):
         self.root = root
         self.n_nodes, self.gpus = nodes, gpus
         self.partitioner_cfg = partitioner or fast_partitioner_config()
         self.report_interval = report_interval
         self.amd_smi_backend = amd_smi_backend   # native: the agents drive this machine's real GPUs
         self.quota = quota                       # also run nos-operator and nos-scheduler (Elastic Resource Quotas)
+        self.kind = kind                         # xcp: partition agents; cumask: CU-mask slice agents
         self.facade = APIFacade(bookmark_every=bookmark_every)
         self.procs: Dict[str, subprocess.Popen] = {}
         self.logs: Dict[str, str] = {}
@@ -83,18 +86,22 @@ class DevCluster:
         self.client = from_kubeconfig(self.kubeconfig)
         names = [f"node-{i}" for i in range(self.n_nodes)]
         for n in names:
-            self.client.create(ko.new_node(n, node_labels(self.gpus)))
+            self.client.create(ko.new_node(n, node_labels(self.gpus, kind=self.kind)))
             self.kubelets[n] = FakeKubelet(os.path.join(self.root, n), self.client, n)
         self._spawn("gpupartitioner", "walkai_nos_amd.cmd.gpupartitioner", self.partitioner_cfg,
                     "GpuPartitionerConfig", {})
         for n in names:
             k = self.kubelets[n]
-            cfg = MigAgentConfig(healthProbeBindAddress="0", metricsBindAddress="0",
-                                 reportConfigIntervalSeconds=self.report_interval, amdSmiBackend=self.amd_smi_backend,
-                                 fakeGpus=self.gpus, podResourcesSocket=k.podres_socket, commitBarrier="none",
-                                 probeOnCommit=False, devicePlugin="nos", devicePluginDir=k.dir)
-            self._spawn(f"partitionagent-{n}", "walkai_nos_amd.cmd.partitionagent", cfg, "MigAgentConfig",
-                        {constant.ENV_NODE_NAME: n})
+            common = dict(healthProbeBindAddress="0", metricsBindAddress="0",
+                          reportConfigIntervalSeconds=self.report_interval, amdSmiBackend=self.amd_smi_backend,
+                          fakeGpus=self.gpus, podResourcesSocket=k.podres_socket, commitBarrier="none",
+                          probeOnCommit=False, devicePluginDir=k.dir)
+            if self.kind == api.PARTITIONING_KIND_CUMASK:
+                self._spawn(f"sliceagent-{n}", "walkai_nos_amd.cmd.sliceagent", GpuAgentConfig(**common),
+                            "GpuAgentConfig", {constant.ENV_NODE_NAME: n})
+            else:
+                self._spawn(f"partitionagent-{n}", "walkai_nos_amd.cmd.partitionagent",
+                            MigAgentConfig(devicePlugin="nos", **common), "MigAgentConfig", {constant.ENV_NODE_NAME: n})
         if self.quota:
             quiet = ["--metrics-bind-address", "0", "--health-probe-bind-address", "0", "--leader-elect", "false"]
             self._spawn("nos-operator", "walkai_nos_amd.cmd.nosoperator", None, "", {}, quiet)
@@ -195,6 +202,7 @@ class DevCluster:
 
     def submit(self, name: str, profile: str, runtime_s: Optional[float] = None, namespace: str = "default",
                scheduler_name: str = "default-scheduler"):
+        """A pod requesting one ``amd.com/<profile>`` (``cpx_nps1``, ``gpu-64cu.72gb``, ...)."""
         pod = ko.new_pod(name, namespace, requests={f"amd.com/{profile}": 1}, scheduler_name=scheduler_name)
         if runtime_s is not None:
             pod["metadata"]["annotations"][RUNTIME_ANNOTATION] = str(runtime_s)
@@ -230,18 +238,21 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--dir", default="", help="working directory (kubeconfig, configs, logs); default: a temp dir")
     ap.add_argument("--demo", action="store_true", help="submit sample pods, print the layouts, exit")
     ap.add_argument("--quota", action="store_true", help="also run nos-operator and nos-scheduler")
+    ap.add_argument("--kind", default=api.PARTITIONING_KIND_XCP, choices=api.PARTITIONING_KINDS,
+                    help="xcp: compute partitions (partition agents); cumask: CU-mask slices (slice agents)")
     ap.add_argument("--log-level", default="info")
     a = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO))
     root = a.dir or tempfile.mkdtemp(prefix="nos-devcluster-")
     os.makedirs(root, exist_ok=True)
-    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus, quota=a.quota).start()
+    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus, quota=a.quota, kind=a.kind).start()
     print(f"nos dev cluster: {a.nodes} node(s) x {a.gpus} GPU(s); KUBECONFIG={c.kubeconfig}; logs in {root}",
           flush=True)
     try:
-        c.run_until(lambda: all(c.allocatable(n, "spx_nps1") == a.gpus for n in c.kubelets), 60,
-                    "the partition agents to report")
-        if a.demo:
+        if a.kind == api.PARTITIONING_KIND_XCP:
+            c.run_until(lambda: all(c.allocatable(n, "spx_nps1") == a.gpus for n in c.kubelets), 60,
+                        "the partition agents to report")
+        if a.demo and a.kind == api.PARTITIONING_KIND_XCP:
             _demo(c)
             return 0
         last = None

@@ -7,6 +7,7 @@ plugin manager for the node's slices.
 from __future__ import annotations
 
 import logging
+import os
 import sys
 import threading
 
@@ -45,8 +46,9 @@ def main(argv=None) -> int:
     mgr = make_manager(client, cfg, "sliceagent")
     # render nodes and slice health come from the device map (a slice whose GPU left the map is
     # Unhealthy); the sysfs listing is only the fallback for a map without render minors
-    plugins = PluginManager(store, render_nodes_from_sysfs(), cu_count=gpus[0].cu_count or 256,
-                            shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map)
+    plugins = PluginManager(store, render_nodes_from_sysfs(), socket_dir=cfg.devicePluginDir,
+                            kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
+                            cu_count=gpus[0].cu_count or 256, shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map)
 
     class Notify:
         def restart(self, node_name, timeout=60):

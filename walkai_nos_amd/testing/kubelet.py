@@ -39,6 +39,7 @@ class FakeKubelet:
         self.used: Dict[Tuple[str, str], Tuple[str, str]] = {}   # (ns, pod) -> (resource, id)
         self.admission_failures: List[Tuple[Tuple[str, str], str]] = []
         self.allocations: Dict[Tuple[str, str], List[str]] = {}  # (ns, pod) -> host device paths
+        self.envs: Dict[Tuple[str, str], Dict[str, str]] = {}     # (ns, pod) -> env Allocate injected
         self.lock = threading.Lock()
         self.podres_socket = os.path.join(root, "pod-resources.sock")
         self.podres = PodResourcesServer(self.podres_socket, self._used, self._alloc).start()
@@ -67,7 +68,9 @@ class FakeKubelet:
             ch.close()
 
     def sync(self) -> None:
-        """(Re)open a ListAndWatch stream for every registered resource whose stream is gone."""
+        """(Re)open a ListAndWatch stream for every registered resource whose stream is gone, and
+        publish the node's allocatable (healthy devices) and capacity (all devices), as kubelet's
+        node-status sync does."""
         latest = {r.resource_name: r.endpoint for r in self.reg.registered}
         for res, ep in latest.items():
             cur = self.readers.get(res)
@@ -75,6 +78,19 @@ class FakeKubelet:
                 t = threading.Thread(target=self._read, args=(res, ep), daemon=True, name=f"law-{res}")
                 t.start()
                 self.readers[res] = (ep, t)
+        self._publish()
+
+    def _publish(self) -> None:
+        with self.lock:
+            alloc = {r: str(sum(1 for _, h in ds if h == dp.HEALTHY)) for r, ds in self.devices.items()}
+            cap = {r: str(len(ds)) for r, ds in self.devices.items()}
+        if not alloc:
+            return
+        st = (self.client.get("Node", self.node).get("status") or {})
+        if all(st.get("allocatable", {}).get(r) == v for r, v in alloc.items()) and \
+                all(st.get("capacity", {}).get(r) == v for r, v in cap.items()):
+            return
+        self.client.patch("Node", self.node, {"status": {"allocatable": alloc, "capacity": cap}})
 
     def healthy(self, resource: str) -> List[str]:
         with self.lock:
@@ -88,7 +104,7 @@ class FakeKubelet:
         for c in pod["spec"].get("containers", []):
             reqs.update((c.get("resources") or {}).get("requests") or {})
             reqs.update((c.get("resources") or {}).get("limits") or {})
-        res = next((k for k in reqs if k.startswith("amd.com/")), None)
+        res = next((k for k in reqs if k.startswith("amd.com/") and k != "amd.com/gpu"), None)
         key = (ko.namespace(pod), ko.name(pod))
         if res is None:
             self.client.patch("Pod", key[1], {"status": {"phase": "Running"}}, key[0])
@@ -117,6 +133,7 @@ class FakeKubelet:
         with self.lock:
             self.used[key] = (res, free[0])
             self.allocations[key] = [d.host_path for d in resp.container_responses[0].devices]
+            self.envs[key] = dict(resp.container_responses[0].envs)
         self.client.patch("Pod", key[1], {"status": {"phase": "Running"}}, key[0])
         return free[0]
 
