@@ -201,3 +201,48 @@ def test_slice_agent_process_serves_cu_mask_slices():
             assert limits[0] == limits[1] == 72 * 10**9 and limits[2] == 36 * 10**9
         finally:
             c.stop()
+
+
+def test_cluster_info_exporter_process_posts_the_cluster():
+    """nos-clusterinfoexporter as a process against the API: its first snapshot (sent at start)
+    reaches the endpoint with the cluster's partition inventory and a bearer token."""
+    import json as _json
+    from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+    got = []
+
+    class Sink(BaseHTTPRequestHandler):
+        def do_POST(self):  # noqa: N802
+            body = self.rfile.read(int(self.headers.get("Content-Length") or 0))
+            got.append((self.headers.get("Authorization"), _json.loads(body)))
+            self.send_response(200)
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+    sink = ThreadingHTTPServer(("127.0.0.1", 0), Sink)
+    threading.Thread(target=sink.serve_forever, daemon=True).start()
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=2)
+        proc = None
+        try:
+            c.start()
+            c.run_until(lambda: c.allocatable(NODE, "spx_nps1") == 2, 30, "the node to report")
+            proc = subprocess.Popen([sys.executable, "-m", "walkai_nos_amd.cmd.clusterinfoexporter",
+                                     "--endpoint", f"http://127.0.0.1:{sink.server_address[1]}/ingest",
+                                     "--interval", "1h", "--api-token", "t0k", "--kubeconfig", c.kubeconfig],
+                                    env=dict(os.environ, PYTHONPATH=REPO), stdout=subprocess.DEVNULL,
+                                    stderr=subprocess.DEVNULL)
+            deadline = time.time() + 30
+            while not got and time.time() < deadline:
+                time.sleep(0.1)
+            assert got, "no snapshot posted"
+            auth, payload = got[0]
+            assert auth == "Bearer t0k"
+            assert {"gpu": "spx_nps1", "allocated": 0, "available": 2} in payload["gpus"], payload
+        finally:
+            if proc is not None:
+                proc.terminate()
+                proc.wait(timeout=10)
+            c.stop()
+            sink.shutdown()
