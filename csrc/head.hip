@@ -17,7 +17,10 @@
 namespace {
 thread_local std::string g_err;
 
-constexpr int TM = 16, TN = 32, KMAX = 384, KS = KMAX + 1;  // tile rows x columns; K <= KMAX
+// tile rows x columns; K <= KMAX. Row stride KS = KMAX + 4 floats: 16-byte aligned rows for
+// ds_read_b128, and KS mod 64 = 4 puts the 16 column rows a ds_read_b128 lane group reads on 16
+// distinct 4-bank slots (conflict-free)
+constexpr int TM = 16, TN = 32, KMAX = 384, KS = KMAX + 4;
 
 struct LinGroup {
   const float* x;  // [M][ldx]
@@ -49,8 +52,8 @@ __global__ __launch_bounds__(256) void small_linear_f32(LinArgs a) {
   const LinGroup& g = a.g[blockIdx.z];
   const int n0 = blockIdx.x * TN, m0 = blockIdx.y * TM;
   if (n0 >= g.n) return;
-  __shared__ float xs[TM * KS];
-  __shared__ float ws[TN * KS];
+  __shared__ __attribute__((aligned(16))) float xs[TM * KS];
+  __shared__ __attribute__((aligned(16))) float ws[TN * KS];
   __shared__ float s_mean[TM], s_rstd[TM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int K = a.K, K4 = K / 4;
@@ -120,11 +123,21 @@ __global__ __launch_bounds__(256) void small_linear_f32(LinArgs a) {
   const float* x0 = xs + r2 * KS;
   const float* x1 = x0 + KS;
   float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll 8
-  for (int k = 0; k < K; ++k) {
-    const float wv = wr[k];
-    acc0 = fmaf(x0[k], wv, acc0);
-    acc1 = fmaf(x1[k], wv, acc1);
+  // 4 k per step: three ds_read_b128 for 8 FMAs (K % 4 == 0 is checked at launch); the FMA order
+  // per output is k ascending, as before
+#pragma unroll 4
+  for (int k = 0; k < K; k += 4) {
+    const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
+    const float4 a4 = *reinterpret_cast<const float4*>(x0 + k);
+    const float4 b4 = *reinterpret_cast<const float4*>(x1 + k);
+    acc0 = fmaf(a4.x, w4.x, acc0);
+    acc1 = fmaf(b4.x, w4.x, acc1);
+    acc0 = fmaf(a4.y, w4.y, acc0);
+    acc1 = fmaf(b4.y, w4.y, acc1);
+    acc0 = fmaf(a4.z, w4.z, acc0);
+    acc1 = fmaf(b4.z, w4.z, acc1);
+    acc0 = fmaf(a4.w, w4.w, acc0);
+    acc1 = fmaf(b4.w, w4.w, acc1);
   }
   const int col = n0 + c;
   if (col >= g.n) return;
