@@ -246,3 +246,23 @@ def test_cluster_info_exporter_process_posts_the_cluster():
                 proc.wait(timeout=10)
             c.stop()
             sink.shutdown()
+
+
+def test_memory_partition_switch_over_processes():
+    """NPS2 pods on an NPS1 node: the partitioner writes a node-wide memory-partition spec, the
+    agent process switches the (idle) node, its plugin serves amd.com/cpx_nps2 and the pods run."""
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=2)
+        try:
+            c.start()
+            c.run_until(lambda: c.allocatable(NODE, "spx_nps1") == 2, 30, "the node to report")
+            for i in range(5):
+                c.submit(f"n{i}", "cpx_nps2")
+            c.run_until(lambda: all(c.phase(f"n{i}") == "Running" for i in range(5)), 120, "the NPS2 pods")
+            anns = ko.annotations(c.client.get("Node", NODE))
+            assert anns["nos.nebuly.com/spec-memory-partition"] == "nps2"
+            c.run_until(lambda: ko.annotations(c.client.get("Node", NODE)).get(
+                "nos.nebuly.com/status-memory-partition") == "nps2", 30, "the NPS status")
+            assert c.kubelets[NODE].admission_failures == []
+        finally:
+            c.stop()

@@ -308,3 +308,70 @@ def test_pack_reserve_break_flips_a_reserved_idle_spx_gpu_for_a_full_queue():
     assert changed["n0"].gpus[0].geometry() == {"spx_nps1": 1}  # the busy GPU is never touched
     # without a reserve the idle GPU flips for a half-GPU queue already (min_fill)
     assert "n0" in plan_cluster_pack(models, three[:1], params=PackParams(), spx_demand=0.0)
+
+
+def test_pack_switches_an_idle_node_to_another_memory_partition_mode_and_back():
+    """``*_nps2`` pods on an NPS1 node: the memory mode is node-wide, so the planner switches a
+    whole idle node (``spec-memory-partition``) with the waiting profile's mode on as many GPUs as
+    the demand starts and the fewest-partition NPS2 geometry (DPX: SPX needs NPS1) on the rest; a
+    whole-GPU NPS1 pod arriving meanwhile waits, and the node switches back once it is idle."""
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=2, policy="pack")
+    c.run(30)
+    for i in range(5):
+        c.submit({"amd.com/cpx_nps2": 1}, name=f"m{i}")
+    c.run(120)
+    anns = ko.annotations(c.api.get("Node", "node-0"))
+    assert anns["nos.nebuly.com/spec-memory-partition"] == "nps2"
+    assert anns["nos.nebuly.com/status-memory-partition"] == "nps2"
+    assert anns["nos.nebuly.com/spec-gpu-0-cpx_nps2"] == "8" and anns["nos.nebuly.com/spec-gpu-1-dpx_nps2"] == "2"
+    assert all(ko.pod_phase(c.api.get("Pod", f"m{i}", "default")) == "Running" for i in range(5))
+    c.submit({"amd.com/spx_nps1": 1}, name="w")
+    c.run(200)
+    assert ko.pod_phase(c.api.get("Pod", "w", "default")) == "Pending"
+    for i in range(5):
+        c.complete(f"m{i}")
+        c.delete_pod(f"m{i}")
+    c.run(600)
+    anns = ko.annotations(c.api.get("Node", "node-0"))
+    assert anns["nos.nebuly.com/status-memory-partition"] == "nps1"
+    assert ko.pod_phase(c.api.get("Pod", "w", "default")) == "Running"
+
+
+def test_pack_drains_a_whole_node_for_an_unserved_memory_partition_mode():
+    """No idle node: once an NPS2 pod has waited unserved_after x GPUs, the least-used node is
+    drained as a whole — every GPU's spec changes at once (idle ones included), none takes new
+    pods — and the agent switches the node when its last pod leaves."""
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, plan_cluster_pack
+    from walkai_nos_amd.models.xcp import node as xn
+    n = ko.new_node("node-0", {"nos.nebuly.com/gpu-partitioning": "xcp",
+                               "amd.com/gpu.product-name": "AMD_Instinct_MI355X", "amd.com/gpu.count": "2"},
+                    {"nos.nebuly.com/status-gpu-0-spx_nps1-used": "1", "nos.nebuly.com/status-gpu-1-spx_nps1-free": "1",
+                     "nos.nebuly.com/status-memory-partition": "nps1"})
+    m = xn.new_node(n)
+    p = PackParams(unserved_after=300)
+    assert plan_cluster_pack({"node-0": m}, [({"cpx_nps2": 1}, 500.0)], None, p) == {}   # not yet: 500 < 300 x 2
+    ch = plan_cluster_pack({"node-0": m}, [({"cpx_nps2": 1}, 700.0)], None, p)
+    out = ch["node-0"]
+    assert out.memory_target == "nps2"
+    assert [g.target for g in out.gpus] == [{"cpx_nps2": 8}, {"dpx_nps2": 2}]
+    # the next pass reads the written spec: every GPU withheld, the idle one included
+    from walkai_nos_amd.partitioning.planner import build_node_partitioning, spec_annotations
+    anns = dict(ko.annotations(n))
+    anns.update(spec_annotations(build_node_partitioning(out, out.memory_target)))
+    anns["nos.nebuly.com/spec-memory-partition"] = "nps2"
+    m2 = xn.new_node(ko.new_node("node-0", ko.labels(n), anns))
+    assert m2.memory_target == "nps2" and all(g.target is not None for g in m2.gpus)
+    with pytest.raises(ValueError):
+        m2.gpus[1].add_pod({"spx_nps1": 1})
+
+
+def test_agent_blocks_every_gpu_while_a_memory_partition_change_waits_for_an_idle_node():
+    from walkai_nos_amd.controllers.agent.plan import XcpState, new_xcp_config_plan
+    from walkai_nos_amd.models.annotation import SpecAnnotation
+    from walkai_nos_amd.models.device import GpuDevice
+    state = XcpState([GpuDevice("amd.com/spx_nps1", "g0", "used", 0), GpuDevice("amd.com/spx_nps1", "g1", "free", 1)])
+    spec = [SpecAnnotation("cpx_nps2", 0, 8), SpecAnnotation("dpx_nps2", 1, 2)]
+    plan = new_xcp_config_plan(state, {0: "spx_nps1", 1: "spx_nps1"}, spec, "nps2", "nps1")
+    assert plan.memory_partition is None and plan.changes == []
+    assert sorted(g for g, _ in plan.blocked) == [0, 1]

@@ -106,9 +106,12 @@ def new_xcp_config_plan(state: XcpState, current: Mapping[int, str], spec: Itera
     if target_nps and current_nps and target_nps != current_nps.lower():
         busy = [g for g in current if state.used_on(g) > 0]
         if busy:
-            plan.blocked.extend((g, f"memory partition change to {target_nps} needs the whole node idle") for g in busy)
-        else:
-            plan.memory_partition = target_nps
+            # nothing moves until the whole node is idle: flipping the idle GPUs' compute modes now
+            # would only give them partitions of the old memory mode to be flipped again
+            plan.blocked.extend((g, f"memory partition change to {target_nps} needs the whole node idle")
+                                for g in sorted(current))
+            return plan
+        plan.memory_partition = target_nps
     for g, p in sorted(desired.items()):
         cur = current.get(g)
         if cur == p:

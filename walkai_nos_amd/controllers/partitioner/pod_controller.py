@@ -186,6 +186,92 @@ def _mode_of(gpu: Any) -> Optional[str]:
     return next(iter(geo)) if len(geo) == 1 else None
 
 
+def _nps_of(profile: str) -> Optional[str]:
+    return profile.split("_", 1)[1] if "_" in profile else None
+
+
+def _plan_memory_partitions(current: Dict[str, NodeModel], changed: Dict[str, NodeModel], demand: Dict[str, float],
+                            oldest: Dict[str, float], unserved: List[Tuple[Dict[str, int], float]],
+                            params: "PackParams", mode_age: Optional[Callable[[str, int], float]],
+                            total_gpus: int, frac: Callable[[str], float]) -> None:
+    """Node-wide memory-partition (NPS) switches for the pack policy.
+
+    A profile of another NPS than a node's (``cpx_nps2`` on an NPS1 node) needs the whole node
+    re-partitioned: the memory mode is node-wide, and the agent changes it only when every GPU is
+    idle. For an NPS no node has (or is switching to): an **idle** node — every GPU idle, each past
+    ``min_stint`` — is switched when the waiting demand fills ``min_fill`` of a GPU or a pod has
+    waited ``starve_after`` (the smallest such node: the fewest GPUs re-partitioned); failing that,
+    once a pod has waited ``unserved_after`` x the cluster's GPUs, the least-used node is
+    **drained** for it (every GPU's spec changes now, the partition plugin withholds them all).
+    The switched node's GPUs take the waiting profiles' modes (most demand first, one GPU per
+    started GPU of demand) and the rest the fewest-partition geometry of the new NPS. Profiles of an NPS that
+    no node serves leave ``demand`` here: the per-GPU rules can only flip modes within a node's NPS."""
+    from ...models.xcp.node import new_gpu
+    nps_now = {n: getattr(m, "memory_partition", None) for n, m in current.items()}
+    nps_next = {n: getattr(m, "memory_target", None) for n, m in current.items()}
+    for target in sorted({_nps_of(p) for p in demand} - {None}):
+        profs = sorted((p for p in demand if _nps_of(p) == target), key=lambda p: (-demand[p], p))
+        if any(nps_now[n] in (None, target) or nps_next[n] == target for n in current):
+            continue  # a node has (or is switching to) this NPS: the per-GPU rules serve it
+        need = sum(demand[p] for p in profs)
+        waited = max(oldest.get(p, 0.0) for p in profs)
+
+        def past_stint(n: str) -> bool:
+            return mode_age is None or params.min_stint <= 0 or \
+                all(mode_age(n, g.index) >= params.min_stint for g in current[n].gpus)
+
+        def layout(m: NodeModel) -> List[Dict[str, int]]:
+            """Per GPU: a waiting profile's mode (one GPU per started GPU of its demand), then the
+            fewest-partition geometry the model allows in the new NPS (SPX needs NPS1)."""
+            left = {p: demand[p] for p in profs}
+            out = []
+            for g in m.gpus:
+                p = next((q for q in profs if left[q] > 1e-9), None)
+                if p is None:
+                    probe = new_gpu(g.model, g.index, target)
+                    probe.init_geometry()
+                    out.append(probe.geometry())
+                    continue
+                out.append({p: round(1.0 / frac(p)) if frac(p) > 0 else 1})
+                left[p] -= 1.0
+            return out
+        idle_nodes = [n for n in sorted(current) if current[n].gpus and nps_next[n] is None and past_stint(n)
+                      and all(g.is_idle() and g.target is None for g in current[n].gpus)]
+        chosen = None
+        if idle_nodes and (need + 1e-9 >= params.min_fill or waited >= params.starve_after):
+            chosen = min(idle_nodes, key=lambda n: (len(current[n].gpus), n))
+            m = current[chosen]
+            try:
+                new = [new_gpu(g.model, g.index, target) for g in m.gpus]
+                for g, geo in zip(new, layout(m)):
+                    g.apply_geometry(geo)
+            except ValueError:
+                chosen = None
+            else:
+                m.gpus = new
+                for i, (req, _) in enumerate(list(unserved)):
+                    if len(req) == 1 and next(iter(req)) in profs:
+                        try:
+                            m.add_pod(req)
+                        except (ValueError, AttributeError):
+                            continue
+        elif params.unserved_after > 0 and waited >= params.unserved_after * max(1, total_gpus):
+            cands = [n for n in sorted(current) if current[n].gpus and nps_next[n] is None and past_stint(n)
+                     and all(g.target is None for g in current[n].gpus)]
+            if cands:
+                used = {n: sum(sum(g.used.values()) * frac(p) for g in current[n].gpus for p in g.used)
+                        for n in cands}
+                chosen = min(cands, key=lambda n: (used[n], n))
+                for g, geo in zip(current[chosen].gpus, layout(current[chosen])):
+                    g.target = geo
+        if chosen is not None:
+            current[chosen].memory_target = target
+            nps_next[chosen] = target
+            changed[chosen] = current[chosen]
+        for p in profs:
+            demand.pop(p, None)
+
+
 def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[str, int], float]],
                       incoming: Optional[Mapping[str, int]] = None, params: Optional[PackParams] = None,
                       spx_demand: float = 0.0,
@@ -283,9 +369,10 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         (p, q), = req.items()
         demand[p] = demand.get(p, 0.0) + q * frac(p)
         oldest[p] = max(oldest.get(p, 0.0), age)
+    total_gpus = sum(len(m.gpus) for m in current.values())
+    _plan_memory_partitions(current, changed, demand, oldest, unserved, params, mode_age, total_gpus, frac)
     idle = [(name, g) for name in sorted(current) for g in current[name].gpus
             if g.is_idle() and g.target is None]
-    total_gpus = sum(len(m.gpus) for m in current.values())
     spx_gpus = [(n, g) for n in sorted(current) for g in current[n].gpus if (_mode_of(g) or "").startswith("spx")]
     reserve = min(len(spx_gpus), int(round(spx_demand))) if (params.spx_reserve and total_gpus > 1) else 0
     # idle GPUs whose mode nobody is waiting for go first; SPX GPUs last (they are the reserve)
@@ -716,7 +803,8 @@ class PodController:
         by_name = {ko.name(n): n for n in nodes}
         for name, model in changed.items():
             plan_id = new_plan_id(self.clock)
-            self.partitioner.apply_partitioning(by_name[name], plan_id, build_node_partitioning(model))
+            self.partitioner.apply_partitioning(by_name[name], plan_id,
+                                                build_node_partitioning(model, getattr(model, "memory_target", None)))
             REGISTRY.repartitions.labels(node=name, kind=self.kind).inc()
             self.plans_written += 1
         return Result(requeue_after=self.retry_after) if req == self.plan_key else Result()

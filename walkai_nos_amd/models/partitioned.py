@@ -154,10 +154,15 @@ class PartitionedNode:
     is_resource: Callable[[str], bool] = lambda r: False
     as_resource: Callable[[str], str] = lambda p: p
     weight: Optional[Callable[[str], float]] = None
+    #: node-wide memory-partition mode (MI355X NPS, e.g. "nps1"): observed, and the one a plan
+    #: switches the node to (every GPU of the node re-partitioned, only when all are idle)
+    memory_partition: Optional[str] = None
+    memory_target: Optional[str] = None
 
     def clone(self) -> "PartitionedNode":
         return PartitionedNode(self.name, [g.clone() for g in self.gpus], dict(self.allocatable),
-                               self.is_resource, self.as_resource, self.weight)
+                               self.is_resource, self.as_resource, self.weight, self.memory_partition,
+                               self.memory_target)
 
     def geometry(self) -> Geometry:
         out: Geometry = {}

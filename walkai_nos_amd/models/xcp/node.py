@@ -53,9 +53,19 @@ def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode
     for i in range(count):
         if i not in gpus:
             gpus[i] = new_gpu(model, i, nps)
+    # a node-wide memory-partition switch in progress (spec NPS != observed): every GPU is
+    # re-partitioned, idle ones included, so none is offered to new pods until the switch lands
+    spec_nps = gpu_util.get_spec_memory_partition(node)
+    switching = spec_nps if spec_nps and spec_nps != nps else None
+    if switching:
+        for idx, g in gpus.items():
+            want = {p: q for p, q in spec_by_gpu.get(idx, {}).items() if q > 0}
+            if want and g.target is None and want != g.geometry():
+                g.target = want
     allocatable = res.from_k8s(ko.node_allocatable(node))
     return PartitionedNode(ko.name(node), [gpus[i] for i in sorted(gpus)], allocatable,
-                           is_resource=is_xcp_resource, as_resource=as_resource_name, weight=SCORING[scoring])
+                           is_resource=is_xcp_resource, as_resource=as_resource_name, weight=SCORING[scoring],
+                           memory_partition=nps, memory_target=switching)
 
 
 def get_requested_profiles(pod: Dict[str, Any]) -> Dict[str, int]:
