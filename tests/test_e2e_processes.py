@@ -266,3 +266,53 @@ def test_memory_partition_switch_over_processes():
             assert c.kubelets[NODE].admission_failures == []
         finally:
             c.stop()
+
+
+def test_component_restarts_and_a_kubelet_restart():
+    """Crash / upgrade scenarios over processes: the partition agent restarts (the GPUs keep their
+    modes: the fake backend persists them as devices do) and resumes reporting and serving; the
+    partitioner restarts and keeps planning from the node annotations; kubelet restarts (plugin
+    sockets wiped, kubelet.sock recreated) and the agent's plugins re-register by themselves."""
+    from walkai_nos_amd.deviceplugin.server import RegistrationServer
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=2)
+        try:
+            c.start()
+            k = c.kubelets[NODE]
+            c.run_until(lambda: c.allocatable(NODE, "spx_nps1") == 2, 30, "the node to report")
+            for i in range(8):
+                c.submit(f"c{i}", "cpx_nps1")
+            c.run_until(lambda: all(c.phase(f"c{i}") == "Running" for i in range(8)), 60, "the 1/8 pods")
+            settled = {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8", "nos.nebuly.com/status-gpu-1-spx_nps1-free": "1"}
+
+            def status():
+                return {k_: v for k_, v in ko.annotations(c.client.get("Node", NODE)).items() if "status-gpu" in k_}
+            c.run_until(lambda: status() == settled, 30, "the layout to be reported")
+            c.restart("partitionagent-node-0")
+            c.run_until(lambda: status() == settled and len(k.healthy("amd.com/spx_nps1")) == 1
+                        and len(k.healthy("amd.com/cpx_nps1")) == 8, 30,
+                        "the restarted agent to report and serve the same layout")
+            c.submit("s0", "spx_nps1")
+            c.run_until(lambda: c.phase("s0") == "Running", 30, "a whole-GPU pod after the agent restart")
+
+            c.restart("gpupartitioner")
+            for i in range(8):
+                k.finish("default", f"c{i}")
+            for i in range(2):
+                c.submit(f"d{i}", "dpx_nps1")
+            c.run_until(lambda: all(c.phase(f"d{i}") == "Running" for i in range(2)), 60,
+                        "1/2 pods planned by the restarted partitioner")
+
+            k.reg.stop()
+            for f in os.listdir(k.dir):
+                os.unlink(os.path.join(k.dir, f))
+            k.reg = RegistrationServer(os.path.join(k.dir, "kubelet.sock")).start()
+            k.readers.clear()
+            c.run_until(lambda: {r.resource_name for r in k.reg.registered} >= {"amd.com/dpx_nps1", "amd.com/spx_nps1"},
+                        30, "re-registration after the kubelet restart")
+            k.finish("default", "d0")
+            c.submit("d2", "dpx_nps1")
+            c.run_until(lambda: c.phase("d2") == "Running", 30, "admission after the kubelet restart")
+            assert k.admission_failures == []
+        finally:
+            c.stop()

@@ -112,6 +112,7 @@ class AgentConfig(ManagerConfig):
     reportConfigIntervalSeconds: float = 10.0
     amdSmiBackend: str = "native"           # native | fake
     fakeGpus: int = 8                       # GPUs of the fake backend (development clusters, e2e tests)
+    fakeStateFile: str = ""                 # fake backend: keep GPU modes in this file across agent restarts
     devicePluginLabel: str = constant.DEFAULT_DEVICE_PLUGIN_LABEL
     devicePluginNamespace: str = ""
     podResourcesSocket: str = constant.DEFAULT_POD_RESOURCES_SOCKET

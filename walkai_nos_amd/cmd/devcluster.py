@@ -72,6 +72,7 @@ class DevCluster:
         self.kind = kind                         # xcp: partition agents; cumask: CU-mask slice agents
         self.facade = APIFacade(bookmark_every=bookmark_every)
         self.procs: Dict[str, subprocess.Popen] = {}
+        self._argv: Dict[str, Any] = {}
         self.logs: Dict[str, str] = {}
         self.kubelets: Dict[str, FakeKubelet] = {}
         self.client: Any = None
@@ -95,7 +96,8 @@ class DevCluster:
             common = dict(healthProbeBindAddress="0", metricsBindAddress="0",
                           reportConfigIntervalSeconds=self.report_interval, amdSmiBackend=self.amd_smi_backend,
                           fakeGpus=self.gpus, podResourcesSocket=k.podres_socket, commitBarrier="none",
-                          probeOnCommit=False, devicePluginDir=k.dir)
+                          probeOnCommit=False, devicePluginDir=k.dir,
+                          fakeStateFile=os.path.join(k.root, "fake-amdsmi.json"))
             if self.kind == api.PARTITIONING_KIND_CUMASK:
                 self._spawn(f"sliceagent-{n}", "walkai_nos_amd.cmd.sliceagent", GpuAgentConfig(**common),
                             "GpuAgentConfig", {constant.ENV_NODE_NAME: n})
@@ -110,6 +112,20 @@ class DevCluster:
                                        on_bind=self._on_bind)
         return self
 
+    def restart(self, name: str) -> None:
+        """Stop a component process and start it again with the same configuration (crash /
+        upgrade scenarios: the agent's start-up reconciliation, the partitioner's re-planning)."""
+        p = self.procs[name]
+        p.terminate()
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        argv, env = self._argv[name]
+        with open(self.logs[name], "a") as out:
+            self.procs[name] = subprocess.Popen(argv, stdout=out, stderr=subprocess.STDOUT, env=env, cwd=self.root)
+
     def _spawn(self, name: str, module: str, cfg: Any, kind: str, env: Dict[str, str],
                extra: Optional[List[str]] = None) -> None:
         argv = [sys.executable, "-m", module, "--kubeconfig", self.kubeconfig] + list(extra or [])
@@ -120,6 +136,7 @@ class DevCluster:
             argv += ["--config", path]
         self.logs[name] = os.path.join(self.root, f"{name}.log")
         e = dict(os.environ, PYTHONPATH=REPO + os.pathsep + os.environ.get("PYTHONPATH", ""), **env)
+        self._argv[name] = (argv, e)
         with open(self.logs[name], "w") as out:
             self.procs[name] = subprocess.Popen(argv, stdout=out, stderr=subprocess.STDOUT, env=e, cwd=self.root)
 

@@ -68,7 +68,7 @@ def main(argv=None) -> int:
     apply_manager_flags(cfg, args)
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node",))
-    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)
+    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus, state_file=cfg.fakeStateFile)
     gpus = smi.list_gpus()
     if not gpus:
         log.error("no AMD GPU found on node %s", node)

@@ -36,7 +36,7 @@ def main(argv=None) -> int:
     apply_manager_flags(cfg, args)
     node = get_env_or_panic(constant.ENV_NODE_NAME)
     client = make_client(args.kubeconfig, cached=("Node", "ConfigMap"))
-    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus)
+    smi = new_backend(cfg.amdSmiBackend, n_gpus=cfg.fakeGpus, state_file=cfg.fakeStateFile)
     if any_partitioned_gpu(smi):
         log.error("CU-mask slicing needs every GPU in SPX mode; use the partition agent on this node")
         return 1

@@ -218,8 +218,12 @@ class FakeAmdSmi(AmdSmi):
 
     def __init__(self, n_gpus: int = 8, model: str = "MI355X", is_root: bool = True,
                  fail_set: Optional[Set[int]] = None, busy: Optional[Set[int]] = None, fail_next: int = 0,
-                 memory_mode_requires_idle: bool = True):
+                 memory_mode_requires_idle: bool = True, state_file: str = ""):
+        """``state_file``: keep the modes in a JSON file, so a restarted process finds the GPUs in
+        the modes it left them (as the real devices stay) — the agent-restart scenarios of the
+        development cluster."""
         super().__init__()
+        self.state_file = state_file
         self.n_gpus, self.model, self.is_root = n_gpus, model, is_root
         self.fail_set: Set[int] = set(fail_set or ())      # GPU indexes whose set fails
         self.busy: Set[int] = set(busy or ())              # GPU indexes reported busy
@@ -233,6 +237,20 @@ class FakeAmdSmi(AmdSmi):
         self._gpus = [_FakeGpu(i, f"GPU-fake-{i:04x}", f"0000:{0x05 + i * 0x10:02x}:00.0") for i in range(n_gpus)]
         self.set_calls: List[tuple] = []
         self.reenumerations = 0
+        if state_file and os.path.exists(state_file):
+            import json
+            with open(state_file) as f:
+                modes = json.load(f)
+            for g, m in zip(self._gpus, modes):
+                g.compute, g.memory = m["compute"], m["memory"]
+
+    def _save(self) -> None:
+        if self.state_file:
+            import json
+            tmp = self.state_file + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump([{"compute": g.compute, "memory": g.memory} for g in self._gpus], f)
+            os.replace(tmp, self.state_file)
 
     # -- hooks ---------------------------------------------------------------------------------
     def _processors(self, reinit: bool) -> List[ProcInfo]:
@@ -290,6 +308,7 @@ class FakeAmdSmi(AmdSmi):
             g.processes.clear()
             self.set_calls.append(("compute", g.index, mode))
             self.reenumerations += 1
+            self._save()
 
     def _set_memory_partition(self, proc: ProcInfo, mode: str) -> None:
         with self._lock:
@@ -304,6 +323,7 @@ class FakeAmdSmi(AmdSmi):
                     g.compute = {1: "SPX", 2: "DPX", 4: "QPX", 8: "CPX"}[nps]
             self.set_calls.append(("memory", None, mode))
             self.reenumerations += 1
+            self._save()
 
     def _process_count(self, proc: ProcInfo) -> int:
         g = self._gpu_of(proc)

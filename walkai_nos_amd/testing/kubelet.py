@@ -41,6 +41,7 @@ class FakeKubelet:
         self.allocations: Dict[Tuple[str, str], List[str]] = {}  # (ns, pod) -> host device paths
         self.envs: Dict[Tuple[str, str], Dict[str, str]] = {}     # (ns, pod) -> env Allocate injected
         self.lock = threading.Lock()
+        self._published: set = set()
         self.podres_socket = os.path.join(root, "pod-resources.sock")
         self.podres = PodResourcesServer(self.podres_socket, self._used, self._alloc).start()
 
@@ -66,6 +67,10 @@ class FakeKubelet:
             pass
         finally:
             ch.close()
+            # the plugin went away (restart, crash): its devices are gone until it registers again,
+            # as kubelet drops a plugin's devices when its endpoint closes
+            with self.lock:
+                self.devices.pop(resource, None)
 
     def sync(self) -> None:
         """(Re)open a ListAndWatch stream for every registered resource whose stream is gone, and
@@ -84,6 +89,9 @@ class FakeKubelet:
         with self.lock:
             alloc = {r: str(sum(1 for _, h in ds if h == dp.HEALTHY)) for r, ds in self.devices.items()}
             cap = {r: str(len(ds)) for r, ds in self.devices.items()}
+        for r in self._published - set(alloc):   # a resource whose plugin is gone counts 0
+            alloc[r] = cap[r] = "0"
+        self._published |= set(alloc)
         if not alloc:
             return
         st = (self.client.get("Node", self.node).get("status") or {})
