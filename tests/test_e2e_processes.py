@@ -316,3 +316,39 @@ def test_component_restarts_and_a_kubelet_restart():
             assert k.admission_failures == []
         finally:
             c.stop()
+
+
+def test_partitioner_leader_election_failover_over_rest():
+    """Two partitioner replicas with leader election (a coordination.k8s.io Lease over the REST
+    API): one holds the lease; the leader is killed; the standby takes the lease over once it
+    expires and plans the next pods."""
+    from walkai_nos_amd.cmd.devcluster import fast_partitioner_config
+    cfg = fast_partitioner_config()
+    le = cfg.leaderElection
+    le.leaderElect, le.resourceName = True, "gpu-partitioner.nos.nebuly.com"
+    le.leaseDurationSeconds, le.renewDeadlineSeconds, le.retryPeriodSeconds = 3.0, 2.0, 0.5
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=2, partitioner=cfg)
+        try:
+            c.start()
+            c._spawn("gpupartitioner-2", "walkai_nos_amd.cmd.gpupartitioner", cfg, "GpuPartitionerConfig", {})
+            c.run_until(lambda: c.allocatable(NODE, "spx_nps1") == 2, 30, "the node to report")
+
+            def holder():
+                leases = c.client.list("Lease")
+                return leases[0]["spec"].get("holderIdentity") if leases else None
+            c.run_until(lambda: holder() is not None, 20, "a leader")
+            first = holder()
+            leader = next(n for n in ("gpupartitioner", "gpupartitioner-2") if first in open(c.logs[n]).read())
+            for i in range(8):
+                c.submit(f"c{i}", "cpx_nps1")
+            c.run_until(lambda: all(c.phase(f"c{i}") == "Running" for i in range(8)), 60, "pods planned by the leader")
+            c.procs[leader].kill()
+            c.procs[leader].wait()
+            del c.procs[leader]
+            c.run_until(lambda: holder() not in (None, first), 30, "the standby to take the lease")
+            for i in range(2):
+                c.submit(f"d{i}", "dpx_nps1")
+            c.run_until(lambda: all(c.phase(f"d{i}") == "Running" for i in range(2)), 60, "pods planned by the new leader")
+        finally:
+            c.stop()
