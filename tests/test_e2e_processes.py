@@ -352,3 +352,38 @@ def test_partitioner_leader_election_failover_over_rest():
             c.run_until(lambda: all(c.phase(f"d{i}") == "Running" for i in range(2)), 60, "pods planned by the new leader")
         finally:
             c.stop()
+
+
+def test_churn_soak_over_processes():
+    """Random fractional pods (1/8, 1/2, whole GPU; 2-6 s lifetimes) arriving for 25 s on two
+    2-GPU nodes, run by the binaries: flips and drains happen under kube-scheduler semantics and
+    no pod is ever admitted to a partition its plugin withholds (zero admission failures); once
+    arrivals stop, every waiting pod runs."""
+    import random
+    rng = random.Random(7)
+    mix = [("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2)]
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=2, gpus=2)
+        try:
+            c.start()
+            c.run_until(lambda: all(c.allocatable(n, "spx_nps1") == 2 for n in c.kubelets), 30, "the nodes to report")
+            seq, t_end = 0, time.time() + 25
+            while time.time() < t_end:
+                if rng.random() < 0.35:
+                    r, acc, prof = rng.random(), 0.0, mix[-1][0]
+                    for p, w in mix:
+                        acc += w
+                        if r < acc:
+                            prof = p
+                            break
+                    c.submit(f"p{seq}", prof, runtime_s=rng.uniform(2, 6))
+                    seq += 1
+                c.step()
+                time.sleep(0.2)
+            c.run_until(lambda: all(ko.pod_phase(p) != "Pending" for p in c.client.list("Pod")), 150,
+                        "every waiting pod to run")
+            assert seq > 20
+            fails = [f for k in c.kubelets.values() for f in k.admission_failures]
+            assert fails == [], fails
+        finally:
+            c.stop()

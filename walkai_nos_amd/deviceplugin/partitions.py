@@ -221,9 +221,13 @@ def partition_plugin_manager(state: PartitionState, socket_dir: str = DEVICE_PLU
 
 
 class AllocatablePublisher:
-    """Patches the node's ``status.allocatable`` with the healthy partition counts of a view (the
-    partition agent's eager update: kubelet's own node status sync runs every 10 s, and a scheduler
-    reading a stale allocatable would bind pods that kubelet then rejects at admission)."""
+    """Patches the node's ``status.allocatable`` when the healthy partition counts of a view DROP
+    (a drain starting, a flip taking partitions away, a GPU lost): kubelet's own node-status sync
+    runs every 10 s, and a scheduler reading the stale, higher count would bind pods that kubelet
+    then rejects at admission. Increases are left to kubelet, which publishes a resource only once
+    its device manager holds the devices: published first by the agent, a partition kubelet has
+    not yet received through ListAndWatch would be bound and then fail admission
+    (``UnexpectedAdmissionError``; found by ``tests/test_e2e_processes.py::test_churn_soak_over_processes``)."""
 
     def __init__(self, client: Any, node: str):
         self.client = client
@@ -231,17 +235,25 @@ class AllocatablePublisher:
         self.patches = 0
 
     def publish(self, view: Mapping[str, List[PartitionDevice]]) -> bool:
-        want = {r: str(sum(1 for d in ds if d.healthy)) for r, ds in view.items()}
+        healthy = {r: sum(1 for d in ds if d.healthy) for r, ds in view.items()}
         try:
             cur = (self.client.get("Node", self.node).get("status") or {}).get("allocatable") or {}
         except Exception as e:  # noqa: BLE001 - kubelet's own sync still gets there
             log.warning("node %s unavailable for the allocatable update: %s", self.node, e)
             return False
-        # partition resources no longer served drop to 0 (kubelet keeps a registered resource at 0)
-        for r in cur:
-            if r.startswith(constant.AMD_RESOURCE_PREFIX) and r not in want and _is_partition_resource(r):
-                want[r] = "0"
-        if all(cur.get(r) == v for r, v in want.items()):
+        want: Dict[str, str] = {}
+        for r, v in cur.items():
+            if not (r.startswith(constant.AMD_RESOURCE_PREFIX) and _is_partition_resource(r)):
+                continue
+            # only decreases: a resource no longer served drops to 0 (kubelet keeps a registered
+            # resource at 0), fewer healthy partitions lower it; more are kubelet's to publish
+            n = healthy.get(r, 0)
+            try:
+                if n < int(v):
+                    want[r] = str(n)
+            except ValueError:
+                want[r] = str(n)
+        if not want:
             return False
         self.client.patch("Node", self.node, {"status": {"allocatable": want}})
         self.patches += 1
