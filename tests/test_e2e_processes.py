@@ -171,6 +171,43 @@ def test_quota_processes_borrow_and_reclaim():
             c.stop()
 
 
+def test_quota_reclaim_that_needs_a_mode_flip_over_processes():
+    """Team A borrows both GPUs in CPX (16 x 1/8 GPU); team B reclaims a whole SPX GPU.  No node
+    offers spx, so ordinary preemption cannot help: nos-scheduler evicts every pod of one GPU (all
+    over-quota, per the agent's status-pods annotation), holds B's request against its quota so A
+    cannot take the GPU back, and the partitioner flips the idle GPU for B."""
+    from walkai_nos_amd.api import v1alpha1 as api
+
+    def quota(ns):
+        return {"apiVersion": api.API_VERSION, "kind": api.KIND_ELASTIC_QUOTA,
+                "metadata": {"name": f"q-{ns}", "namespace": ns},
+                "spec": {"min": {api.RESOURCE_GPU_MEMORY: "288"}}}
+
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=2, quota=True)
+        try:
+            c.start()
+            c.run_until(lambda: c.allocatable("node-0", "spx_nps1") == 2, 30, "two idle GPUs")
+            for ns in ("team-a", "team-b"):
+                c.client.create(quota(ns))
+            for i in range(16):
+                c.submit(f"a{i}", "cpx_nps1", namespace="team-a", scheduler_name="nos-scheduler")
+            c.run_until(lambda: all(c.phase(f"a{i}", "team-a") == "Running" for i in range(16)), 90,
+                        "team A on both GPUs in CPX")
+            c.submit("b0", "spx_nps1", namespace="team-b", scheduler_name="nos-scheduler")
+            # team A keeps resubmitting (as a Job controller would): the held quota keeps them pending
+            for i in range(16, 20):
+                c.submit(f"a{i}", "cpx_nps1", namespace="team-a", scheduler_name="nos-scheduler")
+            c.run_until(lambda: c.phase("b0", "team-b") == "Running", 120, "team B's whole GPU")
+            running_a = [p for p in c.client.list("Pod", "team-a") if p.get("status", {}).get("phase") == "Running"]
+            assert len(running_a) == 8                      # one GPU's worth of A's pods was evicted
+            b0 = c.client.get("Pod", "b0", "team-b")
+            assert ko.annotations(b0).get(api.ANNOTATION_QUOTA_RECLAIM) == "node-0"
+            assert all(c.phase(f"a{i}", "team-a") == "Pending" for i in range(16, 20))
+        finally:
+            c.stop()
+
+
 def test_slice_agent_process_serves_cu_mask_slices():
     """A cumask node: the partitioner plans CU-mask slices for pending slice pods, the slice agent
     process materialises them in its slice store and its device plugin serves them; kubelet's

@@ -183,3 +183,53 @@ def test_erq_on_partitioned_nodes_borrow_reclaim_under_churn():
     late = [x for x in r["samples"] if x["epoch"] >= 30]
     assert all(x["used_gb"]["team-a"] <= 2 * share for x in late)
     assert sum(x["used_gb"]["team-b"] for x in late) / len(late) >= 0.6 * share
+
+
+def test_nos_scheduler_frees_a_whole_gpu_for_a_profile_no_node_offers():
+    """A reclaiming spx pod on a node whose GPUs are all CPX: the scheduler evicts the pods of the
+    GPU the partitioner is draining for spx (all over-quota), not those of a GPU holding an
+    in-quota pod, marks the pod quota-reclaim and holds its request against its quota."""
+    import json
+    from walkai_nos_amd.api import v1alpha1 as v1
+    from walkai_nos_amd.quota.scheduler import SCHEDULER_NAME, NosScheduler
+    api = InMemoryAPIServer()
+    n = _node("n0")
+    n["status"]["allocatable"].update({"amd.com/cpx_nps1": "16"})
+    anns = {"nos.nebuly.com/status-gpu-0-cpx_nps1-used": "8", "nos.nebuly.com/status-gpu-1-cpx_nps1-used": "8",
+            "nos.nebuly.com/status-gpu-2-cpx_nps1-used": "8",
+            "nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", "nos.nebuly.com/spec-gpu-1-cpx_nps1": "8",
+            "nos.nebuly.com/spec-gpu-2-spx_nps1": "1",
+            v1.ANNOTATION_MEMORY_PARTITION_STATUS: "nps1"}
+    gpus = {0: [f"team-a/a{i}" for i in range(8)], 1: [f"team-a/a{i}" for i in range(8, 15)] + ["team-c/c0"],
+            2: [f"team-a/a{i}" for i in range(15, 23)]}
+    anns[v1.ANNOTATION_GPU_PODS_STATUS] = json.dumps({str(g): v for g, v in gpus.items()})
+    n["metadata"]["annotations"] = anns
+    n["status"]["allocatable"]["amd.com/cpx_nps1"] = "24"
+    api.create(n)
+    for ns, gb in (("team-a", 288), ("team-b", 288), ("team-c", 288)):
+        api.create({"apiVersion": v1.API_VERSION, "kind": v1.KIND_ELASTIC_QUOTA, "metadata": {"name": f"q-{ns}", "namespace": ns},
+                    "spec": {"min": {v1.RESOURCE_GPU_MEMORY: str(gb)}}})
+    t = 0
+    for g, keys in gpus.items():
+        for k in keys:
+            ns, name = k.split("/")
+            p = ko.new_pod(name, ns, requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME)
+            p["spec"]["nodeName"] = "n0"
+            p["status"]["phase"] = "Running"
+            p["metadata"]["creationTimestamp"] = f"2026-01-01T00:00:{t:02d}Z"
+            t += 1
+            api.create(p)
+    s = NosScheduler(api)
+    b = ko.new_pod("b0", "team-b", requests={"amd.com/spx_nps1": 1}, scheduler_name=SCHEDULER_NAME)
+    api.create(b)
+    s.reconcile(NosScheduler.KEY)
+    left = {ko.name(p) for p in api.list("Pod", "team-a")}
+    assert left == {f"a{i}" for i in range(15)}            # GPU 2 (draining for spx) was freed
+    b = api.get("Pod", "b0", "team-b")
+    assert ko.annotations(b).get(v1.ANNOTATION_QUOTA_RECLAIM) == "n0" and not ko.pod_node_name(b)
+    # a second cycle before the agent reports: GPU 2's pods are gone, so nothing more is evicted,
+    # and a new team-A pod cannot borrow the held share
+    api.create(ko.new_pod("a99", "team-a", requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME))
+    s.reconcile(NosScheduler.KEY)
+    assert len(api.list("Pod", "team-a")) == 16 and not ko.pod_node_name(api.get("Pod", "a99", "team-a"))
+    assert s.preempted == 8

@@ -43,6 +43,12 @@ ANNOTATION_COMMIT_STATUS = "nos.nebuly.com/status-partitioning-commit"
 ANNOTATION_INFLIGHT_PLAN = "nos.nebuly.com/status-partitioning-inflight"
 # MI355X: probe-kernel measurement published by the agent (JSON: per slice TFLOP/s per CU)
 ANNOTATION_PROBE_RESULT = "nos.nebuly.com/status-probe"
+# MI355X: pods per physical GPU as the agent reads them from kubelet's PodResources (JSON
+# {"<gpu index>": ["<ns>/<pod>", ...]}): what nos-scheduler must evict to free a whole GPU for a flip
+ANNOTATION_GPU_PODS_STATUS = "nos.nebuly.com/status-pods"
+# MI355X (pods): set by nos-scheduler on a pod it evicted a whole GPU for (value: the node); the
+# pod's request stays held against its quota until it is bound, so borrowers cannot take it back
+ANNOTATION_QUOTA_RECLAIM = "nos.nebuly.com/quota-reclaim"
 
 # -- resources (reference constants.go:24-27) ------------------------------------------
 RESOURCE_GPU_MEMORY = "nos.nebuly.com/gpu-memory"

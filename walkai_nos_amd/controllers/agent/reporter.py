@@ -58,6 +58,10 @@ class Reporter:
         nps = self._nps()
         if nps:
             desired_extra[api.ANNOTATION_MEMORY_PARTITION_STATUS] = nps
+        pods = getattr(self.pc, "pods_by_gpu", None)
+        if pods is not None:
+            desired_extra[api.ANNOTATION_GPU_PODS_STATUS] = json.dumps({str(g): v for g, v in pods().items()},
+                                                                       sort_keys=True, separators=(",", ":"))
         if self.shared.last_commit:
             desired_extra[api.ANNOTATION_COMMIT_STATUS] = self.shared.last_commit
         if self.extra is not None:

@@ -566,7 +566,9 @@ class PodController:
 
     # -- helpers -------------------------------------------------------------------------
     def should_consider(self, pod: Dict[str, Any]) -> bool:
-        return podutil.is_pending(pod) and not podutil.is_scheduled(pod) and podutil.is_unschedulable(pod)
+        # a pod nos-scheduler holds back for its quota would not run on a new partition either
+        return podutil.is_pending(pod) and not podutil.is_scheduled(pod) and podutil.is_unschedulable(pod) \
+            and not podutil.is_blocked_by_quota(pod)
 
     def list_nodes(self) -> List[Dict[str, Any]]:
         return self.client.list("Node", label_selector=f"{api.LABEL_GPU_PARTITIONING}={self.kind}", copy=False)

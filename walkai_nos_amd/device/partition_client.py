@@ -14,7 +14,7 @@ from __future__ import annotations
 
 import logging
 import time
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 from ..models.device import STATUS_FREE, DeviceList, GpuDevice
 from ..models.errors import GpuError
@@ -56,6 +56,17 @@ class PartitionClient:
                 log.debug("device %s: GPU not found, skipping", device_id)
                 return None
             raise
+
+    def pods_by_gpu(self) -> Dict[int, List[str]]:
+        """Physical GPU index -> ``<ns>/<pod>`` of the pods using one of its partitions."""
+        out: Dict[int, set] = {}
+        for ns, pod, d in self.resources.get_used_devices_by_pod():
+            if not is_xcp_resource(d.resource_name):
+                continue
+            g = self._gpu_index(d.device_id)
+            if g is not None:
+                out.setdefault(g, set()).add(f"{ns}/{pod}")
+        return {g: sorted(v) for g, v in sorted(out.items())}
 
     def current_profiles(self) -> Dict[int, str]:
         """Physical GPU index -> current profile name (``<mode>_<nps>``) from the device map."""

@@ -36,6 +36,10 @@ class ResourceClient:
     def get_allocatable_devices(self) -> List[Device]:
         raise NotImplementedError
 
+    def get_used_devices_by_pod(self) -> List[Tuple[str, str, Device]]:
+        """[(namespace, pod, device)] of running containers; empty when the source cannot tell."""
+        return []
+
 
 class PodResourcesClient(ResourceClient):
     def __init__(self, socket_path: str = constant.DEFAULT_POD_RESOURCES_SOCKET,
@@ -61,6 +65,11 @@ class PodResourcesClient(ResourceClient):
                         out.append(Device(d.resource_name, i, STATUS_USED))
         return out
 
+    def get_used_devices_by_pod(self) -> List[Tuple[str, str, Device]]:
+        resp = self._list(podres.ListPodResourcesRequest(), timeout=self.timeout)
+        return [(p.namespace, p.name, Device(d.resource_name, i, STATUS_USED))
+                for p in resp.pod_resources for c in p.containers for d in c.devices for i in d.device_ids]
+
     def get_allocatable_devices(self) -> List[Device]:
         resp = self._alloc(podres.AllocatableResourcesRequest(), timeout=self.timeout)
         return [Device(d.resource_name, i, STATUS_UNKNOWN) for d in resp.devices for i in d.device_ids]
@@ -72,15 +81,22 @@ class PodResourcesClient(ResourceClient):
 class StaticResourceClient(ResourceClient):
     """In-process client over callables (simulator / unit tests)."""
 
-    def __init__(self, used: Callable[[], Iterable[Tuple[str, str]]], allocatable: Callable[[], Iterable[Tuple[str, str]]]):
+    def __init__(self, used: Callable[[], Iterable[Tuple[str, str]]], allocatable: Callable[[], Iterable[Tuple[str, str]]],
+                 used_by_pod: Optional[Callable[[], Iterable[Tuple[str, str, str, str]]]] = None):
         self._used = used
         self._alloc = allocatable
+        self._by_pod = used_by_pod    # -> [(namespace, pod, resource, id)]
 
     def get_used_devices(self) -> List[Device]:
         return [Device(r, i, STATUS_USED) for r, i in self._used()]
 
     def get_allocatable_devices(self) -> List[Device]:
         return [Device(r, i, STATUS_UNKNOWN) for r, i in self._alloc()]
+
+    def get_used_devices_by_pod(self) -> List[Tuple[str, str, Device]]:
+        if self._by_pod is None:
+            return []
+        return [(ns, p, Device(r, i, STATUS_USED)) for ns, p, r, i in self._by_pod()]
 
 
 class PodResourcesServer:

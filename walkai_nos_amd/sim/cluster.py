@@ -171,7 +171,9 @@ class SimKubelet:
     def resource_client(self) -> StaticResourceClient:
         # PodResources GetAllocatableResources lists every registered device, healthy or not
         return StaticResourceClient(lambda: [(r, i) for devs in self.allocations.values() for r, i in devs],
-                                    lambda: [(r, i) for r, ids in self.plugin.advertised.items() for i in ids])
+                                    lambda: [(r, i) for r, ids in self.plugin.advertised.items() for i in ids],
+                                    lambda: [(ns, p, r, i) for (ns, p), devs in list(self.allocations.items())
+                                             for r, i in devs])
 
     def allocatable(self) -> Dict[str, str]:
         out = {"cpu": "256", "memory": "2048Gi", "pods": "250"}

@@ -11,9 +11,9 @@ are under ``min``, preempt over-quota pods to reclaim), the partitioner and the 
 
 Reported per quantum and summarised: each team's ``used`` against its ``min``, the node's
 allocation, and the **reclaim latency** — from the preemption nos-scheduler makes for a
-reclaiming pod to that pod being bound.  A reclaiming pod whose profile no preemption can free
-(the node has no partition of that mode) waits for the partitioner to drain a GPU instead: every
-team-B pod's wait (creation -> bound) is reported as ``team_b_wait_s``.
+reclaiming pod to that pod being bound.  A reclaiming pod whose profile no node offers has a whole
+GPU freed for it (every pod of one GPU evicted, quota/scheduler.py) and waits for the partitioner
+to flip it: every team-B pod's wait (creation -> bound) is reported as ``team_b_wait_s``.
 """
 from __future__ import annotations
 

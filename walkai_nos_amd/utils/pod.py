@@ -33,6 +33,17 @@ def is_unschedulable(pod: Obj) -> bool:
     return False
 
 
+# nos-scheduler's PreFilter messages (quota/scheduler.py): the pod waits for quota, not for devices
+QUOTA_UNSCHEDULABLE_PREFIX = "quota "
+
+
+def is_blocked_by_quota(pod: Obj) -> bool:
+    for c in pod.get("status", {}).get("conditions") or []:
+        if c.get("type") == "PodScheduled" and c.get("reason") == "Unschedulable":
+            return (c.get("message") or "").startswith(QUOTA_UNSCHEDULABLE_PREFIX)
+    return False
+
+
 def is_owned_by(pod: Obj, api_version: str, kind: str) -> bool:
     for ref in pod.get("metadata", {}).get("ownerReferences") or []:
         if ref.get("apiVersion") == api_version and ref.get("kind") == kind:
