@@ -4,7 +4,7 @@ IMG ?= ghcr.io/walkai/nos-mi355x:0.1.0
 CLIENT_IMG ?= ghcr.io/walkai/nos-mi355x-client:0.1.0
 NAMESPACE ?= nos-system
 
-.PHONY: all native test test-gpu lint sanitize bench bench-8 smoke simulate devcluster kbench docker-build docker-push \
+.PHONY: all native test test-gpu lint sanitize helm-docs bench bench-8 smoke simulate devcluster kbench docker-build docker-push \
         deploy undeploy install-crds helm-install helm-uninstall kind-up clean
 
 all: native test
@@ -65,6 +65,9 @@ helm-install:
 
 helm-uninstall:
 	helm uninstall nos -n $(NAMESPACE)
+
+helm-docs:         ## regenerate helm-charts/nos/README.md from values.yaml's `# --` comments
+	$(PYTHON) hack/helm_docs.py
 
 kind-up:
 	kind create cluster --config hack/kind/cluster.yaml

@@ -179,6 +179,24 @@ def test_metrics_behind_kube_rbac_proxy_and_optional_service_monitor():
     assert mon["kind"] == "ServiceMonitor" and mon["spec"]["endpoints"][0]["port"] == "https"
 
 
+def test_chart_readme_is_generated_from_values():
+    """helm-charts/nos/README.md is hack/helm_docs.py's rendering of values.yaml (helm-docs'
+    convention, ref Makefile:110-111): every value has a row, and every row is documented."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, _p("hack/helm_docs.py"), "--check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    sys.path.insert(0, _p("hack"))
+    import helm_docs
+    text = open(_p("helm-charts/nos/values.yaml")).read()
+    import yaml
+    rows = helm_docs.rows(yaml.safe_load(text), helm_docs.key_comments(text))
+    keys = {r[0] for r in rows}
+    assert {"gpuPartitioner.planningPolicy", "partitionAgent.commitBarrier", "scheduler.name",
+            "operator.resources", "image.tag"} <= keys
+    assert all(r[3] for r in rows), [r[0] for r in rows if not r[3]]
+
+
 def test_lint_is_clean_and_fails_on_errors(tmp_path):
     import subprocess
     import sys
