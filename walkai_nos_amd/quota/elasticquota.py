@@ -135,12 +135,20 @@ class QuotaSet:
         return True
 
     def may_preempt(self, preemptor: QuotaInfo, req: Mapping[str, int], victim: QuotaInfo) -> bool:
-        """Fair-share conditions 2 and 3 (condition 1, victim over-quota, is per pod)."""
+        """Fair-share conditions 2 and 3 (condition 1, victim over-quota, is per pod).
+
+        A preemptor that stays within its own ``min`` is reclaiming what it lent: any quota using
+        more than its ``min`` may lose pods to it (as the upstream capacity-scheduling plugin
+        lets an in-min preemptor take from over-min quotas).  Condition 3's guaranteed share is
+        computed from the *unused* guarantees, and the preemptor's is about to be used: counting
+        it as lendable would let the borrower keep part of the very quota being reclaimed."""
         if preemptor is victim:
             return False
         relevant = [r for r in preemptor.resources() if req.get(r, 0) > 0]
         if not relevant:
             return False
+        if all(preemptor.used.get(r, 0) + req[r] <= preemptor.min.get(r, 0) for r in relevant):
+            return any(victim.used_over_quota(r) > 0 for r in relevant)
         for r in relevant:
             if preemptor.used.get(r, 0) + req[r] > preemptor.min.get(r, 0) + self.guaranteed_over_quota(preemptor, r):
                 return False
