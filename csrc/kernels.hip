@@ -1451,7 +1451,7 @@ int nos_attention_x3_wg_per_cu() {
 // nos_attention_ws_bytes of the LDS variant (variant 0 layout), merged by the same fixup kernel.
 static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
                                int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream,
-                               bool f32in) {
+                               bool f32in, bool fixup = true) {
   if ((out == nullptr) == (outp == nullptr)) {
     g_err = "attention x3: exactly one of out / outp";
     return -1;
@@ -1518,6 +1518,7 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
     hipLaunchKernelGGL(attn_fwd_x3p<4>, grid, dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B,
                        T, hn, h0, H, sl2, pk);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
+  if (!fixup) return 0;  // the partials are merged by the consumer (attn_proj.hip)
   if (G == 8)
     hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(B * hn * QG * 8, pin)), dim3(256), 0, s,
                        part_o, part_ml,
@@ -1538,6 +1539,18 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
 int nos_attention_x3f_sk_heads(const float* qkv, float* out, void* outp, float* ws, int B, int T, int H, int h0,
                                int hn, int head_dim, float scale, int waves, void* stream) {
   return attention_x3_launch(qkv, 8, out, outp, ws, B, T, H, h0, hn, head_dim, scale, waves, stream, true);
+}
+
+// The x3 attention from fp32 QKV over all heads WITHOUT the stream-K fixup: split query tiles
+// leave their partials in ws, tiles one workgroup finished go to `out` (fp32); the fused
+// merge + projection + LayerNorm kernel (nos_attn_merge_proj_ln) consumes both.
+int nos_attention_x3f_partials(const float* qkv, float* out, float* ws, int B, int T, int H, int head_dim,
+                               float scale, int waves, void* stream) {
+  if (out == nullptr) {
+    g_err = "attention x3 partials: needs the fp32 direct-output buffer";
+    return -1;
+  }
+  return attention_x3_launch(qkv, 8, out, nullptr, ws, B, T, H, 0, H, head_dim, scale, waves, stream, true, false);
 }
 
 int nos_attention_x3_sk(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B, int T,

@@ -464,3 +464,34 @@ def test_linear_residual_ln_x3_tuned_pipeline(K):
     assert (x - x_ref).abs().max().item() < 1e-4
     assert (h3.double().sum(0) - h_ref.double().sum(0)).abs().max().item() < 1e-4
     assert G.fused_table()
+
+
+@pytest.mark.parametrize("B,T,waves", [(1, 3401, None), (1, 3401, 32), (1, 3401, 126), (1, 3401, 500),
+                                       (2, 77, 5), (2, 200, None), (3, 45, 7)])
+def test_attention_merge_proj_layernorm_fused(K, B, T, waves):
+    # attention partials + the fused merge / projection / residual / LayerNorm kernel vs fp64, over
+    # stream-K grids that split query tiles 2-4 ways, leave whole groups to one workgroup, and
+    # batches whose rows straddle the kernel's 32-row tiles; and vs the unfused fixup + GEMM + LN
+    import torch.nn.functional as F
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(12)
+    H, Dh = 6, 64
+    D = H * Dh
+    qkv = torch.randn(B, T, 3 * D, device="cuda")
+    w = torch.randn(D, D, device="cuda") * 0.05
+    b = torch.randn(D, device="cuda")
+    r = torch.randn(B, T, D, device="cuda")
+    lw, lb = torch.randn(D, device="cuda"), torch.randn(D, device="cuda")
+    x, h3 = K.attention_proj_ln_x3f(qkv, H, Dh, 0.125, w, b, r, (lw, lb, 1e-12), waves=waves)
+    torch.cuda.synchronize()
+    o = _ref_attention(qkv, H, Dh, 0.125).double()
+    ref_x = o @ G.weight_planes(w).double().sum(0).t() + b.double() + r.double()
+    ref_ln = F.layer_norm(ref_x, (D,), lw.double(), lb.double(), 1e-12)
+    assert x.shape == r.shape and h3.shape == (3,) + r.shape
+    assert (x.double() - ref_x).abs().max().item() < 1e-4
+    assert (h3.double().sum(0) - ref_ln).abs().max().item() < 1e-4
+    o3 = K.attention_qkv_x3f(qkv, H, Dh, 0.125)
+    x2, h2 = K.linear_residual_ln_x3(o3, w, b, r, ln=(lw, lb, 1e-12))
+    torch.cuda.synchronize()
+    assert (x - x2).abs().max().item() < 1e-4
+    assert (h3.double().sum(0) - h2.double().sum(0)).abs().max().item() < 1e-4

@@ -19,6 +19,8 @@
 #   pmc_op             PMC passes over one op (NOS_OP, NOS_SLICE), counters in their own runs
 #   pmc_modes          L2 counters of a partition mode with all partitions busy (NOS_MODE, NOS_PARTS)
 #   kbench             tools/kbench.py per-op / per-mode microbenchmarks (NOS_KBENCH_ARGS)
+#   attn_proj          tools/attn_proj_probe.py: fused merge+projection+LayerNorm vs the unfused launches
+#   pmc_attn_proj      PMC passes over the fused kernel (NOS_ABLATE = its timing-only ablation mask)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$PWD
@@ -88,6 +90,17 @@ for s in "$@"; do
       pmc "$D" p python3 "$ROOT/tools/kbench.py" --only modes --slices "${NOS_MODE:-cpx}" --partitions "${NOS_PARTS:-8}" \
           --out "$D/kb.json" -- TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCC_EA0_RDREQ_sum
       rc=$?; echo "pmc_modes rc=$rc" | tee -a "$OUT/gpu_sh.log"; [ $rc -eq 0 ] || exit $rc ;;
+    attn_proj) step attn_proj 300 python tools/attn_proj_probe.py --iters 400 --out "$OUT/attn_proj.json" ;;
+    pmc_attn_proj)
+      D="$OUT/pmc_attn_proj"; mkdir -p "$D"
+      P=(python3 "$ROOT/tools/attn_proj_probe.py" --iters 40 --ablate "${NOS_ABLATE:-0}" --fused-only)
+      pmc "$D" p1 "${P[@]}" -- SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU \
+          SQ_INSTS_MFMA SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU && \
+      pmc "$D" p2 "${P[@]}" -- SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS \
+          SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT && \
+      pmc "$D" p3 "${P[@]}" -- TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum && \
+      pmc "$D" p4 "${P[@]}" -- TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE
+      rc=$?; echo "pmc_attn_proj rc=$rc" | tee -a "$OUT/gpu_sh.log"; [ $rc -eq 0 ] || exit $rc ;;
     kbench) step kbench 600 python tools/kbench.py ${NOS_KBENCH_ARGS:-} --out "$OUT/kbench.json" ;;
     *) echo "unknown step $s" | tee -a "$OUT/gpu_sh.log"; exit 2 ;;
   esac

@@ -87,12 +87,19 @@ class _Block(nn.Module):
             h3 = K.layernorm_x3(x, self.ln1.weight, self.ln1.bias, eps)
         if K.attention_input_f32():
             qkv = K.linear_x3(h3, self.qkv.weight, self.qkv.bias)
-            o3 = K.attention_qkv_x3f(qkv, H, Dh, 1.0 / math.sqrt(Dh))
+            if K.attn_proj_fusable(H, Dh):
+                # attention partials -> one merge + projection + residual + LN2 kernel
+                x, h3 = K.attention_proj_ln_x3f(qkv, H, Dh, 1.0 / math.sqrt(Dh), self.proj.weight, self.proj.bias,
+                                                x, (self.ln2.weight, self.ln2.bias, eps))
+            else:
+                o3 = K.attention_qkv_x3f(qkv, H, Dh, 1.0 / math.sqrt(Dh))
+                x, h3 = K.linear_residual_ln_x3(o3, self.proj.weight, self.proj.bias, x,
+                                                ln=(self.ln2.weight, self.ln2.bias, eps))
         else:
             qkv3 = K.linear_x3(h3, self.qkv.weight, self.qkv.bias, out_x3=True)
             o3 = K.attention_qkv_x3(qkv3, H, Dh, 1.0 / math.sqrt(Dh))
-        x, h3 = K.linear_residual_ln_x3(o3, self.proj.weight, self.proj.bias, x,
-                                        ln=(self.ln2.weight, self.ln2.bias, eps))
+            x, h3 = K.linear_residual_ln_x3(o3, self.proj.weight, self.proj.bias, x,
+                                            ln=(self.ln2.weight, self.ln2.bias, eps))
         f3 = K.linear_x3(h3, self.fc1.weight, self.fc1.bias, gelu=True, out_x3=True)
         nl = (next_ln.weight, next_ln.bias, next_ln.eps) if next_ln is not None else None
         return K.linear_residual_ln_x3(f3, self.fc2.weight, self.fc2.bias, x, residual2=mid, ln=nl)

@@ -96,7 +96,7 @@ TARGETS: Sequence[Target] = (
     Target("libnos_hbmlimit.so", ["hbm_limit.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"], libs=["dl"]),
     Target("libnos_barrier.so", ["rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
            libs=["rccl", "amdhip64"]),
-    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip"], "hipcc"),
+    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip", "attn_proj.hip"], "hipcc"),
     # the agent's commit-barrier helper as a native program: no interpreter start-up on the flip path
     Target("nos-gpuhelper", ["gpuhelper.cpp", "rccl_barrier.cpp", "p2p_barrier.hip"], "hipcc",
            libs=["rccl", "amdhip64"], executable=True),

@@ -277,6 +277,52 @@ def attention_qkv_x3f(qkv: torch.Tensor, heads: int, head_dim: int, scale: float
     return attention_x3f(qkv, out, heads, head_dim, scale, attention_x3_waves(cus, B, T, hb), head_block=hb)
 
 
+def attn_proj_fusable(heads: int, head_dim: int) -> bool:
+    """``NOS_ATTN_PROJ_FUSED=1``: the attention -> projection -> LayerNorm step as two launches
+    (attention partials, then csrc/attn_proj.hip's merge + projection + residual + LayerNorm) for the
+    384-wide model with fp32 QKV in. Off by default: measured slower than fixup + tuned GEMM +
+    LayerNorm (38 vs 29 us per layer on the whole GPU, ``profiles/attn_proj_fused_r3.json``) — a
+    workgroup that owns whole rows must stream the whole x3 weight (884 KB) per 32 rows through the
+    texture path, which is busy 80% of the kernel."""
+    return (os.environ.get("NOS_ATTN_PROJ_FUSED", "0") == "1" and head_dim == 64 and heads * head_dim == 384
+            and attention_input_f32())
+
+
+def attention_proj_ln_x3f(qkv: torch.Tensor, heads: int, head_dim: int, scale: float, w: torch.Tensor,
+                          b: torch.Tensor, residual: torch.Tensor, ln, waves: Optional[int] = None):
+    """``x = residual + attention(qkv) @ w^T + b`` and the x3 planes of ``LayerNorm(x)`` (``ln =
+    (weight, bias, eps)``): the x3 attention leaves its stream-K partials in the workspace and one
+    kernel merges them, projects, adds bias and residual and normalises (csrc/attn_proj.hip), instead
+    of the fixup, the projection GEMM and a LayerNorm kernel. Returns ``(x, planes)``."""
+    B, T, _ = qkv.shape
+    D = heads * head_dim
+    if not _use_hip(qkv):
+        o = attention_ref(qkv, heads, head_dim, scale)
+        x = (residual.double() + o.double() @ w.double().t() + b.double()).float()
+        return x, split3(F.layer_norm(x, (D,), ln[0], ln[1], ln[2]))
+    from .gemm import weight_planes
+    qkv = qkv.contiguous()
+    if waves is None:
+        waves = attention_x3_waves(slice_cus(), B, T, heads)
+    ws = torch.empty(waves * 2 * (64 * 32 + 64) * 8, dtype=torch.float32, device=qkv.device)
+    odirect = torch.empty(B, T, D, dtype=torch.float32, device=qkv.device)
+    L = _L()
+    _check(L.nos_attention_x3f_partials(qkv.data_ptr(), odirect.data_ptr(), ws.data_ptr(), B, T, heads, head_dim,
+                                        scale, waves, _stream()))
+    w3 = weight_planes(w)
+    res = residual.contiguous()
+    if res.shape != (B, T, D) and res.numel() != B * T * D:
+        raise ValueError("attention_proj_ln_x3f: residual must hold B*T*D elements")
+    x = torch.empty_like(res)
+    planes = torch.empty((3,) + tuple(res.shape), dtype=torch.bfloat16, device=qkv.device)
+    rc = L.nos_attn_merge_proj_ln(ws.data_ptr(), waves, odirect.data_ptr(), B, T, heads, w3.data_ptr(),
+                                  w3[0].numel(), b.data_ptr(), res.data_ptr(), ln[0].data_ptr(), ln[1].data_ptr(),
+                                  float(ln[2]), x.data_ptr(), planes.data_ptr(), _stream())
+    if rc != 0:
+        raise RuntimeError(f"nos kernel failed: {L.nos_attn_proj_last_error().decode()} (rc={rc})")
+    return x, planes
+
+
 def attention_qkv_x3(planes: torch.Tensor, heads: int, head_dim: int, scale: float) -> torch.Tensor:
     """x3 planes of packed QKV in, x3 planes ``[3, B, T, H*64]`` of the attention output out."""
     _, B, T, _ = planes.shape
@@ -328,6 +374,10 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                                                     i32, vp]
             L.nos_attention_x3f_sk_heads.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_x3f_partials.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attn_merge_proj_ln.argtypes = [vp, i32, vp, i32, i32, i32, vp, ctypes.c_size_t, vp, vp, vp, vp, f32,
+                                                 vp, vp, vp]
+            L.nos_attn_proj_last_error.restype = ctypes.c_char_p
             L.nos_attention_x3_set_flags.argtypes = [i32]
             L.nos_attention_x3_set_flags(int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))
             group = os.environ.get("NOS_ATTN_X3_GROUP")  # A/B switch for whole-model runs
