@@ -292,14 +292,16 @@ def weight_planes(w: torch.Tensor) -> torch.Tensor:
 
 def x3_eligible(N: int, Kd: int) -> list:
     """Tiles that can run this shape; ``NOS_X3_EXCLUDE`` (comma-separated kind prefixes, e.g.
-    ``m16,p``) and ``NOS_X3_MIN_TILE`` (minimum BM*BN) drop tiles from autotuning for A/B runs."""
+    ``m16,p``), ``NOS_X3_DROP`` (comma-separated tile ids) and ``NOS_X3_MIN_TILE`` (minimum BM*BN)
+    drop tiles from autotuning for A/B runs."""
     if Kd % 32:
         return []
     skip = tuple(x for x in os.environ.get("NOS_X3_EXCLUDE", "").split(",") if x)
+    drop = {int(x) for x in os.environ.get("NOS_X3_DROP", "").split(",") if x}
     min_area = int(os.environ.get("NOS_X3_MIN_TILE", "0"))
     return [c for c, (bm, bn, _, kind) in X3_TILES.items()
             if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))
-            and bm * bn >= min_area]
+            and bm * bn >= min_area and c not in drop]
 
 
 #: tiles at least this large (BM*BN) on a partition that shares the GPU with sibling partitions
