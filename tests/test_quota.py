@@ -233,3 +233,23 @@ def test_nos_scheduler_frees_a_whole_gpu_for_a_profile_no_node_offers():
     s.reconcile(NosScheduler.KEY)
     assert len(api.list("Pod", "team-a")) == 16 and not ko.pod_node_name(api.get("Pod", "a99", "team-a"))
     assert s.preempted == 8
+
+
+def test_preemptor_reclaim_timer_dropped_when_the_pod_leaves_the_queue():
+    # a preemptor deleted before it binds stops being timed (no unbounded growth of the timer map,
+    # no reclaim latency recorded for it)
+    from walkai_nos_amd.quota.scheduler import SCHEDULER_NAME, NosScheduler
+    api = InMemoryAPIServer()
+    api.create(_node("n1", {"pool": "a"}))
+    s = NosScheduler(api)
+    p = ko.new_pod("waiting", "default", requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME)
+    p["spec"]["nodeSelector"] = {"pool": "none"}
+    api.create(p)
+    s._preempted_for["default/waiting"] = 0.0
+    s._preempted_for["default/gone"] = 0.0
+    s.reconcile(NosScheduler.KEY)
+    assert "default/gone" not in s._preempted_for and not s.reclaim_latency_s
+    assert list(s._preempted_for) == ["default/waiting"]
+    api.delete("Pod", "waiting", "default")
+    s.reconcile(NosScheduler.KEY)
+    assert not s._preempted_for

@@ -310,6 +310,10 @@ class NosScheduler:
     def reconcile(self, req: Request) -> Result:
         pending = [p for p in self.client.list("Pod", field_selector="status.phase=Pending")
                    if p["spec"].get("schedulerName") == self.scheduler_name and not podutil.is_scheduled(p)]
+        # preemptors that left the queue without being bound (deleted, bound elsewhere) stop being timed
+        waiting = {_pkey(p) for p in pending}
+        for k in [k for k in self._preempted_for if k not in waiting]:
+            del self._preempted_for[k]
         if not pending:
             return Result()
         pending.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
