@@ -56,6 +56,9 @@ def main() -> int:
     ap.add_argument("--only", choices=("all", "attn", "gemm", "model", "modes"), default="all")
     ap.add_argument("--slices", default="spx,dpx,qpx,cpx")
     ap.add_argument("--partitions", type=int, default=0, help="modes: run only this many partitions of each mode")
+    ap.add_argument("--free-s", type=float, default=0.0,
+                    help="modes: serve free-running (one thread per pod, as the bench) for this many seconds "
+                         "instead of lock-step rounds")
     ap.add_argument("--lane-cus", type=int, default=0,
                     help="modes: serve partitions wider than this as request lanes of this many CUs (the bench's --lane-cus)")
     ap.add_argument("--emulation", default="spread", choices=("pinned", "spread", "landing"),
@@ -154,6 +157,7 @@ def modes_bench(a) -> int:
                       pin=slice_pin(prof, k, a.emulation), split=a.lane_cus > 0) for k in range(n)]
         for sl in slots:
             sl.warm()
+            sl.latency_ms.clear()
         torch.cuda.synchronize()
         work = 8 // n
         rounds = 6
@@ -161,17 +165,27 @@ def modes_bench(a) -> int:
         sampler = HwBusySampler(0, period=0.02)
         sampler.start()
         t0 = time.perf_counter()
-        for _ in range(rounds):
-            for sl in slots:
-                for _ in range(work):
-                    sl.submit()
-            for sl in slots:
-                sl.drain()
+        if a.free_s > 0:
+            # as the bench serves them: one thread per pod lane, each replaying its inference graph
+            # and waiting for it before the next (the reference demo's loop), free-running
+            done = free_running(slots, a.free_s)
+        else:
+            for _ in range(rounds):
+                for sl in slots:
+                    for _ in range(work):
+                        sl.submit()
+                for sl in slots:
+                    sl.drain()
+            done = rounds * work * n
         dt = time.perf_counter() - t0
         busy = sampler.stop()
+        lat = [x for sl in slots for x in sl.latency_ms]
         r = {"mode": prof, "emulation": a.emulation, "partitions": n, "lanes_per_partition": len(slots[0].lanes),
-             "inf_per_s_per_gpu": round(rounds * work * n / dt, 1),
-             "ms_per_round": round(1000 * dt / rounds, 2), "hw_busy_pct": busy, **sampler.power_summary()}
+             "serving": f"free-running threads, {a.free_s} s" if a.free_s > 0 else f"{rounds} lock-step rounds",
+             "inf_per_s_per_gpu": round(done / dt, 1),
+             "ms_per_round": round(1000 * dt / rounds, 2) if a.free_s <= 0 else None,
+             "latency_ms_mean": round(sum(lat) / len(lat), 3) if lat else None,
+             "hw_busy_pct": busy, **sampler.power_summary()}
         print(json.dumps(r), flush=True)
         results.append(r)
         for sl in slots:
@@ -181,6 +195,39 @@ def modes_bench(a) -> int:
     with open(a.out, "w") as f:
         json.dump(results, f, indent=1)
     return 0
+
+
+def free_running(slots, seconds: float) -> int:
+    """Every lane of every slot on its own thread: replay, wait, replay ... until the deadline
+    (``bench_core.NodeBench._serve_loops``); returns the inferences completed."""
+    import threading
+    deadline = time.perf_counter() + seconds
+    counts = []
+
+    def run(slot, lane):
+        K.set_slice_cus(lane.n_cus)
+        K.set_slice_pin(slot.pin)
+        done = 0
+        with torch.no_grad(), torch.cuda.stream(lane.stream):
+            while time.perf_counter() < deadline:
+                st = torch.cuda.Event(enable_timing=True)
+                st.record(lane.stream)
+                if lane.graph is not None:
+                    lane.graph.replay()
+                else:
+                    lane.out = slot.model(lane.x)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(lane.stream)
+                ev.synchronize()
+                slot.latency_ms.append(st.elapsed_time(ev))
+                done += 1
+        counts.append(done)
+    threads = [threading.Thread(target=run, args=(sl, lane), daemon=True) for sl in slots for lane in sl.lanes]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    return sum(counts)
 
 
 def model_bench(r, s, iters):
