@@ -372,3 +372,14 @@ def test_splitk_is_only_timed_on_slices_of_64_cus_or_more(monkeypatch):
     finally:
         K.set_slice_cus(None)
         G._fused_cache.clear()
+
+
+@pytest.mark.parametrize("gpus,load,seed", [(1, 1.3, 101), (3, 0.7, 102), (3, 1.3, 103), (8, 1.0, 104)])
+def test_control_plane_soak_no_admission_failures(gpus, load, seed):
+    # the whole control plane (pack planner, agents, partition plugin view, kubelet admission,
+    # kube-scheduler semantics) under over- and under-load on odd node sizes: no pod is ever bound
+    # to a partition kubelet then rejects, and the allocation figures stay physical
+    from walkai_nos_amd.bench_core import BenchConfig, control_only
+    r = control_only(BenchConfig(gpus=gpus, seed=seed, offered_load=load), 60)
+    assert r["admission_failures"] == 0
+    assert 0.0 < r["util_pct"] <= 100.0 and r["util_pct"] <= r["util_incl_outage_pct"] + 1e-9
