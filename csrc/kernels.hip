@@ -387,6 +387,17 @@ __global__ __launch_bounds__(64, 2) void attn_fwd_f32(const float* __restrict__ 
 // 4 MB L2 holds at most two heads' K/V (1.7 MB each at T=3401) instead of all of them.
 __device__ __forceinline__ long long sk_begin(long long w, long long U, long long P) { return w * U / P; }
 
+// floor(n / d) for 0 <= n < 2^23 through the f32 reciprocal rd = 1/d (within one of the quotient
+// there; one integer correction makes it exact): the stream-K bookkeeping of a segment as a few
+// vector instructions instead of 64-bit scalar divisions (~150 instructions each, before the
+// segment's first load can be addressed)
+__device__ __forceinline__ long long udiv23(long long n, long long d, float rd) {
+  int q = int(float(int(n)) * rd);
+  const int r = int(n) - q * int(d);
+  q += (r < 0) ? -1 : (r >= int(d) ? 1 : 0);
+  return q;
+}
+
 // any P: XCD x (= phys % 8) owns the contiguous logical run of its P/8 (+1 for the first P % 8
 // XCDs) workgroups — a bijection, so a grid trimmed to query-group boundaries (252 on 256 CUs)
 // keeps each XCD on about one head's K/V
@@ -1010,7 +1021,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_x3(const __bf16* __restrict__
 // G = query tiles (waves) per workgroup sharing each K/V block: 4 (two workgroups per CU) or 8 (one
 // 512-thread workgroup per CU: half the K/V bytes per query, the L2/Infinity-Cache traffic that
 // concurrent partitions share; the K and V loads are split between the two halves of the group).
-template <int G, bool QW = false, bool F32IN = false, bool PRIO = false>
+template <int G, bool QW = false, bool F32IN = false, bool PRIO = false, bool FDIV = false>
 __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __restrict__ qkv3, size_t plane,
                                                              float* __restrict__ out, __bf16* __restrict__ outp,
                                                              float* __restrict__ part_o, float* __restrict__ part_ml,
@@ -1027,8 +1038,11 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
   const int w = (Pk >> 30) ? pb.id : xcd_major_n(pb.id, P, pb.nx);
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
-  long long u = sk_begin(w, U, P);
-  const long long u1 = sk_begin(w + 1, U, P);
+  // FDIV (host-checked: every numerator < 2^23): reciprocal divisions for the bookkeeping
+  const float rP = FDIV ? 1.f / float(P) : 0.f, rNK = FDIV ? 1.f / float(NK) : 0.f;
+  const float rQG = FDIV ? 1.f / float(QG) : 0.f, rH = FDIV ? 1.f / float(H) : 0.f;
+  long long u = FDIV ? udiv23(w * U, P, rP) : sk_begin(w, U, P);
+  const long long u1 = FDIV ? udiv23((w + 1) * U, P, rP) : sk_begin(w + 1, U, P);
   const int D = Ht * HD, ld = 3 * D;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int j = lane & 31, hf = lane >> 5;
@@ -1039,13 +1053,15 @@ __global__ __launch_bounds__(64 * G, 8 / G) void attn_fwd_x3p(const __bf16* __re
   const int vtr = (4 * hf + (gi >> 2)) * XV_STR + 16 * (gg & 1) + 4 * (gi & 3);
   bool first = true;
   while (u < u1) {
-    const long long grp = u / NK;
+    const long long grp = FDIV ? udiv23(u, NK, rNK) : u / NK;
     const int kb0 = int(u - grp * NK);
     const int kb1 = int(min<long long>(NK, kb0 + (u1 - u)));
     const int nb = kb1 - kb0;
-    const int qg = int(grp % QG);
-    const int head = h0 + int((grp / QG) % H);
-    const int b = int(grp / ((long long)QG * H));
+    const long long gq = FDIV ? udiv23(grp, QG, rQG) : grp / QG;  // (b, head) of the group
+    const int qg = int(grp - gq * QG);
+    const long long bq = FDIV ? udiv23(gq, H, rH) : gq / H;
+    const int head = h0 + int(gq - bq * H);
+    const int b = int(bq);
     const __bf16* base = qkv3 + size_t(b) * T * ld;
     // F32IN: qkv arrives as fp32 [B][T][3D] (4 B per element instead of three 2-B planes) and is
     // split here — Q once per segment, each K/V chunk as it is stashed (the same RNE split the
@@ -1406,7 +1422,8 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
 
 static int g_x3_pipelined = 1;
 static int g_x3_flags = 0;  // A/B switches: bit 0 explicit vmcnt(0) after a segment's prologue (planes input),
-                            // bit 1 static s_setprio 1 for waves 4-7 (fp32 input)
+                            // bit 1 static s_setprio 1 for waves 4-7 (fp32 input), bit 3 64-bit
+                            // stream-K bookkeeping (no reciprocal divisions)
 
 int nos_attention_x3_set_flags(int f) {
   g_x3_flags = f;
@@ -1498,6 +1515,10 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   }
   const unsigned pin = g_pin;
   const int pk = waves | int(pin << 22) | ((g_x3_flags & 4) ? (1 << 30) : 0);
+  // reciprocal-division bookkeeping while every numerator (w * U <= (P + 1) * U) is < 2^23;
+  // flag bit 3 keeps the 64-bit form (A/B runs)
+  const long long Uk = (long long)B * hn * QG * NK;
+  const bool fdiv = !(g_x3_flags & 8) && (Uk + 1) * (waves + 1) < (1ll << 23);
   const dim3 grid(pinned_grid(waves, pin));
   if (!g_x3_pipelined)
     hipLaunchKernelGGL(attn_fwd_x3, dim3(waves), dim3(256), 0, s, q3, plane_stride, out, op, part_o, part_ml, B, T, H,
@@ -1505,6 +1526,9 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   else if (G == 8 && f32in && (g_x3_flags & 2))
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op,
                        part_o, part_ml, B, T, hn, h0, H, sl2, pk);
+  else if (G == 8 && f32in && fdiv)
+    hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, false, true>), grid, dim3(512), 0, s, q3, plane_stride, out,
+                       op, part_o, part_ml, B, T, hn, h0, H, sl2, pk);
   else if (G == 8 && f32in)
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op, part_o,
                        part_ml, B, T, hn, h0, H, sl2, pk);
