@@ -1,5 +1,6 @@
 """Numerics of the HIP workload kernels vs plain PyTorch fp32 references (GPU only)."""
 import math
+import os
 
 import pytest
 import torch
@@ -495,3 +496,26 @@ def test_attention_merge_proj_layernorm_fused(K, B, T, waves):
     torch.cuda.synchronize()
     assert (x - x2).abs().max().item() < 1e-4
     assert (h3.double().sum(0) - h2.double().sum(0)).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("B,T,waves", [(1, 3401, None), (1, 3401, 32), (2, 300, 7), (1, 77, 3)])
+def test_attention_reciprocal_bookkeeping_bit_identical(K, B, T, waves):
+    # the stream-K bookkeeping through f32-reciprocal divisions (default) and through 64-bit
+    # divisions (flag bit 3) must place every unit identically: the outputs are bit-identical
+    torch.manual_seed(13)
+    H, Dh = 6, 64
+    qkv = torch.randn(B, T, 3 * H * Dh, device="cuda")
+    w = waves or K.attention_x3_waves(K.slice_cus(), B, T, H)
+    outs = []
+    L = K._L()
+    try:
+        for flags in (0, 8):
+            L.nos_attention_x3_set_flags(flags)
+            out = torch.empty(3, B, T, H * Dh, dtype=torch.bfloat16, device="cuda")
+            outs.append(K.attention_x3f(qkv, out, H, Dh, 0.125, w).clone())
+        torch.cuda.synchronize()
+    finally:
+        L.nos_attention_x3_set_flags(int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))
+    assert torch.equal(outs[0], outs[1])
+    ref = _ref_attention(qkv, H, Dh, 0.125).double()
+    assert (outs[0].double().sum(0) - ref).abs().max().item() < 1e-5
