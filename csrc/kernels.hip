@@ -677,6 +677,8 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   __shared__ float s_tile[64][33];
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
+  const bool narrow_stores = (pin >> 8) & 1u;  // A/B: the earlier 2-byte plane stores
+  pin &= 0xffu;
   const PinnedBlock pb = pinned_block(pin);
   if (pb.id < 0) return;
   // grid-stride over the (group, query tile) units: a pinned launch runs a few workgroups per CU
@@ -739,9 +741,31 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 8; ++i) s_tile[(tid + 256 * i) >> 5][q] = acc[i] * inv;
   __syncthreads();
+  const size_t plane = size_t(B) * T * D;
+  if (!narrow_stores) {
+    // transposed store: thread -> (query row, 8 consecutive dims), one pass: each plane row of the
+    // tile leaves as 16-B stores (the fp32 output as two)
+    const int jq = tid >> 3, c8 = 8 * (tid & 7);
+    const int qq = qt * 32 + jq;
+    if (qq < T) {
+      const size_t i = (size_t(b) * T + qq) * D + head * HD + c8;
+      f32x8 v;
+#pragma unroll
+      for (int dd = 0; dd < 8; ++dd) v[dd] = s_tile[c8 + dd][jq];
+      if (outp) {
+        bf16x8 p0, p1, p2;
+        split3(v, p0, p1, p2);
+        *reinterpret_cast<bf16x8*>(outp + i) = p0;
+        *reinterpret_cast<bf16x8*>(outp + plane + i) = p1;
+        *reinterpret_cast<bf16x8*>(outp + 2 * plane + i) = p2;
+      } else {
+        *reinterpret_cast<f32x4*>(out + i) = f32x4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4*>(out + i + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+    }
+  } else {
   // transposed store: thread -> (query row, 64 dims), 4 rows per pass
   const int d = tid & 63;
-  const size_t plane = size_t(B) * T * D;
   for (int jq = tid >> 6; jq < 32; jq += 4) {
     const int qq = qt * 32 + jq;
     if (qq >= T) break;
@@ -750,6 +774,7 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
       store_x3(outp, plane, i, s_tile[d][jq]);
     else
       out[i] = s_tile[d][jq];
+  }
   }
   __syncthreads();  // s_tile is rewritten by the next unit
   }
@@ -1423,7 +1448,8 @@ int nos_split3_f32(const float* x, void* planes, size_t n, void* stream) {
 static int g_x3_pipelined = 1;
 static int g_x3_flags = 0;  // A/B switches: bit 0 explicit vmcnt(0) after a segment's prologue (planes input),
                             // bit 1 static s_setprio 1 for waves 4-7 (fp32 input), bit 3 64-bit
-                            // stream-K bookkeeping (no reciprocal divisions)
+                            // stream-K bookkeeping (no reciprocal divisions), bit 5 the fixup's
+                            // 2-byte plane stores
 
 int nos_attention_x3_set_flags(int f) {
   g_x3_flags = f;
@@ -1543,10 +1569,11 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
                        T, hn, h0, H, sl2, pk);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (!fixup) return 0;  // the partials are merged by the consumer (attn_proj.hip)
+  const unsigned fpin = pin | ((g_x3_flags & 32) ? 0x100u : 0u);  // bit 8: the earlier 2-byte stores (A/B)
   if (G == 8)
     hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(B * hn * QG * 8, pin)), dim3(256), 0, s,
                        part_o, part_ml,
-                       out, B, T, hn, waves, op, h0, H, pin);
+                       out, B, T, hn, waves, op, h0, H, fpin);
   else
     hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(pinned_grid(B * hn * QG * 4, pin)), dim3(256), 0, s,
                        part_o, part_ml,
