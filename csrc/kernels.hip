@@ -1577,7 +1577,7 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   else
     hipLaunchKernelGGL(attn_sk_lds_fixup<4>, dim3(pinned_grid(B * hn * QG * 4, pin)), dim3(256), 0, s,
                        part_o, part_ml,
-                       out, B, T, hn, waves, op, h0, H, pin);
+                       out, B, T, hn, waves, op, h0, H, fpin);
   return check_launch("attn_sk_lds_fixup");
 }
 

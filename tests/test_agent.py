@@ -149,6 +149,38 @@ def test_actuator_rolls_back_on_barrier_veto():
     assert e.smi.get_compute_partition(0) == "SPX"
 
 
+def test_plugin_registration_failure_after_a_commit_does_not_leave_the_journal():
+    """kubelet restarting during an apply (the plugin sync raising) must not escape
+    apply(): the flip is committed, the journal cleared and the commit recorded."""
+    e = Env()
+
+    class FailingHook:
+        def restart(self, node, timeout=60):
+            raise RuntimeError("unable to register amd.com/cpx_nps1 with kubelet")
+    e.actuator.device_plugin = FailingHook()
+    e.reporter.reconcile(Request("node-a"))
+    e.spec({"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8", api.ANNOTATION_PARTITIONING_PLAN: "7"})
+    e.actuator.reconcile(Request("node-a"))
+    assert e.smi.get_compute_partition(0) == "CPX" and e.shared.last_commit == "ok"
+    assert api.ANNOTATION_INFLIGHT_PLAN not in e.annotations()
+
+
+def test_barrier_that_cannot_start_is_a_veto_and_rolls_back():
+    """a commit barrier whose construction fails (native helper missing) after the
+    switch vetoes the plan: the GPU is flipped back and the journal cleared."""
+    e = Env()
+
+    def broken(n):
+        raise RuntimeError("native helper nos-gpuhelper is not built")
+    e.actuator.barrier_factory = broken
+    e.reporter.reconcile(Request("node-a"))
+    e.spec({"nos.nebuly.com/spec-gpu-0-cpx_nps1": "8"})
+    with pytest.raises(Exception):
+        e.actuator.reconcile(Request("node-a"))
+    assert e.smi.get_compute_partition(0) == "SPX" and e.shared.last_commit == "failed"
+    assert api.ANNOTATION_INFLIGHT_PLAN not in e.annotations()
+
+
 def test_actuator_never_flips_a_gpu_with_used_partitions():
     e = Env()
     e.smi.set_compute_partition(0, "CPX")

@@ -194,6 +194,39 @@ def test_partition_plugin_reports_a_vanished_gpu_unhealthy():
     assert [d.healthy for d in state.view()["amd.com/spx_nps1"]] == [True, True]
 
 
+def test_partition_plugin_survives_a_device_map_error():
+    """an amd-smi failure while building the view must not end ListAndWatch (kubelet
+    would drop the resource until the plugin registers again): the last known devices are listed
+    Unhealthy until the map reads again, and a pushed update carries it."""
+    smi = FakeAmdSmi(n_gpus=2)
+    broken = {"on": False}
+
+    def dmap():
+        if broken["on"]:
+            raise RuntimeError("amdsmi_init failed")
+        return smi.device_map()
+    state = PartitionState(dmap, lambda: {}, lambda: set())
+    assert [d.healthy for d in state.view()["amd.com/spx_nps1"]] == [True, True]
+    broken["on"] = True
+    v = state.view()
+    assert [d.healthy for d in v["amd.com/spx_nps1"]] == [False, False]
+    assert "device map unavailable" in v["amd.com/spx_nps1"][0].reason
+    with tempfile.TemporaryDirectory() as d:
+        reg = RegistrationServer(os.path.join(d, "kubelet.sock")).start()
+        mgr = partition_plugin_manager(state, socket_dir=d, kubelet_socket=reg.socket, register_backoff=0.01)
+        try:
+            mgr.sync()
+            law = _Law(mgr.plugins["amd.com/spx_nps1"].socket)
+            assert [h for _, h in law.next()] == [dp.UNHEALTHY, dp.UNHEALTHY]
+            broken["on"] = False
+            mgr.sync()                      # the same stream carries the recovery
+            assert [h for _, h in law.next()] == [dp.HEALTHY, dp.HEALTHY]
+            law.close()
+        finally:
+            mgr.stop()
+            reg.stop()
+
+
 def test_registration_retries_with_backoff_then_succeeds():
     from walkai_nos_amd.deviceplugin.server import SliceDevicePlugin
     from walkai_nos_amd.device.slicing_client import MemorySliceStore

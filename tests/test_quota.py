@@ -253,3 +253,58 @@ def test_preemptor_reclaim_timer_dropped_when_the_pod_leaves_the_queue():
     api.delete("Pod", "waiting", "default")
     s.reconcile(NosScheduler.KEY)
     assert not s._preempted_for
+
+
+class _GracefulAPI:
+    """An API server whose pod deletes are graceful: ``delete`` only sets
+    ``metadata.deletionTimestamp``; ``finish()`` removes the terminating pods (kubelet done)."""
+
+    def __init__(self, api):
+        self.api = api
+        self.deletes = 0
+
+    def __getattr__(self, k):
+        return getattr(self.api, k)
+
+    def delete(self, kind, name, namespace=None):
+        if kind != "Pod":
+            return self.api.delete(kind, name, namespace)
+        self.deletes += 1
+        self.api.patch("Pod", name, {"metadata": {"deletionTimestamp": "2026-01-01T00:01:00Z"}}, namespace)
+
+    def finish(self):
+        for p in self.api.list("Pod"):
+            if p["metadata"].get("deletionTimestamp"):
+                self.api.delete("Pod", ko.name(p), ko.namespace(p))
+
+
+def test_preemption_waits_for_terminating_victims():
+    """with graceful deletion, victims stay (terminating) for a while; a preemptor must
+    not evict more pods while its victims shut down, and no other preemptor may count them."""
+    from walkai_nos_amd.quota.scheduler import SCHEDULER_NAME, NosScheduler
+    mem = InMemoryAPIServer()
+    mem.create(_node("n0"))
+    mem.create(eq("qa", "team-a", {GM: 36}))
+    mem.create(eq("qb", "team-b", {GM: 7 * 36}))
+    for i in range(8):
+        p = ko.new_pod(f"a{i}", "team-a", requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME)
+        p["spec"]["nodeName"] = "n0"
+        p["status"]["phase"] = "Running"
+        p["metadata"]["creationTimestamp"] = f"2026-01-01T00:00:{i:02d}Z"
+        mem.create(p)
+    api = _GracefulAPI(mem)
+    s = NosScheduler(api)
+    for i in range(2):
+        mem.create(ko.new_pod(f"b{i}", "team-b", requests={"amd.com/cpx_nps1": 1}, scheduler_name=SCHEDULER_NAME))
+    s.reconcile(NosScheduler.KEY)
+    assert api.deletes == 2                                   # one victim per preemptor
+    terminating = {ko.name(p) for p in mem.list("Pod", "team-a") if p["metadata"].get("deletionTimestamp")}
+    assert len(terminating) == 2
+    for _ in range(3):                                        # victims still shutting down
+        s.reconcile(NosScheduler.KEY)
+    assert api.deletes == 2
+    assert not any(ko.pod_node_name(mem.get("Pod", f"b{i}", "team-b")) for i in range(2))
+    api.finish()
+    s.reconcile(NosScheduler.KEY)
+    assert all(ko.pod_node_name(mem.get("Pod", f"b{i}", "team-b")) == "n0" for i in range(2))
+    assert api.deletes == 2

@@ -83,7 +83,12 @@ def main(argv=None) -> int:
                            [Watch("Node", [ExcludeDelete(), MatchingName(node), AnnotationsChanged()])])
     else:
         dp = DevicePluginClient(client, cfg.devicePluginLabel, cfg.devicePluginNamespace or None)
-    from ..parallel.spawned import HelperRegistry
+    from ..parallel.spawned import HelperRegistry, native_helper
+    if cfg.commitBarrier == "xgmi" and native_helper() is None:
+        # fail before the first flip, not after it: a barrier that cannot start is a veto, and a
+        # node whose every commit is vetoed rolls every flip back
+        log.error("commitBarrier xgmi needs the native nos-gpuhelper (make native); not found")
+        return 1
     helpers = HelperRegistry()
     bf = node_barrier_factory(helpers, cfg.commitBarrier) if cfg.commitBarrier != "none" else None
     probe = None

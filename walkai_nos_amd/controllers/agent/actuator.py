@@ -228,7 +228,14 @@ class Actuator:
         self.last_votes = votes
         if self.barrier_factory is None:
             return all(votes)
-        barrier = self.barrier_factory(max(1, len(votes)))
+        try:
+            # the GPUs are already switched: a barrier that cannot even be built (the native helper
+            # missing, a spawn failure) is a veto, so the rollback below runs
+            barrier = self.barrier_factory(max(1, len(votes)))
+        except Exception as e:  # noqa: BLE001
+            log.error("commit barrier unavailable (%s): vetoing the plan", e)
+            REGISTRY.apply_errors.labels(node=self.node_name, op="barrier_unavailable").inc()
+            return False
         participants = getattr(barrier, "set_participants", None)
         if participants is not None and self._vote_devices:
             participants(self._vote_devices)
@@ -314,7 +321,7 @@ class Actuator:
             return
         try:
             self.device_plugin.restart(self.node_name)
-        except GpuError as e:
+        except Exception as e:  # noqa: BLE001 - the change is committed; the plugin's own sync retries
             log.error("unable to re-register the device plugin: %s", e)
 
     # -- journal ------------------------------------------------------------------------------

@@ -153,7 +153,18 @@ class PartitionState:
             log.warning("kubelet allocations unavailable: %s", e)
             used = set()
         withheld = reconfiguring_gpus(anns)
-        m = self._map()
+        try:
+            m = self._map()
+        except Exception as e:  # noqa: BLE001 - a ListAndWatch stream must not end on a map error
+            # amd-smi failing (driver reload, a GPU falling off the bus): keep listing the last
+            # known devices, all Unhealthy, until the map is readable again
+            log.warning("device map unavailable (%s): last known devices reported unhealthy", e)
+            out: Dict[str, List[PartitionDevice]] = defaultdict(list)
+            for d in list(self._last.values()) + [d for i, d in self._lost.items() if i not in self._last]:
+                out[d.resource].append(PartitionDevice(d.id, d.resource, d.gpu_index, d.partition_index,
+                                                       d.render_minor, False, f"device map unavailable: {e}"[:120],
+                                                       d.bdf))
+            return {r: sorted(v, key=lambda x: (x.gpu_index, x.partition_index, x.id)) for r, v in out.items()}
         bdfs = {g.bdf.lower() for g in m.gpus}
         for d in self._last.values():
             if d.bdf not in bdfs:
@@ -276,8 +287,13 @@ class PartitionPluginHook:
         self.publisher = publisher
 
     def restart(self, node: str = "", timeout: float = 60.0) -> None:
+        """Never raises: it runs after a flip has committed, and a kubelet that is restarting (its
+        registration failing) must not keep the actuator from clearing its journal; one
+        registration attempt here, the periodic sync (``run_forever``) retries."""
         try:
-            self.manager.sync()
+            self.manager.sync(attempts=1)
+        except Exception as e:  # noqa: BLE001 - retried by the periodic sync
+            log.warning("device plugin sync after the change failed (retried by the periodic sync): %s", e)
         finally:
             if self.publisher is not None:
                 self.publisher.publish(self.state.view())

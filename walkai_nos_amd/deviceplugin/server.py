@@ -377,7 +377,9 @@ class PluginManager:
         return SliceDevicePlugin(r, self.store, self.render, self.cu_count, self.shim_path, self.socket_dir,
                                  device_map=self.device_map)
 
-    def sync(self) -> None:
+    def sync(self, attempts: Optional[int] = None) -> None:
+        """``attempts``: registration attempts per plugin this call (default: the manager's); the
+        agents' flip path passes 1 and leaves further retries to the periodic sync."""
         with self._lock:
             for r in self._resources():
                 if r not in self.plugins:
@@ -392,7 +394,8 @@ class PluginManager:
                     if p.registered_inode is not None and kubelet is not None and p.registered_inode != kubelet:
                         log.info("kubelet restarted (new %s): re-registering %s", self.kubelet_socket, r)
                     try:
-                        p.register(self.kubelet_socket, attempts=self.register_attempts,
+                        p.register(self.kubelet_socket,
+                                   attempts=self.register_attempts if attempts is None else attempts,
                                    backoff=self.register_backoff)
                     except RuntimeError as e:
                         p.registered_inode = None  # retried on the next sync
@@ -403,8 +406,9 @@ class PluginManager:
                 raise RuntimeError("; ".join(errors))
 
     def restart(self, node_name: str = "", timeout: float = 60.0) -> None:
-        """The agents' device-plugin hook after a change: no pod restart, just a pushed update."""
-        self.sync()
+        """The agents' device-plugin hook after a change: no pod restart, just a pushed update (one
+        registration attempt; a kubelet that is restarting is retried by :func:`run_forever`)."""
+        self.sync(attempts=1)
 
     def stop(self) -> None:
         with self._lock:

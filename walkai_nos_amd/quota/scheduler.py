@@ -133,7 +133,9 @@ class CapacityScheduling:
         labels = self._labels(state)
         cands = []
         for v in state.node_pods.get(node, []):
-            if not podutil.is_running(v):
+            # a terminating pod already frees its capacity for whoever evicted it: counting it
+            # again would let a second preemptor claim capacity the first one paid for
+            if not podutil.is_running(v) or podutil.is_terminating(v):
                 continue
             qb = state.quotas.for_namespace(ko.namespace(v))
             if qb is None:
@@ -209,6 +211,8 @@ class CapacityScheduling:
         for g, keys in pods_by_gpu.items():
             gi = int(g)
             live = [on_node[k] for k in keys if k in on_node]   # pods already gone need no eviction
+            if any(podutil.is_terminating(v) for v in live):
+                continue   # being freed already (for another preemptor, or shutting down)
             if gi in serving or not live or not self._evictable_together(state, pod, live):
                 continue
             rank = (0 if gi in draining else 1, len(live), gi)
@@ -260,6 +264,7 @@ class NosScheduler:
         self.bound = 0
         self.preempted = 0
         self._preempted_for: Dict[str, float] = {}  # preemptor -> when its first victims were evicted
+        self._victims_of: Dict[str, set] = {}       # preemptor -> keys of the pods it evicted
         self.reclaim_latency_s: List[float] = []    # preemption -> preemptor bound
 
     KEY = Request("nos-scheduler-cycle")
@@ -314,6 +319,8 @@ class NosScheduler:
         waiting = {_pkey(p) for p in pending}
         for k in [k for k in self._preempted_for if k not in waiting]:
             del self._preempted_for[k]
+        for k in [k for k in self._victims_of if k not in waiting]:
+            del self._victims_of[k]
         if not pending:
             return Result()
         pending.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
@@ -331,6 +338,12 @@ class NosScheduler:
             allowed, reasons = feasible_nodes(pod, list(state.nodes.values()))
             allowed_names = {ko.name(n) for n in allowed}
             feasible = [n for n, free in state.node_free.items() if n in allowed_names and self.fits(req_, free)]
+            if not feasible and self._victims_terminating(state, pod):
+                # its victims are still shutting down (graceful deletion): wait for them instead of
+                # preempting again (kube-scheduler's PodEligibleToPreemptOthers)
+                self.plugin.hold(state, pod)
+                retry = True
+                continue
             if not feasible:
                 preempted = bool(allowed_names) and (self._preempt(state, pod, allowed_names) or
                                                      self._preempt_gpu(state, pod, allowed_names))
@@ -405,9 +418,16 @@ class NosScheduler:
             pass
         return True
 
+    def _victims_terminating(self, state: CycleState, pod: Dict[str, Any]) -> bool:
+        mine = self._victims_of.get(_pkey(pod))
+        if not mine:
+            return False
+        return any(_pkey(v) in mine and podutil.is_terminating(v) for ps in state.node_pods.values() for v in ps)
+
     def _evict(self, state: CycleState, pod: Dict[str, Any], node: str, victims: List[Dict[str, Any]]) -> None:
         self._preempted_for.setdefault(_pkey(pod), self.clock())
         gone = {_pkey(v) for v in victims}
+        self._victims_of.setdefault(_pkey(pod), set()).update(gone)
         for v in victims:
             try:
                 self.client.delete("Pod", ko.name(v), ko.namespace(v))

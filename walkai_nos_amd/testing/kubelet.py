@@ -35,7 +35,7 @@ class FakeKubelet:
         self.node = node
         self.reg = RegistrationServer(os.path.join(self.dir, "kubelet.sock")).start()
         self.devices: Dict[str, List[Tuple[str, str]]] = {}      # resource -> [(id, health)]
-        self.readers: Dict[str, Tuple[str, threading.Thread]] = {}
+        self.readers: Dict[str, Tuple[int, threading.Thread]] = {}  # resource -> (registration #, reader)
         self.used: Dict[Tuple[str, str], Tuple[str, str]] = {}   # (ns, pod) -> (resource, id)
         self.admission_failures: List[Tuple[Tuple[str, str], str]] = []
         self.allocations: Dict[Tuple[str, str], List[str]] = {}  # (ns, pod) -> host device paths
@@ -73,17 +73,25 @@ class FakeKubelet:
                 self.devices.pop(resource, None)
 
     def sync(self) -> None:
-        """(Re)open a ListAndWatch stream for every registered resource whose stream is gone, and
-        publish the node's allocatable (healthy devices) and capacity (all devices), as kubelet's
-        node-status sync does."""
-        latest = {r.resource_name: r.endpoint for r in self.reg.registered}
-        for res, ep in latest.items():
+        """Open a ListAndWatch stream for every *new registration* (a resource registered for the
+        first time, or registered again), and publish the node's allocatable (healthy devices) and
+        capacity (all devices), as kubelet's node-status sync does.  A stream that ended is not
+        reopened on its own: kubelet drops the endpoint and waits for the plugin to register
+        again, so a plugin whose stream dies must notice and re-register."""
+        latest: Dict[str, Tuple[int, str]] = {}
+        for k, r in enumerate(self.reg.registered):
+            latest[r.resource_name] = (k, r.endpoint)
+        for res, (k, ep) in latest.items():
             cur = self.readers.get(res)
-            if cur is None or cur[0] != ep or not cur[1].is_alive():
+            if cur is None or cur[0] != k:
                 t = threading.Thread(target=self._read, args=(res, ep), daemon=True, name=f"law-{res}")
                 t.start()
-                self.readers[res] = (ep, t)
+                self.readers[res] = (k, t)
         self._publish()
+
+    def endpoint(self, resource: str) -> str:
+        k, _ = self.readers[resource]
+        return self.reg.registered[k].endpoint
 
     def _publish(self) -> None:
         with self.lock:
@@ -123,7 +131,7 @@ class FakeKubelet:
         try:
             if not free:
                 raise RuntimeError(f"no healthy {res} device")
-            ch = grpc.insecure_channel("unix://" + os.path.join(self.dir, self.readers[res][0]))
+            ch = grpc.insecure_channel("unix://" + os.path.join(self.dir, self.endpoint(res)))
             req = dp.AllocateRequest()
             req.container_requests.add(devicesIDs=[free[0]])
             try:

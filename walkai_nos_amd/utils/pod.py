@@ -18,6 +18,11 @@ def is_terminated(pod: Obj) -> bool:
     return pod.get("status", {}).get("phase") in ("Succeeded", "Failed")
 
 
+def is_terminating(pod: Obj) -> bool:
+    """Deleted with a grace period and not gone yet (``metadata.deletionTimestamp`` set)."""
+    return bool(pod.get("metadata", {}).get("deletionTimestamp"))
+
+
 def is_scheduled(pod: Obj) -> bool:
     return bool(pod.get("spec", {}).get("nodeName"))
 
