@@ -51,21 +51,32 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default="gpurun_out/multiproc.json")
+    ap.add_argument("--env", default="{}", help="extra env for every pod, JSON (e.g. {\"NOS_POD_STREAMS\": \"4\"})")
+    ap.add_argument("--tag", default="", help="suffix of the scenario names in the output")
     args = ap.parse_args()
+    extra = json.loads(args.env)
     todo = scenarios()
     if args.only:
         todo = {k: v for k, v in todo.items() if k in args.only.split(",")}
     res = {"seconds": args.seconds, "reference_inf_per_s_a100": REFERENCE, "scenarios": {}}
+    if os.path.exists(args.out):  # several variants (--env/--tag) accumulate in one file
+        with open(args.out) as f:
+            res["scenarios"] = json.load(f).get("scenarios", {})
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     for name, (profiles, shim) in todo.items():
         t0 = time.time()
         dedicated = all("cu." in p for p in profiles)
-        r = run_pods(profiles, seconds=args.seconds, shim=shim, census=dedicated)
+        r = run_pods(profiles, seconds=args.seconds, shim=shim, census=dedicated, extra_env=extra)
         r["profiles"] = profiles
         r["shim"] = shim
+        r["env"] = extra
         r["wall_s"] = round(time.time() - t0, 1)
+        rates = [p["inf_per_s"] for p in r["per_pod"]]
+        r["per_pod_max_over_min"] = round(max(rates) / max(1e-9, min(rates)), 3) if rates else None
+        name = name + args.tag
         res["scenarios"][name] = r
         print(json.dumps({"scenario": name, "pods": r["pods"], "agg_inf_per_s": r["aggregate_inf_per_s"],
+                          "per_pod": rates, "max_over_min": r["per_pod_max_over_min"],
                           "mean_latency_ms": r["mean_latency_ms"],
                           "census_pairs_overlapping": r.get("census_pairs_overlapping"), "wall_s": r["wall_s"]}),
               flush=True)

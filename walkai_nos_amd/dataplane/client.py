@@ -58,6 +58,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--census", action="store_true")
     ap.add_argument("--hw", default="800,1066")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("NOS_POD_STREAMS", "1")),
+                    help="HIP streams the inference loop rotates over (one inference at a time)")
     args = ap.parse_args(argv)
     t_boot = time.perf_counter()
     import torch
@@ -69,7 +71,8 @@ def main(argv=None) -> int:
     dev = "cuda:0"
     model = YolosSmall().to(dev).eval()
     x = demo_input(1, hw, dev, seed=int(os.environ.get("NOS_POD_SEED", "0")))
-    stream = torch.cuda.Stream()
+    streams = [torch.cuda.Stream() for _ in range(max(1, args.streams))]
+    stream = streams[0]
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(2):
             model(x)
@@ -82,7 +85,8 @@ def main(argv=None) -> int:
         stream.synchronize()
     out: Dict[str, Any] = {"pid": os.getpid(), "slice_ids": os.environ.get("NOS_SLICE_IDS", ""),
                            "hsa_cu_mask": os.environ.get("HSA_CU_MASK", ""), "slice_cus": K.slice_cus(),
-                           "boot_s": round(time.perf_counter() - t_boot, 2)}
+                           "boot_s": round(time.perf_counter() - t_boot, 2), "streams": len(streams),
+                           "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "")}
     print("READY", flush=True)
     line = sys.stdin.readline().split()
     if not line or line[0] != "GO":
@@ -94,7 +98,8 @@ def main(argv=None) -> int:
     lat: List[float] = []
     census_at = start + 0.25 * args.seconds if args.census else None
     census = None
-    with torch.no_grad(), torch.cuda.stream(stream):
+    k = 0
+    with torch.no_grad():
         while True:
             now = time.time()
             if now >= end:
@@ -102,12 +107,15 @@ def main(argv=None) -> int:
             if census_at is not None and now >= census_at:
                 census = _census()  # every other pod is mid-loop now
                 census_at = None
+            s = streams[k % len(streams)]  # one inference at a time, rotated over the process's queues
+            k += 1
             t0 = time.perf_counter()
-            if graph is not None:
-                graph.replay()
-            else:
-                model(x)
-            stream.synchronize()
+            with torch.cuda.stream(s):
+                if graph is not None:
+                    graph.replay()
+                else:
+                    model(x)
+            s.synchronize()
             lat.append(1e3 * (time.perf_counter() - t0))
     out["window_s"] = round(time.time() - start, 3)
     out["inferences"] = len(lat)
