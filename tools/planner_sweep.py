@@ -20,11 +20,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(job):
-    gpus, load, seed, steps, pack = job
+    gpus, load, seed, steps, pack, layout = job
     import logging
     logging.disable(logging.CRITICAL)
     from walkai_nos_amd.bench_core import BenchConfig, control_only
-    r = control_only(BenchConfig(gpus=gpus, offered_load=load, seed=seed, pack=pack or None), steps)
+    r = control_only(BenchConfig(gpus=gpus, offered_load=load, seed=seed, pack=pack or None, layout=layout), steps)
     pp = r["per_profile"]
     return {"gpus": gpus, "load": load, "seed": seed, "util_pct": r["util_pct"], "flips": r["flips"],
             "time_in_flip_pct": r["time_in_flip_pct"], "pending_mean": r["pending_mean"],
@@ -41,11 +41,12 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--pack", default="{}", help="PackParams overrides as JSON")
     ap.add_argument("--workers", type=int, default=6)
+    ap.add_argument("--layout", default="partitions", help="xcp-layout of the node: partitions | slices | auto")
     ap.add_argument("--out", default="profiles/planner_sweep_r3.json")
     a = ap.parse_args()
     pack = json.loads(a.pack)
     jobs = list(itertools.product([int(g) for g in a.gpus.split(",")], [float(x) for x in a.loads.split(",")],
-                                  [int(s) for s in a.seeds.split(",")], [a.steps], [pack]))
+                                  [int(s) for s in a.seeds.split(",")], [a.steps], [pack], [a.layout]))
     with mp.Pool(a.workers) as pool:
         rows = pool.map(run, jobs)
     cells = {}
@@ -61,7 +62,7 @@ def main() -> int:
             "pending_mean": round(sum(r["pending_mean"] for r in grp) / len(grp), 2),
             "tts_p99_lifetimes_worst_seed": tts}
         print(f"{g}gpu/load{l}", json.dumps(cells[f"{g}gpu/load{l}"]), flush=True)
-    out = {"steps": a.steps, "seeds": a.seeds, "pack_overrides": pack, "cells": cells, "rows": rows}
+    out = {"steps": a.steps, "seeds": a.seeds, "pack_overrides": pack, "layout": a.layout, "cells": cells, "rows": rows}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)

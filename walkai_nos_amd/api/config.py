@@ -73,18 +73,21 @@ class GpuPartitionerConfig(ManagerConfig):
     scoring: str = "fraction"
     #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
     #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds,
-    #: reserveBreakFill, minStintSeconds, unservedAfterSeconds
+    #: reserveBreakFill, minStintSeconds, unservedAfterSeconds; sliced GPUs (xcp-layout slices /
+    #: auto): sliceReserveAfterSeconds, sliceFill
     packing: Dict[str, Any] = field(default_factory=dict)
 
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
                     "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
                     "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after", "minStintSeconds": "min_stint",
                     "unservedAfterSeconds": "unserved_after", "replanEverySeconds": "replan_every",
-                    "reserveBreakFill": "reserve_break_fill"}
+                    "reserveBreakFill": "reserve_break_fill", "sliceReserveAfterSeconds": "slice_reserve_after",
+                    "sliceFill": "slice_fill"}
+    BOOL_PACKING_KEYS = ("spxReserve", "sliceFill")
 
     def pack_params(self) -> Any:
         from ..controllers.partitioner.pod_controller import PackParams
-        return PackParams(**{self.PACKING_KEYS[k]: (bool(v) if k == "spxReserve" else float(v))
+        return PackParams(**{self.PACKING_KEYS[k]: (bool(v) if k in self.BOOL_PACKING_KEYS else float(v))
                              for k, v in self.packing.items()})
 
     def validate(self) -> None:
@@ -93,7 +96,7 @@ class GpuPartitionerConfig(ManagerConfig):
         if unknown:
             raise ValueError(f"packing: unknown keys {sorted(unknown)}")
         for k, v in self.packing.items():
-            if k != "spxReserve" and (not isinstance(v, (int, float)) or v < 0):
+            if k not in self.BOOL_PACKING_KEYS and (not isinstance(v, (int, float)) or v < 0):
                 raise ValueError(f"packing.{k} must be a non-negative number")
         if self.batchWindowTimeoutSeconds <= 0:
             raise ValueError("batchWindowTimeoutSeconds must be greater than 0")
@@ -142,6 +145,10 @@ class MigAgentConfig(AgentConfig):
     partitioner drains keeps receiving pods on its free partitions)."""
     devicePlugin: str = "nos"
     publishAllocatable: bool = True         # patch node status.allocatable right after each plugin sync
+    # CU-mask slice layout of the node's sliced GPUs (xcp-layout slices/auto): a host path, so an
+    # agent restart keeps serving the slices pods run on
+    sliceStateFile: str = "/var/lib/nos/xcp-slices.json"
+    hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
 
     def validate(self) -> None:
         super().validate()

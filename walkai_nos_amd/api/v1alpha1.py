@@ -21,6 +21,10 @@ API_VERSION = f"{GROUP}/{VERSION}"
 # -- labels (reference labels.go:21) --------------------------------------------------
 LABEL_GPU_PARTITIONING = "nos.nebuly.com/gpu-partitioning"
 LABEL_CAPACITY_INFO = "nos.nebuly.com/capacity"
+# MI355X: how an xcp node's GPUs may be laid out — "partitions" (hardware compute partitions only,
+# the default), "slices" (every GPU in SPX carved into CU-mask slices of the partition sizes: mixed
+# geometries, re-carved without a drain), "auto" (the planner chooses per GPU); models/xcp/slices.py
+LABEL_XCP_LAYOUT = "nos.nebuly.com/xcp-layout"
 CAPACITY_IN_QUOTA = "in-quota"
 CAPACITY_OVER_QUOTA = "over-quota"
 
@@ -35,6 +39,10 @@ ANNOTATION_REPORTED_PARTITIONING_PLAN = "nos.nebuly.com/status-partitioning-plan
 # MI355X: node-wide memory partition mode (NPS1/NPS2/NPS4/NPS8)
 ANNOTATION_MEMORY_PARTITION_SPEC = "nos.nebuly.com/spec-memory-partition"
 ANNOTATION_MEMORY_PARTITION_STATUS = "nos.nebuly.com/status-memory-partition"
+# MI355X: GPUs served as CU-mask slices (comma-separated indexes): the ones the plan wants sliced
+# (written with the spec by the partitioner) and the ones the agent serves sliced (status)
+ANNOTATION_SLICED_GPUS_SPEC = "nos.nebuly.com/spec-sliced-gpus"
+ANNOTATION_SLICED_GPUS_STATUS = "nos.nebuly.com/status-sliced-gpus"
 # MI355X: outcome of the node-atomic commit barrier for the last plan ("ok" / "failed:<reason>")
 ANNOTATION_COMMIT_STATUS = "nos.nebuly.com/status-partitioning-commit"
 # MI355X: write-ahead journal of the plan the agent is applying (JSON {plan, from, to}); written

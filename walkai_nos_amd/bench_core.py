@@ -57,6 +57,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from .kube import objects as ko
 from .models.xcp.profile import COMPUTE_MODES, extract_profile_name
+from .models.xcp.slices import slice_groups
 
 # reference numbers: 1x A100-80GB PCIe, 7 pods, MPS 10 GB slices
 BASELINE_INFER_PER_S_PER_GPU = 21.89
@@ -146,6 +147,7 @@ class BenchConfig:
     device_plugin: str = "nos"           # nos (drain enforced by device health) | amd (no drain enforcement)
     pack: Optional[Dict[str, float]] = None  # PackParams overrides (field name -> value)
     arrivals: str = "steady"             # steady (constant rate, seeded phase) | poisson
+    layout: str = "partitions"           # node label nos.nebuly.com/xcp-layout: partitions | slices | auto
 
     def __post_init__(self) -> None:
         if self.flip_cost_s < 0:
@@ -437,6 +439,9 @@ class DataPlane:
         A different set of compute modes than in the last quantum means the GPU was re-partitioned:
         every queued inference of the old layout finishes first (the agent only flips an idle GPU),
         so slots of two layouts never overlap."""
+        missing = {k: [32 * g + i for g in k[2] for i in range(32)] for k in keys if k not in self.slots}
+        if missing:
+            self.add_slots(missing)  # an unaligned CU-mask slice: its own replica (warmed in the window)
         layout = frozenset(k[0] for k in keys)
         if layout != self._layout:
             if any(s.in_flight for s in self.slots.values()):
@@ -582,7 +587,8 @@ class NodeBench:
         self.cfg = cfg
         from .controllers.partitioner.pod_controller import PackParams
         self.cluster = SimCluster(n_nodes=cfg.nodes, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy,
-                                  device_plugin=cfg.device_plugin, pack=PackParams(**(cfg.pack or {})))
+                                  device_plugin=cfg.device_plugin, pack=PackParams(**(cfg.pack or {})),
+                                  xcp_layout=cfg.layout)
         self.sn = next(iter(self.cluster.nodes.values()))  # the node this rank's data plane serves
         if barrier_factory is not None or verify is not None:
             self._set_commit(barrier_factory, verify)
@@ -690,17 +696,32 @@ class NodeBench:
             if self.outage[g] <= 1e-9:
                 del self.outage[g]
 
-    def my_pods(self) -> List[Tuple[str, int]]:
-        """(profile, partition index) of the pods served on this rank's GPU this quantum."""
-        out = []
+    def my_pods(self) -> List[Tuple[Any, ...]]:
+        """Data-plane keys of the pods served on this rank's GPU this quantum: (profile, partition
+        index) of a partition, and of a CU-mask slice whose row groups are that partition's CU set
+        (slices are placed buddy-aligned, so they usually are); ("slice", profile, groups) of any
+        other slice."""
+        out: List[Tuple[Any, ...]] = []
+        slices = {s.id: s for ss in (self.sn.xcp_slices.load() if self.sn.xcp_slices is not None else {}).values()
+                  for s in ss}
         for devs in self.sn.kubelet.allocations.values():
             for r, dev_id in devs:
                 prof = extract_profile_name(r)
                 if prof is None:
                     continue
                 d = self.sn.smi.resolve(dev_id)
-                if d.gpu_index == self.cfg.rank:
+                if d.gpu_index != self.cfg.rank:
+                    continue
+                s = slices.get(dev_id)
+                if s is None:
                     out.append((prof, d.partition_index))
+                    continue
+                groups = slice_groups(s)
+                n = len(groups)
+                if groups == list(range(groups[0], groups[0] + n)) and groups[0] % n == 0:
+                    out.append((prof, groups[0] // n))
+                else:
+                    out.append(("slice", prof, tuple(groups)))
         return out
 
     def step(self, deadline: Optional[float] = None) -> int:
@@ -728,7 +749,7 @@ class NodeBench:
         total = sum(n.values())
         self.inferences += total
         for k, v in n.items():
-            self.profile_inferences[str(k[0])] += v
+            self.profile_inferences[str(k[1] if k[0] == "slice" else k[0])] += v
         self.end_step()
         return total
 
@@ -843,7 +864,8 @@ def inference_latency(data: Optional[DataPlane]) -> Dict[str, Dict[str, float]]:
         return out
     by_mode: Dict[str, List[float]] = collections.defaultdict(list)
     for key, s in data.slots.items():
-        by_mode[str(key[0]).split("_")[0]] += s.latency_ms
+        prof = key[1] if key[0] == "slice" else key[0]
+        by_mode[str(prof).split("_")[0]] += s.latency_ms
     for mode, v in sorted(by_mode.items()):
         if v:
             v = sorted(v)
@@ -1035,16 +1057,23 @@ def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
         return {"error": str(e)[:200]}
 
 
+#: inferences/s per GPU with every partition of the mode busy, one serving thread per pod — the
+#: final round-3 tree (``profiles/kbench_r3_modes_final.json``, free-running): a CU-mask slice runs
+#: the same kernels on the same CU set as the emulated partition of its size, so slices are priced
+#: with the rate of that mode per partition
+MODE_RATES = {"spx": 359.9, "dpx": 415.9, "qpx": 433.0, "cpx": 404.2}
+
+
 def control_only(cfg: BenchConfig, steps: int, skip: int = 0) -> Dict[str, Any]:
     """The control plane + outage model alone (no GPU): allocation, flips, queue and per-profile
     time-to-schedule over ``steps`` quanta after the preroll (the first ``skip`` of them are warm-up,
     not counted).  ``inf_per_s_model`` prices the served partition-quanta with the measured
-    one-loop-per-pod mode rates (``profiles/kbench_r2_modes_tiles256.json``)."""
+    one-loop-per-pod mode rates (:data:`MODE_RATES`)."""
     nb = NodeBench(cfg, gpu_data_plane=False)
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
-    rate = {"spx": 358.2, "dpx": 429.3, "qpx": 440.4, "cpx": 376.2}
+    rate = MODE_RATES
     served = 0.0
     for i in range(steps):
         if i == skip:

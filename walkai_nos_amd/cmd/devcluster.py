@@ -44,10 +44,14 @@ RUNTIME_ANNOTATION = "nos.nebuly.com/dev-runtime-seconds"
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def node_labels(gpus: int, model: str = "MI355X", kind: str = api.PARTITIONING_KIND_XCP) -> Dict[str, str]:
-    return {api.LABEL_GPU_PARTITIONING: kind,
-            constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}", constant.LABEL_AMD_GPU_COUNT: str(gpus),
-            constant.LABEL_AMD_GPU_VRAM: "288G", constant.LABEL_AMD_GPU_CU_COUNT: "256"}
+def node_labels(gpus: int, model: str = "MI355X", kind: str = api.PARTITIONING_KIND_XCP,
+                layout: str = "partitions") -> Dict[str, str]:
+    out = {api.LABEL_GPU_PARTITIONING: kind,
+           constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}", constant.LABEL_AMD_GPU_COUNT: str(gpus),
+           constant.LABEL_AMD_GPU_VRAM: "288G", constant.LABEL_AMD_GPU_CU_COUNT: "256"}
+    if kind == api.PARTITIONING_KIND_XCP and layout != "partitions":
+        out[api.LABEL_XCP_LAYOUT] = layout
+    return out
 
 
 def fast_partitioner_config(**packing: float) -> GpuPartitionerConfig:
@@ -62,7 +66,7 @@ class DevCluster:
     def __init__(self, root: str, nodes: int = 1, gpus: int = 1,
                  partitioner: Optional[GpuPartitionerConfig] = None, report_interval: float = 1.0,
                  bookmark_every: float = 5.0, amd_smi_backend: str = "fake", quota: bool = False,
-                 kind: str = api.PARTITIONING_KIND_XCP):
+                 kind: str = api.PARTITIONING_KIND_XCP, layout: str = "partitions"):
         self.root = root
         self.n_nodes, self.gpus = nodes, gpus
         self.partitioner_cfg = partitioner or fast_partitioner_config()
@@ -70,6 +74,7 @@ class DevCluster:
         self.amd_smi_backend = amd_smi_backend   # native: the agents drive this machine's real GPUs
         self.quota = quota                       # also run nos-operator and nos-scheduler (Elastic Resource Quotas)
         self.kind = kind                         # xcp: partition agents; cumask: CU-mask slice agents
+        self.xcp_layout = layout                 # xcp nodes' nos.nebuly.com/xcp-layout
         self.facade = APIFacade(bookmark_every=bookmark_every)
         self.procs: Dict[str, subprocess.Popen] = {}
         self._argv: Dict[str, Any] = {}
@@ -87,7 +92,7 @@ class DevCluster:
         self.client = from_kubeconfig(self.kubeconfig)
         names = [f"node-{i}" for i in range(self.n_nodes)]
         for n in names:
-            self.client.create(ko.new_node(n, node_labels(self.gpus, kind=self.kind)))
+            self.client.create(ko.new_node(n, node_labels(self.gpus, kind=self.kind, layout=self.xcp_layout)))
             self.kubelets[n] = FakeKubelet(os.path.join(self.root, n), self.client, n)
         self._spawn("gpupartitioner", "walkai_nos_amd.cmd.gpupartitioner", self.partitioner_cfg,
                     "GpuPartitionerConfig", {})
@@ -103,7 +108,8 @@ class DevCluster:
                             "GpuAgentConfig", {constant.ENV_NODE_NAME: n})
             else:
                 self._spawn(f"partitionagent-{n}", "walkai_nos_amd.cmd.partitionagent",
-                            MigAgentConfig(devicePlugin="nos", **common), "MigAgentConfig", {constant.ENV_NODE_NAME: n})
+                            MigAgentConfig(devicePlugin="nos", sliceStateFile=os.path.join(k.root, "xcp-slices.json"),
+                                           **common), "MigAgentConfig", {constant.ENV_NODE_NAME: n})
         if self.quota:
             quiet = ["--metrics-bind-address", "0", "--health-probe-bind-address", "0", "--leader-elect", "false"]
             self._spawn("nos-operator", "walkai_nos_amd.cmd.nosoperator", None, "", {}, quiet)

@@ -44,19 +44,21 @@ def node_barrier_factory(registry, backend: str = "xgmi"):
     return lambda n: SpawnedNodeBarrier(n, backend=backend, registry=registry)
 
 
-def nos_partition_plugin(client, node: str, smi, resources, cfg):
+def nos_partition_plugin(client, node: str, smi, resources, cfg, slice_store=None):
     """The nos partition device plugin of this node: its view (device map, the node's spec/status
-    annotations, kubelet's allocated ids), one gRPC plugin per ``amd.com/<mode>_<nps>`` resource,
-    and the hook the actuator calls after a flip."""
+    annotations, kubelet's allocated ids, the CU-mask slices of sliced GPUs), one gRPC plugin per
+    ``amd.com/<mode>_<nps>`` resource, and the hook the actuator calls after a flip."""
     from ..deviceplugin.partitions import AllocatablePublisher, PartitionPluginHook, PartitionState, \
         partition_plugin_manager
     from ..kube import objects as ko
 
     def used_ids():
         return {d.device_id for d in resources.get_used_devices()}
-    state = PartitionState(smi.device_map, lambda: ko.annotations(client.get("Node", node)), used_ids)
+    state = PartitionState(smi.device_map, lambda: ko.annotations(client.get("Node", node)), used_ids,
+                           slices=slice_store.load if slice_store is not None else None)
     plugins = partition_plugin_manager(state, socket_dir=cfg.devicePluginDir,
-                                       kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"))
+                                       kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
+                                       shim_path=cfg.hbmLimitShimPath)
     publisher = AllocatablePublisher(client, node) if cfg.publishAllocatable else None
     return PartitionPluginHook(plugins, state, publisher), plugins
 
@@ -77,8 +79,11 @@ def main(argv=None) -> int:
     pc = PartitionClient(resources, smi)
     mgr = make_manager(client, cfg, "partitionagent")
     plugins = None
+    slice_store = None
     if cfg.devicePlugin == "nos":
-        dp, plugins = nos_partition_plugin(client, node, smi, resources, cfg)
+        from ..device.slicing_client import FileSliceStore
+        slice_store = FileSliceStore(cfg.sliceStateFile)  # sliced GPUs (xcp-layout slices/auto)
+        dp, plugins = nos_partition_plugin(client, node, smi, resources, cfg, slice_store)
         mgr.new_controller("nos-partition-plugin", dp.reconcile,
                            [Watch("Node", [ExcludeDelete(), MatchingName(node), AnnotationsChanged()])])
     else:
@@ -97,7 +102,7 @@ def main(argv=None) -> int:
         probe = lambda shared: ProbeRunner(shared, node, targets=device_map_targets(smi)).annotations  # noqa: E731
     _, _, actuator = setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
                                            refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe,
-                                           helpers=helpers)
+                                           helpers=helpers, slice_store=slice_store)
     log.info("device map: %s", smi.device_map().describe())
     log.info("start-up reconciliation: %s", actuator.startup())
     from ..exporters.gpu_metrics import GpuMetricsPoller

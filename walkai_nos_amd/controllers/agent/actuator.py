@@ -49,6 +49,7 @@ from ...kube.runtime import Request, Result
 from ...models import annotation as ann
 from ...models.errors import GpuError, is_not_found
 from ...models.xcp.profile import parse_profile
+from ...models.xcp.slices import parse_gpu_set
 from ...parallel.barrier import CommitBarrier
 from ...utils.metrics import REGISTRY
 from .plan import XcpConfigPlan, XcpState, new_xcp_config_plan
@@ -63,7 +64,9 @@ class Actuator:
     def __init__(self, client: Any, partition_client: Any, shared: SharedState, node_name: str,
                  device_plugin: Any = None, barrier_factory: Optional[BarrierFactory] = None,
                  verify: Optional[Callable[[int, str], bool]] = None, clock: Callable[[], float] = time.time,
-                 journal: bool = True):
+                 journal: bool = True, slice_store: Any = None):
+        """``slice_store``: where the CU-mask slice layout of sliced GPUs lives (read by the nos
+        partition plugin); None = the node has no sliced GPUs."""
         self.client = client
         self.pc = partition_client
         self.shared = shared
@@ -73,6 +76,7 @@ class Actuator:
         self.verify = verify
         self.clock = clock
         self.journal = journal
+        self.slice_store = slice_store
         self.last_applied_plan: Optional[XcpConfigPlan] = None
         self.last_applied_status: Optional[list] = None
         self.applied_plans = 0
@@ -95,10 +99,12 @@ class Actuator:
             status, spec = ann.parse_node_annotations(anns)
             spec_nps = anns.get(api.ANNOTATION_MEMORY_PARTITION_SPEC)
             status_nps = anns.get(api.ANNOTATION_MEMORY_PARTITION_STATUS)
-            if ann.spec_matches_status(spec, status) and (not spec_nps or spec_nps == status_nps):
+            sliced = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_SPEC))
+            same_layout = sliced == parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_STATUS))
+            if ann.spec_matches_status(spec, status) and (not spec_nps or spec_nps == status_nps) and same_layout:
                 log.debug("reported status matches desired partitioning")
                 return Result()
-            plan = self.plan(spec, spec_nps)
+            plan = self.plan(spec, spec_nps, sliced)
             if plan is None:
                 return Result()
             try:
@@ -123,7 +129,8 @@ class Actuator:
                 raise err
             return Result()
 
-    def plan(self, spec: List[ann.SpecAnnotation], spec_nps: Optional[str]) -> Optional[XcpConfigPlan]:
+    def plan(self, spec: List[ann.SpecAnnotation], spec_nps: Optional[str],
+             sliced: Optional[set] = None) -> Optional[XcpConfigPlan]:
         try:
             devices = self.pc.get_partition_devices()
         except GpuError as e:
@@ -134,11 +141,18 @@ class Actuator:
         state = XcpState(devices)
         current = self.pc.current_profiles()
         cur_nps = next(iter(current.values())).split("_", 1)[1] if current else None
-        if state.matches(spec) and (not spec_nps or spec_nps == cur_nps):
+        slices = self.slice_store.load() if self.slice_store is not None else {}
+        sliced = set(sliced or ()) if self.slice_store is not None else set()
+        if state.matches(spec) and (not spec_nps or spec_nps == cur_nps) and not sliced and not any(slices.values()):
             # devices already match the spec (e.g. the previous apply succeeded but was not reported)
             if all(current.get(a.index) == a.profile for a in spec):
                 return XcpConfigPlan()
-        return new_xcp_config_plan(state, current, spec, spec_nps, cur_nps)
+        extra: Dict[str, Any] = {}
+        if sliced or any(slices.values()):
+            m = self.pc.device_map()
+            extra = dict(sliced=sliced, slices=slices, used_ids=self.pc.used_ids(),
+                         gpu_ids={g.index: g.bdf for g in m.gpus}, vram_bytes={g.index: g.vram_bytes for g in m.gpus})
+        return new_xcp_config_plan(state, current, spec, spec_nps, cur_nps, **extra)
 
     # -- apply --------------------------------------------------------------------------------
     def apply(self, plan: XcpConfigPlan, plan_id: str = "") -> Optional[Exception]:
@@ -192,6 +206,13 @@ class Actuator:
             ok = self._commit(applied)
             if not ok:
                 errors.append("commit barrier vetoed the plan")
+        if ok and plan.slices and self.slice_store is not None:
+            # a re-carve is a configuration change only (no device operation, nothing to vote on):
+            # the plugin serves the new layout after its next sync
+            cur = self.slice_store.load()
+            cur.update({g: ss for g, ss in plan.slices.items()})
+            self.slice_store.save({g: ss for g, ss in cur.items() if ss})
+            changed = True
         if not ok and flipped:
             gate = helpers.held() if hasattr(helpers, "held") else contextlib.nullcontext()
             with gate:

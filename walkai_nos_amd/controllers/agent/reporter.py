@@ -27,13 +27,14 @@ log = logging.getLogger("nos.agent.reporter")
 class Reporter:
     def __init__(self, client: Any, partition_client: Any, shared: SharedState, refresh_interval: float = 10.0,
                  profile_extractor: Callable[[str], Optional[str]] = extract_profile_name,
-                 extra_annotations: Optional[Callable[[], Dict[str, str]]] = None):
+                 extra_annotations: Optional[Callable[[], Dict[str, str]]] = None, slice_store: Any = None):
         self.client = client
         self.pc = partition_client
         self.shared = shared
         self.refresh_interval = refresh_interval
         self.extract = profile_extractor
         self.extra = extra_annotations
+        self.slice_store = slice_store
 
     def reconcile(self, req: Request) -> Result:
         with self.shared.lock:
@@ -64,9 +65,17 @@ class Reporter:
                                                                        sort_keys=True, separators=(",", ":"))
         if self.shared.last_commit:
             desired_extra[api.ANNOTATION_COMMIT_STATUS] = self.shared.last_commit
+        remove = []
+        if self.slice_store is not None:
+            from ...models.xcp.slices import format_gpu_set
+            sliced = format_gpu_set(g for g, ss in self.slice_store.load().items() if ss)
+            if sliced:
+                desired_extra[api.ANNOTATION_SLICED_GPUS_STATUS] = sliced
+            elif api.ANNOTATION_SLICED_GPUS_STATUS in anns:
+                remove.append(api.ANNOTATION_SLICED_GPUS_STATUS)
         if self.extra is not None:
             desired_extra.update(self.extra())
-        extra_same = all(anns.get(k) == v for k, v in desired_extra.items())
+        extra_same = all(anns.get(k) == v for k, v in desired_extra.items()) and not remove
         if new_map == old_map and extra_same and \
                 anns.get(api.ANNOTATION_REPORTED_PARTITIONING_PLAN) == self.shared.last_parsed_plan_id:
             return Result(requeue_after=self.refresh_interval)
@@ -78,6 +87,8 @@ class Reporter:
         for s in new_status:
             a[s.key] = s.value()
         a.update(desired_extra)
+        for k in remove:
+            a.pop(k, None)
         a[api.ANNOTATION_REPORTED_PARTITIONING_PLAN] = self.shared.last_parsed_plan_id
         self.client.patch("Node", req.name, create_merge_patch(node, updated))
         log.debug("reported status for node %s (plan %s)", req.name, self.shared.last_parsed_plan_id)

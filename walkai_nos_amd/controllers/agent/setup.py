@@ -16,7 +16,7 @@ def setup_partition_agent(mgr: Manager, node_name: str, partition_client: Any, d
                           verify: Optional[Callable[[int, str], bool]] = None,
                           extra_annotations: Optional[Callable[[], dict]] = None,
                           probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None,
-                          helpers: Any = None):
+                          helpers: Any = None, slice_store: Any = None):
     """``probe``: factory taking the agent's SharedState and returning an extra-annotation hook
     (e.g. ``lambda sh: ProbeRunner(sh, node).annotations``) that measures each commit."""
     shared = SharedState(helpers)
@@ -27,9 +27,10 @@ def setup_partition_agent(mgr: Manager, node_name: str, partition_client: Any, d
         else:
             user = extra_annotations
             extra_annotations = lambda: {**user(), **hook()}  # noqa: E731
-    reporter = Reporter(mgr.client, partition_client, shared, refresh_interval, extra_annotations=extra_annotations)
+    reporter = Reporter(mgr.client, partition_client, shared, refresh_interval, extra_annotations=extra_annotations,
+                        slice_store=slice_store)
     actuator = Actuator(mgr.client, partition_client, shared, node_name, device_plugin, barrier_factory, verify,
-                        clock=mgr.clock)
+                        clock=mgr.clock, slice_store=slice_store)
     mgr.new_controller(constant.AGENT_REPORTER_CONTROLLER, reporter.reconcile,
                        [Watch("Node", [ExcludeDelete(), MatchingName(node_name), NodeResourcesChanged()])])
     mgr.new_controller(constant.AGENT_ACTUATOR_CONTROLLER, actuator.reconcile,

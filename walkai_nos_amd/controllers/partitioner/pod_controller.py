@@ -179,9 +179,14 @@ class PackParams:
                                     # to it) whose oldest pod waited this long gets a GPU drained for
                                     # it regardless of gain (0 = off) — the fairness that makes a
                                     # single GPU cycle through the modes its pods ask for
+    slice_reserve_after: float = 900.0  # seconds: sliced GPUs (xcp-layout slices/auto) — the oldest pod that
+                                    # fits on no sliced GPU this long drains one for itself (0 = never)
+    slice_fill: bool = True         # carve a sliced GPU's leftover groups into cpx slices
 
 
 def _mode_of(gpu: Any) -> Optional[str]:
+    if getattr(gpu, "sliced", False):
+        return "sliced"  # a layout, not a hardware mode: planned per pod (sliced.py)
     geo = gpu.geometry()
     return next(iter(geo)) if len(geo) == 1 else None
 
@@ -358,6 +363,13 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
             unserved.append((req, age))
     if not unserved or not current:
         return changed
+    if any(getattr(m, "layout", "partitions") != "partitions" for m in current.values()):
+        from .sliced import plan_sliced
+        plan_sliced(current, models, changed, unserved, params, mode_age)
+        if not unserved:
+            return changed
+    # the homogeneous rules below only touch GPUs of nodes laid out as hardware partitions
+    hw_nodes = {n for n, m in current.items() if getattr(m, "layout", "partitions") == "partitions"}
     first = next(iter(current.values()))
     w = getattr(first, "weight", None)
     frac = (lambda p: w(p)) if w is not None else (lambda p: 1.0)
@@ -371,9 +383,9 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         oldest[p] = max(oldest.get(p, 0.0), age)
     total_gpus = sum(len(m.gpus) for m in current.values())
     _plan_memory_partitions(current, changed, demand, oldest, unserved, params, mode_age, total_gpus, frac)
-    idle = [(name, g) for name in sorted(current) for g in current[name].gpus
+    idle = [(name, g) for name in sorted(hw_nodes) for g in current[name].gpus
             if g.is_idle() and g.target is None]
-    spx_gpus = [(n, g) for n in sorted(current) for g in current[n].gpus if (_mode_of(g) or "").startswith("spx")]
+    spx_gpus = [(n, g) for n in sorted(hw_nodes) for g in current[n].gpus if (_mode_of(g) or "").startswith("spx")]
     reserve = min(len(spx_gpus), int(round(spx_demand))) if (params.spx_reserve and total_gpus > 1) else 0
     # idle GPUs whose mode nobody is waiting for go first; SPX GPUs last (they are the reserve)
     idle.sort(key=lambda ng: ((_mode_of(ng[1]) or "").startswith("spx"), ng[0], ng[1].index))
@@ -444,7 +456,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         if not backlog and not gain_ok and not starved:
             continue
         fill = min(demand[p], 1.0)
-        cands = [(used_of(g), name, g) for name in sorted(current) for g in current[name].gpus
+        cands = [(used_of(g), name, g) for name in sorted(hw_nodes) for g in current[name].gpus
                  if g.target is None and not g.is_idle() and _mode_of(g) != p
                  and (mode_age is None or params.min_stint <= 0 or mode_age(name, g.index) >= params.min_stint)]
         if not backlog:

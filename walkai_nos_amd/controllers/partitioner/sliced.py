@@ -1,0 +1,145 @@
+"""The ``pack`` policy's planning of sliced GPUs (SPX + CU-mask slices, ``models/xcp/slices.py``).
+
+A sliced GPU changes its free slices without a drain or an amd-smi call, the way a MIG GPU
+changes free instances (ref ``internal/controllers/migagent/actuator.go:225-229``), so it is
+planned per *pod* rather than per mode:
+
+1. **layout** (``xcp-layout`` label): on a ``slices`` node every idle hardware-partitioned GPU is
+   turned into a sliced one (one flip to SPX, then never again); on an ``auto`` node an idle GPU
+   whose waiting demand is one non-SPX profile filling at least a whole GPU gets that hardware mode
+   (isolation for free when the demand is homogeneous), any other idle GPU is sliced, and a busy
+   hardware GPU that blocks a pod waiting ``slice_reserve_after`` drains towards slices;
+2. **backfill**: waiting pods, oldest first, are given a slice on the sliced GPU with the least room
+   that still fits them (best fit keeps the big holes for big pods), re-carving free slices of
+   other profiles as needed;
+3. **reservation**: the oldest pod that fits nowhere, once it has waited ``slice_reserve_after``,
+   drains the sliced GPU with the fewest groups in use for itself — its spec becomes the slices in
+   use plus the pod's slice, which does not fit yet, so the partition plugin withholds every slice
+   of that GPU (no new pod lands there) until enough of its pods have left; every pass recomputes
+   it from what is in use, and the pod is placed as soon as it fits.  Without it a whole-GPU pod
+   would wait behind an endless stream of smaller ones;
+4. **fill**: the groups left over are carved into ``cpx_nps1`` slices, so small pods are scheduled
+   without waiting for a planning pass.
+
+Measured (``tools/planner_sweep.py``, ``profiles/planner_sweep_r4_slices.json``) against the
+homogeneous pack planner on the same churn.
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, List, Mapping, Optional, Tuple
+
+from ...models.xcp.slices import LAYOUT_AUTO, LAYOUT_PARTITIONS, SLICE_NPS, groups_of, is_slice_profile, new_sliced_gpu
+
+Pending = List[Tuple[Dict[str, int], float]]
+
+
+def _single(req: Mapping[str, int]) -> Optional[Tuple[str, int]]:
+    if len(req) != 1:
+        return None
+    (p, q), = req.items()
+    return (p, q) if q > 0 else None
+
+
+def _spec(g: Any) -> Tuple[Dict[str, int], bool]:
+    return dict(g.spec_geometry()), bool(g.spec_sliced())
+
+
+def _hardware_gpu(g: Any, profile: str) -> Any:
+    """An idle GPU re-modelled as a hardware partition of ``profile`` (every partition free)."""
+    from ...models.xcp.node import new_gpu
+    h = new_gpu(g.model, g.index, profile.split("_", 1)[1])
+    h.apply_geometry({profile: round(8 / groups_of(profile))})
+    return h
+
+
+def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: Dict[str, Any], unserved: Pending,
+                params: Any, mode_age: Optional[Callable[[str, int], float]] = None) -> None:
+    """Layout choice, backfill, reservation and fill for the sliced GPUs of ``current`` (module
+    docstring); places the pods it can (removing them from ``unserved``) and records the nodes
+    whose spec changed in ``changed``."""
+    before = {n: [_spec(g) for g in m.gpus] for n, m in original.items()}
+
+    def past_stint(name: str, idx: int) -> bool:
+        return mode_age is None or params.min_stint <= 0 or mode_age(name, idx) >= params.min_stint
+
+    # 1. layout
+    demand: Dict[str, float] = {}
+    for req, _ in unserved:
+        s = _single(req)
+        if s is not None:
+            demand[s[0]] = demand.get(s[0], 0.0) + s[1] * groups_of(s[0]) / 8.0
+    for name, m in sorted(current.items()):
+        layout = getattr(m, "layout", LAYOUT_PARTITIONS)
+        if layout == LAYOUT_PARTITIONS or (m.memory_partition or SLICE_NPS) != SLICE_NPS:
+            continue
+        for i, g in enumerate(m.gpus):
+            if g.target is not None or not g.is_idle() or not past_stint(name, g.index):
+                continue
+            homogeneous = None
+            if layout == LAYOUT_AUTO and len(demand) == 1:
+                (p, d), = demand.items()
+                if d >= 1.0 - 1e-9 and is_slice_profile(p) and groups_of(p) < 8:
+                    homogeneous = p
+            if homogeneous is not None:
+                if g.sliced or g.geometry() != {homogeneous: round(8 / groups_of(homogeneous))}:
+                    m.gpus[i] = _hardware_gpu(g, homogeneous)
+            elif not g.sliced:
+                m.gpus[i] = new_sliced_gpu(g.model, g.index)
+    sliced = [(name, g) for name, m in sorted(current.items()) for g in m.gpus if g.sliced]
+    # a reservation is recomputed every pass from the slices in use (the original model)
+    used_now = {(name, g.index): dict(g.used) for name, m in original.items() for g in m.gpus}
+    for _, g in sliced:
+        if g.target is not None and g.target_sliced:
+            g.target = None
+    # 2./3. backfill and reservation, oldest first
+    reserved = False
+    claimed = set()   # GPUs that took a pod in this pass: never drained for a younger one
+    for req, age in list(unserved):
+        s = _single(req)
+        if s is None or not is_slice_profile(s[0]):
+            continue
+        p, q = s
+        need = q * groups_of(p)
+        if need > 8:
+            continue
+        cands = [(g.room(), name, g.index, g) for name, g in sliced if g.target is None and g.room() >= need]
+        if cands:
+            _, name, _, g = min(cands, key=lambda c: c[:3])
+            for _ in range(q):
+                g.claim(p)
+            claimed.add((name, g.index))
+            unserved.remove((req, age))
+            continue
+        if reserved or params.slice_reserve_after <= 0 or age < params.slice_reserve_after:
+            continue
+        victims = [(g.used_groups(), name, g.index, g) for name, g in sliced
+                   if g.target is None and (name, g.index) not in claimed]
+        if not victims and any(g.target is None for _, g in sliced):
+            continue  # every sliced GPU just took an older pod: reconsider on the next pass
+        if not victims:
+            # an auto node's busy hardware GPU in another mode drains towards slices for the pod
+            hw = [(sum(g.used.values()), name, g.index, g) for name, m in sorted(current.items())
+                  if getattr(m, "layout", LAYOUT_PARTITIONS) == LAYOUT_AUTO
+                  for g in m.gpus if not g.sliced and g.target is None and not g.is_idle()
+                  and past_stint(name, g.index)]
+            if hw:
+                _, name, _, g = min(hw, key=lambda c: c[:3])
+                g.target, g.target_sliced = {p: q}, True
+                reserved = True
+            continue
+        _, name, _, g = min(victims, key=lambda c: c[:3])
+        want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
+        want[p] = want.get(p, 0) + q
+        g.used = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
+        g.free = {}
+        g.target, g.target_sliced = want, True
+        reserved = True
+    # 4. fill
+    if params.slice_fill:
+        for _, g in sliced:
+            if g.target is None:
+                g.fill()
+    for name, m in current.items():
+        if name in before and [_spec(g) for g in m.gpus] != before[name]:
+            changed[name] = m
+

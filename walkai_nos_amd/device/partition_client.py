@@ -57,6 +57,10 @@ class PartitionClient:
                 return None
             raise
 
+    def used_ids(self) -> set:
+        """Device ids (partitions and slices) kubelet has allocated to running containers."""
+        return {d.device_id for d in self.resources.get_used_devices() if is_xcp_resource(d.resource_name)}
+
     def pods_by_gpu(self) -> Dict[int, List[str]]:
         """Physical GPU index -> ``<ns>/<pod>`` of the pods using one of its partitions."""
         out: Dict[int, set] = {}

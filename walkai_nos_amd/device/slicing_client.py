@@ -58,6 +58,44 @@ class MemorySliceStore(SliceStore):
             self.saves += 1
 
 
+class FileSliceStore(SliceStore):
+    """A node-local JSON file: the partition agent's sliced-GPU layout (``models/xcp/slices.py``),
+    which its own device plugin serves in the same process; it survives an agent restart (a host
+    path), is replaced atomically, and is re-read only when it changed (the plugin reads it on every
+    ListAndWatch poll)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self._lock = threading.Lock()
+        self._cache: Optional[tuple] = None   # (mtime_ns, size, text)
+
+    def load(self) -> SliceMap:
+        import os
+        with self._lock:
+            try:
+                st = os.stat(self.path)
+            except FileNotFoundError:
+                return {}
+            key = (st.st_mtime_ns, st.st_size)
+            if self._cache is None or self._cache[:2] != key:
+                with open(self.path) as f:
+                    self._cache = (*key, f.read())
+            return self.decode(self._cache[2])
+
+    def save(self, slices: SliceMap) -> None:
+        import os
+        text = self.encode(slices)
+        with self._lock:
+            os.makedirs(os.path.dirname(os.path.abspath(self.path)), exist_ok=True)
+            tmp = f"{self.path}.tmp.{os.getpid()}"
+            with open(tmp, "w") as f:
+                f.write(text)
+                f.flush()
+                os.fsync(f.fileno())
+            os.replace(tmp, self.path)
+            self._cache = None
+
+
 class ConfigMapSliceStore(SliceStore):
     """``ConfigMap <namespace>/nos-slices-<node>``, key ``slices.json``."""
 

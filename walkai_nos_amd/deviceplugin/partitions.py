@@ -47,11 +47,14 @@ from __future__ import annotations
 import logging
 from collections import defaultdict
 from dataclasses import dataclass
-from typing import Any, Callable, Dict, Iterable, List, Mapping, Optional, Set
+from typing import Any, Callable, Dict, Iterable, List, Mapping, Optional, Set, Tuple
 
 from .. import constant
+from ..api import v1alpha1 as api
 from ..device.protos import dp
 from ..models import annotation as ann
+from ..models.slicing.cumask import hsa_cu_mask
+from ..models.xcp.slices import SLICED_MODE, parse_gpu_set, recarve, serial_of, spec_by_gpu
 from .server import DEVICE_PLUGIN_DIR, KUBELET_SOCKET, DeviceState, PluginManager, PluginServer, \
     preferred_same_gpu
 
@@ -62,8 +65,10 @@ LOST = "gpu left the device map"
 
 def reconfiguring_gpus(annotations: Mapping[str, str]) -> frozenset:
     """GPUs whose spec annotations ask for a different geometry than their status reports (a GPU
-    without spec annotations is not being changed)."""
-    status, spec = ann.parse_node_annotations(dict(annotations or {}))
+    without spec annotations is not being changed), or for the other layout (hardware partitions
+    vs CU-mask slices, ``models/xcp/slices.py``)."""
+    anns = dict(annotations or {})
+    status, spec = ann.parse_node_annotations(anns)
     want: Dict[int, Dict[str, int]] = defaultdict(dict)
     have: Dict[int, Dict[str, int]] = defaultdict(dict)
     for a in spec:
@@ -71,7 +76,35 @@ def reconfiguring_gpus(annotations: Mapping[str, str]) -> frozenset:
     for a in status:
         if a.quantity > 0:
             have[a.index][a.profile] = have[a.index].get(a.profile, 0) + a.quantity
-    return frozenset(g for g, w in want.items() if {p: q for p, q in w.items() if q > 0} != have.get(g, {}))
+    sliced_want = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_SPEC))
+    sliced_have = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_STATUS))
+    return frozenset(g for g, w in want.items() if {p: q for p, q in w.items() if q > 0} != have.get(g, {})
+                     or (g in sliced_want) != (g in sliced_have))
+
+
+def slice_withholding(annotations: Mapping[str, str], slices: Mapping[int, List[Any]],
+                      used_ids: Set[str]) -> Tuple[frozenset, frozenset]:
+    """(GPUs whose every device is withheld, slice ids withheld) for a node with sliced GPUs.
+
+    A sliced GPU the spec keeps sliced is re-carved, not flipped: while the change is pending only
+    the free slices the agent is about to delete are withheld (the same :func:`recarve` decides),
+    so its other slices keep serving.  A spec its slices in use leave no room for is a drain: every
+    slice of the GPU is withheld, like a partitioned GPU being re-partitioned.  Any other GPU
+    follows :func:`reconfiguring_gpus`."""
+    anns = dict(annotations or {})
+    recon = set(reconfiguring_gpus(anns))
+    _, spec = ann.parse_node_annotations(anns)
+    want = spec_by_gpu(spec)
+    sliced_want = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_SPEC))
+    ids: Set[str] = set()
+    for g, ss in slices.items():
+        if not ss or g not in sliced_want or g not in recon:
+            continue
+        rc = recarve(ss, used_ids, want.get(g, {}))
+        if rc.achievable:
+            recon.discard(g)
+            ids.update(s.id for s in rc.delete)
+    return frozenset(recon), frozenset(ids)
 
 
 def draining_gpus(annotations: Mapping[str, str]) -> frozenset:
@@ -95,17 +128,37 @@ class PartitionDevice:
     healthy: bool
     reason: str = ""
     bdf: str = ""
+    #: a CU-mask slice of an SPX GPU (``models/xcp/slices.py``): its CU bits and HBM budget
+    cus: Tuple[int, ...] = ()
+    hbm_bytes: int = 0
+
+    @property
+    def sliced(self) -> bool:
+        return bool(self.cus)
 
 
 def partition_view(device_map: Any, withheld_gpus: Iterable[int], used_ids: Set[str],
-                   lost: Iterable[PartitionDevice] = ()) -> Dict[str, List[PartitionDevice]]:
+                   lost: Iterable[PartitionDevice] = (), slices: Optional[Mapping[int, List[Any]]] = None,
+                   withheld_slices: Iterable[str] = ()) -> Dict[str, List[PartitionDevice]]:
     """resource name -> the partitions to advertise, with their health (see the module docstring).
-    ``lost``: devices of GPUs that left the map since the last view, kept listed as unhealthy."""
+    ``lost``: devices of GPUs that left the map since the last view, kept listed as unhealthy.
+    ``slices``: GPU index -> CU-mask slices of the GPUs served sliced (their SPX device is
+    advertised as its slices instead); ``withheld_slices``: slice ids being re-carved away."""
     withheld = frozenset(withheld_gpus)
+    held_slices = frozenset(withheld_slices)
     out: Dict[str, List[PartitionDevice]] = defaultdict(list)
     for d in device_map.devices:
-        r = resource_of(d)
         held = d.gpu_index in withheld
+        ss = (slices or {}).get(d.gpu_index) if d.compute_mode.lower() == SLICED_MODE else None
+        if ss:
+            for s in ss:
+                r = constant.AMD_RESOURCE_PREFIX + s.profile
+                why = ("gpu re-partitioning (in use, draining)" if s.id in used_ids else "gpu re-partitioning") \
+                    if held else ("slice being re-carved" if s.id in held_slices else "")
+                out[r].append(PartitionDevice(s.id, r, d.gpu_index, serial_of(s.id), d.render_minor, not why, why,
+                                              d.bdf.lower(), tuple(s.cus), s.hbm_bytes))
+            continue
+        r = resource_of(d)
         why = ("gpu re-partitioning (in use, draining)" if d.device_id in used_ids else "gpu re-partitioning") \
             if held else ""
         out[r].append(PartitionDevice(d.device_id, r, d.gpu_index, d.partition_index, d.render_minor,
@@ -114,7 +167,7 @@ def partition_view(device_map: Any, withheld_gpus: Iterable[int], used_ids: Set[
     for d in lost:
         if d.id not in present:
             out[d.resource].append(PartitionDevice(d.id, d.resource, d.gpu_index, d.partition_index, d.render_minor,
-                                                   False, LOST, d.bdf))
+                                                   False, LOST, d.bdf, d.cus, d.hbm_bytes))
     return {r: sorted(v, key=lambda x: (x.gpu_index, x.partition_index, x.id)) for r, v in out.items()}
 
 
@@ -134,10 +187,11 @@ class PartitionState:
     spec, the reporter's status) and the partitions kubelet has allocated."""
 
     def __init__(self, device_map: Callable[[], Any], annotations: Callable[[], Mapping[str, str]],
-                 used_ids: Callable[[], Set[str]]):
+                 used_ids: Callable[[], Set[str]], slices: Optional[Callable[[], Mapping[int, List[Any]]]] = None):
         self._map = device_map
         self._annotations = annotations
         self._used = used_ids
+        self._slices = slices
         self._last: Dict[str, PartitionDevice] = {}   # devices of the previous view, by id
         self._lost: Dict[str, PartitionDevice] = {}   # devices of GPUs that left the map
 
@@ -152,7 +206,16 @@ class PartitionState:
         except Exception as e:  # noqa: BLE001 - usage only labels the reason
             log.warning("kubelet allocations unavailable: %s", e)
             used = set()
-        withheld = reconfiguring_gpus(anns)
+        slices: Mapping[int, List[Any]] = {}
+        if self._slices is not None:
+            try:
+                slices = self._slices()
+            except Exception as e:  # noqa: BLE001 - the slice store unreadable: its GPUs are withheld
+                log.warning("slice layout unavailable: %s", e)
+                slices = {}
+                anns = dict(anns)
+                anns[api.ANNOTATION_SLICED_GPUS_STATUS] = ""
+        withheld, held_slices = slice_withholding(anns, slices, used) if slices else (reconfiguring_gpus(anns), ())
         try:
             m = self._map()
         except Exception as e:  # noqa: BLE001 - a ListAndWatch stream must not end on a map error
@@ -163,14 +226,14 @@ class PartitionState:
             for d in list(self._last.values()) + [d for i, d in self._lost.items() if i not in self._last]:
                 out[d.resource].append(PartitionDevice(d.id, d.resource, d.gpu_index, d.partition_index,
                                                        d.render_minor, False, f"device map unavailable: {e}"[:120],
-                                                       d.bdf))
+                                                       d.bdf, d.cus, d.hbm_bytes))
             return {r: sorted(v, key=lambda x: (x.gpu_index, x.partition_index, x.id)) for r, v in out.items()}
         bdfs = {g.bdf.lower() for g in m.gpus}
         for d in self._last.values():
             if d.bdf not in bdfs:
                 self._lost[d.id] = d
         self._lost = {i: d for i, d in self._lost.items() if d.bdf not in bdfs}  # back on the bus
-        v = partition_view(m, withheld, used, self._lost.values())
+        v = partition_view(m, withheld, used, self._lost.values(), slices, held_slices)
         self._last = {d.id: d for ds in v.values() for d in ds if d.bdf in bdfs}
         return v
 
@@ -179,9 +242,11 @@ class PartitionDevicePlugin(PluginServer):
     """One ``amd.com/<mode>_<nps>`` resource of the node's compute partitions."""
 
     def __init__(self, resource_name: str, state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
-                 poll_interval: float = 1.0):
+                 poll_interval: float = 1.0, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so", cu_count: int = 256):
         super().__init__(resource_name, socket_dir, poll_interval, prefix="nos-xcp-")
         self.state = state
+        self.shim_path = shim_path
+        self.cu_count = cu_count
 
     def _devices(self) -> List[PartitionDevice]:
         return self.state.view().get(self.resource_name, [])
@@ -200,12 +265,19 @@ class PartitionDevicePlugin(PluginServer):
         return resp
 
     def Allocate(self, req, ctx):
+        """A partition: ``/dev/kfd`` + its own render node.  A CU-mask slice of an SPX GPU: its
+        GPU's render node + ``HSA_CU_MASK`` (the slice's CU set, every queue of the container) +
+        the HBM budget (``NOS_HBM_LIMIT_BYTES`` and the ``LD_PRELOAD`` limiter), as the CU-mask
+        slice plugin serves ``amd.com/gpu-<c>cu.<m>gb``; a whole-GPU slice needs no mask."""
         import grpc
         by_id = {d.id: d for d in self._devices()}
         resp = dp.AllocateResponse()
         for cr in req.container_requests:
             car = resp.container_responses.add()
             nodes = []
+            cus: List[int] = []
+            hbm = 0
+            gpus = set()
             for did in cr.devicesIDs:
                 d = by_id.get(did)
                 if d is None or not d.healthy:
@@ -215,7 +287,23 @@ class PartitionDevicePlugin(PluginServer):
                     raise KeyError(msg)
                 if d.render_minor >= 0:
                     nodes.append(f"/dev/dri/renderD{d.render_minor}")
+                if d.sliced:
+                    cus.extend(d.cus)
+                    hbm += d.hbm_bytes
+                    gpus.add(d.gpu_index)
+            if len(gpus) > 1:
+                msg = f"slices {list(cr.devicesIDs)} span GPUs {sorted(gpus)}: one CU mask covers one GPU"
+                if ctx is not None:
+                    ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, msg)
+                raise ValueError(msg)
             car.envs["NOS_PARTITION_IDS"] = ",".join(cr.devicesIDs)
+            if cus and len(set(cus)) < self.cu_count:
+                car.envs[constant.ENV_HSA_CU_MASK] = hsa_cu_mask(cus, 0)
+            if cus:
+                car.envs[constant.ENV_HBM_LIMIT] = str(hbm)
+                car.envs["LD_PRELOAD"] = self.shim_path
+                car.envs["NOS_SLICE_IDS"] = ",".join(cr.devicesIDs)
+                car.mounts.add(container_path=self.shim_path, host_path=self.shim_path, read_only=True)
             car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
             for n in sorted(set(nodes)):
                 car.devices.add(container_path=n, host_path=n, permissions="rw")
@@ -223,12 +311,13 @@ class PartitionDevicePlugin(PluginServer):
 
 
 def partition_plugin_manager(state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
-                             kubelet_socket: str = KUBELET_SOCKET, **kw: Any) -> PluginManager:
+                             kubelet_socket: str = KUBELET_SOCKET, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so",
+                             **kw: Any) -> PluginManager:
     """A :class:`PluginManager` over the partition view: one plugin per resource name present (a
     flip to a mode never served before registers its resource on the next sync)."""
     return PluginManager(None, socket_dir=socket_dir, kubelet_socket=kubelet_socket,
                          resources=lambda: sorted(state.view()),
-                         factory=lambda r: PartitionDevicePlugin(r, state, socket_dir), **kw)
+                         factory=lambda r: PartitionDevicePlugin(r, state, socket_dir, shim_path=shim_path), **kw)
 
 
 class AllocatablePublisher:

@@ -36,14 +36,24 @@ class PartitionedGPU:
     #: are still in use: the GPU is *draining* — no new pod is placed on it, and it flips to
     #: ``target`` as soon as it is idle (MI355X: a flip destroys every partition)
     target: Optional[Dict[str, int]] = None
+    #: the drain target is a sliced layout (SPX + CU-mask slices, ``models/xcp/slices.py``)
+    target_sliced: bool = False
+
+    #: served as CU-mask slices of an SPX GPU (``SlicedGPU``) rather than hardware partitions
+    sliced = False
 
     def clone(self) -> "PartitionedGPU":
         return PartitionedGPU(self.model, self.index, [dict(g) for g in self.allowed_geometries],
-                              dict(self.used), dict(self.free), dict(self.target) if self.target else None)
+                              dict(self.used), dict(self.free), dict(self.target) if self.target else None,
+                              self.target_sliced)
 
     def spec_geometry(self) -> Geometry:
         """What the spec should say for this GPU: the drain target, else the geometry."""
         return dict(self.target) if self.target else self.geometry()
+
+    def spec_sliced(self) -> bool:
+        """Whether the spec asks for this GPU as slices (the drain target's layout, else its own)."""
+        return self.target_sliced if self.target else self.sliced
 
     def geometry(self) -> Geometry:
         out: Geometry = {}
@@ -158,11 +168,13 @@ class PartitionedNode:
     #: switches the node to (every GPU of the node re-partitioned, only when all are idle)
     memory_partition: Optional[str] = None
     memory_target: Optional[str] = None
+    #: xcp layout of the node (``partitions`` | ``slices`` | ``auto``, ``models/xcp/slices.py``)
+    layout: str = "partitions"
 
     def clone(self) -> "PartitionedNode":
         return PartitionedNode(self.name, [g.clone() for g in self.gpus], dict(self.allocatable),
                                self.is_resource, self.as_resource, self.weight, self.memory_partition,
-                               self.memory_target)
+                               self.memory_target, self.layout)
 
     def geometry(self) -> Geometry:
         out: Geometry = {}

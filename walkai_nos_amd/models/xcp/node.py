@@ -9,6 +9,7 @@ from __future__ import annotations
 
 from typing import Any, Dict, List, Mapping
 
+from ...api import v1alpha1 as api
 from ...kube import objects as ko
 from .. import annotation as ann
 from .. import gpu_util
@@ -16,6 +17,7 @@ from .. import resource as res
 from ..partitioned import PartitionedGPU, PartitionedNode
 from .known_configs import get_allowed_geometries
 from .profile import as_resource_name, extract_profile_name, is_xcp_resource
+from .slices import LAYOUT_PARTITIONS, LAYOUT_SLICES, LAYOUTS, SLICE_NPS, new_sliced_gpu, parse_gpu_set
 
 
 def new_gpu(model: str, index: int, nps: str, used: Mapping[str, int] | None = None,
@@ -34,11 +36,24 @@ def fraction_weight(profile: str) -> float:
 SCORING = {"pods": None, "fraction": fraction_weight}
 
 
+def get_layout(node: Dict[str, Any]) -> str:
+    """The node's ``nos.nebuly.com/xcp-layout`` (unknown values: hardware partitions only). Slices
+    need NPS1 (a sliced GPU is in SPX, which other memory modes do not offer)."""
+    v = (ko.labels(node).get(api.LABEL_XCP_LAYOUT) or LAYOUT_PARTITIONS).lower()
+    if v not in LAYOUTS or gpu_util.get_memory_partition(node) != SLICE_NPS:
+        return LAYOUT_PARTITIONS
+    return v
+
+
 def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode:
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
     nps = gpu_util.get_memory_partition(node)
-    status, spec = ann.parse_node_annotations(ko.annotations(node))
+    anns = ko.annotations(node)
+    status, spec = ann.parse_node_annotations(anns)
+    layout = get_layout(node)
+    sliced_now = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_STATUS)) if layout != LAYOUT_PARTITIONS else set()
+    sliced_spec = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_SPEC))
     gpus: Dict[int, PartitionedGPU] = {}
     spec_by_gpu: Dict[int, Dict[str, int]] = {}
     for a in spec:
@@ -46,13 +61,21 @@ def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode
     for idx, items in sorted(ann.group_by_gpu_index(status).items()):
         used = {a.profile: a.quantity for a in items if a.is_used()}
         free = {a.profile: a.quantity for a in items if a.is_free()}
-        gpus[idx] = new_gpu(model, idx, nps, used, free)
+        sliced = idx in sliced_now
+        gpus[idx] = new_sliced_gpu(model, idx, used, free) if sliced else new_gpu(model, idx, nps, used, free)
         want = {p: q for p, q in spec_by_gpu.get(idx, {}).items() if q > 0}
-        if want and any(q > 0 for q in used.values()) and want != gpus[idx].geometry():
-            gpus[idx].target = want  # a flip the agent cannot apply until the GPU drains
+        want_sliced = idx in sliced_spec
+        busy = any(q > 0 for q in used.values())
+        if want and (want != gpus[idx].geometry() or want_sliced != sliced) and (busy or (sliced and want_sliced)):
+            # a change the agent cannot apply until the GPU drains; on a sliced GPU also when idle:
+            # a reservation spec that no longer matches what is in use is replanned, never left in
+            # place (the plugin withholds the GPU for as long as the spec says so)
+            gpus[idx].target = want
+            gpus[idx].target_sliced = want_sliced
     for i in range(count):
         if i not in gpus:
-            gpus[i] = new_gpu(model, i, nps)
+            # a GPU nothing is reported for yet (a fresh node): in SPX, sliced on a slices node
+            gpus[i] = new_sliced_gpu(model, i) if layout == LAYOUT_SLICES else new_gpu(model, i, nps)
     # a node-wide memory-partition switch in progress (spec NPS != observed): every GPU is
     # re-partitioned, idle ones included, so none is offered to new pods until the switch lands
     spec_nps = gpu_util.get_spec_memory_partition(node)
@@ -65,7 +88,7 @@ def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode
     allocatable = res.from_k8s(ko.node_allocatable(node))
     return PartitionedNode(ko.name(node), [gpus[i] for i in sorted(gpus)], allocatable,
                            is_resource=is_xcp_resource, as_resource=as_resource_name, weight=SCORING[scoring],
-                           memory_partition=nps, memory_target=switching)
+                           memory_partition=nps, memory_target=switching, layout=layout)
 
 
 def get_requested_profiles(pod: Dict[str, Any]) -> Dict[str, int]:

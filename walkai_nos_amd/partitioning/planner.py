@@ -50,7 +50,8 @@ def build_node_partitioning(node: Union[PartitionedNode, SlicingNode], memory_pa
                 continue
             r = as_res(p) if as_res is not None else _slice_resource(p)
             resources[r] = resources.get(r, 0) + q
-        gpus.append(GPUPartitioning(g.index, resources))
+        sliced = g.spec_sliced() if hasattr(g, "spec_sliced") else False
+        gpus.append(GPUPartitioning(g.index, resources, sliced))
     return NodePartitioning(gpus, memory_partition)
 
 
@@ -92,6 +93,12 @@ class Partitioner:
             if k.startswith(api.ANNOTATION_GPU_SPEC_PREFIX):
                 del anns[k]
         anns.update(spec_annotations(partitioning))
+        sliced = [g.gpu_index for g in partitioning.gpus if g.sliced]
+        if sliced:
+            from ..models.xcp.slices import format_gpu_set
+            anns[api.ANNOTATION_SLICED_GPUS_SPEC] = format_gpu_set(sliced)
+        else:
+            anns.pop(api.ANNOTATION_SLICED_GPUS_SPEC, None)
         anns[api.ANNOTATION_PARTITIONING_PLAN] = plan_id
         if partitioning.memory_partition:
             anns[api.ANNOTATION_MEMORY_PARTITION_SPEC] = partitioning.memory_partition

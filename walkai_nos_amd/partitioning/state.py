@@ -11,9 +11,12 @@ from ..utils.util import unordered_equal
 class GPUPartitioning:
     gpu_index: int
     resources: Dict[str, int] = field(default_factory=dict)  # resource name -> quantity
+    #: MI355X: served as CU-mask slices of an SPX GPU (models/xcp/slices.py)
+    sliced: bool = False
 
     def canonical(self) -> str:
-        return f"{self.gpu_index}|" + ",".join(f"{k}={v}" for k, v in sorted(self.resources.items()))
+        return f"{self.gpu_index}|" + ",".join(f"{k}={v}" for k, v in sorted(self.resources.items())) + \
+            ("|sliced" if self.sliced else "")
 
 
 @dataclass

@@ -64,7 +64,9 @@ class SimDevicePlugin:
 
     def __init__(self, smi: FakeAmdSmi, store: Optional[MemorySliceStore] = None, plugin: str = "nos",
                  annotations: Optional[Callable[[], Dict[str, str]]] = None,
-                 used: Optional[Callable[[], set]] = None):
+                 used: Optional[Callable[[], set]] = None, xcp_slices: Optional[MemorySliceStore] = None):
+        """``store``: a cumask node's slice store; ``xcp_slices``: the CU-mask slices of an xcp
+        node's sliced GPUs (served by the nos partition plugin next to its partitions)."""
         self.smi = smi
         self.store = store
         self.plugin = plugin
@@ -74,7 +76,8 @@ class SimDevicePlugin:
         self.state = None
         if store is None and plugin == "nos":
             from ..deviceplugin.partitions import PartitionState
-            self.state = PartitionState(smi.device_map, annotations or (lambda: {}), used or (lambda: set()))
+            self.state = PartitionState(smi.device_map, annotations or (lambda: {}), used or (lambda: set()),
+                                        slices=xcp_slices.load if xcp_slices is not None else None)
         self.reregister()
 
     def current(self) -> Dict[str, List[Tuple[str, bool]]]:
@@ -196,6 +199,7 @@ class SimNode:
     kubelet: SimKubelet
     manager: Manager
     dp_counter: Any = field(default_factory=lambda: itertools.count(1))
+    xcp_slices: Optional[MemorySliceStore] = None   # CU-mask slices of the node's sliced GPUs
 
 
 class KubeScheduler:
@@ -300,11 +304,16 @@ class SimCluster:
                  kind: str = api.PARTITIONING_KIND_XCP, refresh_interval: float = 10.0,
                  batch_timeout: float = 0.0, batch_idle: float = 0.0, clock: Optional[SimClock] = None,
                  scoring: str = "fraction", policy: str = "fifo", elastic_quota: bool = False,
-                 device_plugin: str = "nos", pack: Any = None):
+                 device_plugin: str = "nos", pack: Any = None, xcp_layout: str = "partitions"):
         """``device_plugin``: ``nos`` (the nos partition plugin: drains enforced through device
-        health) or ``amd`` (the AMD k8s-device-plugin, restarted after flips: no drain enforcement)."""
+        health) or ``amd`` (the AMD k8s-device-plugin, restarted after flips: no drain enforcement).
+        ``xcp_layout``: the nodes' ``nos.nebuly.com/xcp-layout`` (``partitions`` | ``slices`` |
+        ``auto``; slices need the nos plugin)."""
         if device_plugin not in ("nos", "amd"):
             raise ValueError(f"unknown device plugin {device_plugin!r}")
+        if xcp_layout != "partitions" and device_plugin != "nos":
+            raise ValueError("CU-mask slices of xcp nodes are served by the nos partition plugin")
+        self.xcp_layout = xcp_layout
         self.clock = clock or SimClock()
         self.api = InMemoryAPIServer(clock=self.clock)
         self.kind = kind
@@ -345,6 +354,7 @@ class SimCluster:
     def add_node(self, name: str, n_gpus: int, model: str, refresh_interval: float) -> SimNode:
         smi = FakeAmdSmi(n_gpus=n_gpus, model=model)
         store = MemorySliceStore() if self.kind == api.PARTITIONING_KIND_CUMASK else None
+        xcp_slices = MemorySliceStore() if store is None and self.device_plugin == "nos" else None
         holder: Dict[str, SimKubelet] = {}
 
         def node_annotations() -> Dict[str, str]:
@@ -353,15 +363,18 @@ class SimCluster:
             except NotFound:
                 return {}
         plugin = SimDevicePlugin(smi, store, plugin=self.device_plugin, annotations=node_annotations,
-                                 used=lambda: set(holder["k"].used_ids()) if "k" in holder else set())
+                                 used=lambda: set(holder["k"].used_ids()) if "k" in holder else set(),
+                                 xcp_slices=xcp_slices)
         kubelet = SimKubelet(name, plugin, smi)
         holder["k"] = kubelet
         labels = {api.LABEL_GPU_PARTITIONING: self.kind, constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}",
                   constant.LABEL_AMD_GPU_COUNT: str(n_gpus), constant.LABEL_AMD_GPU_VRAM: "288G",
                   constant.LABEL_AMD_GPU_CU_COUNT: "256"}
+        if self.kind == api.PARTITIONING_KIND_XCP and self.xcp_layout != "partitions":
+            labels[api.LABEL_XCP_LAYOUT] = self.xcp_layout
         self.api.create(ko.new_node(name, labels, allocatable=kubelet.allocatable()))
         mgr = Manager(self.api, clock=self.clock)
-        sn = SimNode(name, smi, plugin, kubelet, mgr)
+        sn = SimNode(name, smi, plugin, kubelet, mgr, xcp_slices=xcp_slices)
         self.nodes[name] = sn
         self._create_dp_pod(sn)
         if store is None and self.device_plugin == "nos":
@@ -376,7 +389,7 @@ class SimCluster:
         else:
             pc = PartitionClient(kubelet.resource_client(), smi)
             setup_partition_agent(mgr, name, pc, device_plugin=dp, barrier_factory=lambda n: LocalBarrier(n),
-                                  refresh_interval=refresh_interval)
+                                  refresh_interval=refresh_interval, slice_store=xcp_slices)
         return sn
 
     def _create_dp_pod(self, sn: SimNode) -> None:
