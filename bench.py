@@ -40,6 +40,9 @@ def main() -> int:
     ap.add_argument("--device-plugin", default="nos", choices=("nos", "amd"),
                     help="nos: drains enforced by the partition plugin's device health; amd: no enforcement")
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
+    ap.add_argument("--layout", default="slices", choices=("partitions", "slices", "auto"),
+                    help="the node's nos.nebuly.com/xcp-layout: hardware partitions only, sliced GPUs "
+                         "(SPX + CU-mask slices, mixed geometries), or the planner's choice per GPU")
     ap.add_argument("--depth", type=int, default=1,
                     help="inferences in flight per pod stream (1 = the reference demo's synchronous loop)")
     ap.add_argument("--pod-streams", type=int, default=1,
@@ -76,7 +79,7 @@ def main() -> int:
                       preroll=args.preroll, quantum_s=args.quantum, cluster_s=args.cluster_s,
                       flip_cost_s=args.flip_cost, policy=args.policy, depth=args.depth,
                       density=not args.no_density, pod_streams=args.pod_streams, lane_cus=args.lane_cus,
-                      device_plugin=args.device_plugin)
+                      device_plugin=args.device_plugin, layout=args.layout)
     if args.emulation:
         cfg.emulation = args.emulation
     res = run_bench(cfg)

@@ -2,9 +2,10 @@
 //
 //   nos-gpuhelper barrier --votes 1,1,0,... [--expect N] [--backend xgmi|rccl]
 //
-// ``xgmi`` (default): a ring of peer-to-peer token writes over xGMI (csrc/p2p_barrier.hip) — every
-// device executes, every link of the ring carries its token; ``rccl``: one ncclCommInitAll clique
-// and a grouped 4-byte all-reduce (csrc/rccl_barrier.cpp).
+// ``xgmi`` (default): a ring of peer-to-peer token writes over xGMI (csrc/p2p_barrier.hip), planned
+// over the peer-capable links (csrc/ring_plan.h; a device without a peer path writes locally) —
+// every device executes, every link of the ring carries its token; ``rccl``: one ncclCommInitAll
+// clique and a grouped 4-byte all-reduce (csrc/rccl_barrier.cpp).
 //
 // The agent never initialises HIP itself (a KFD context in the agent would make every later mode
 // switch fail with "busy"), so each node-atomic commit runs in a child process spawned after the
@@ -35,6 +36,9 @@ int nos_barrier_init_all(int ndev, const int* devlist, void** handle);
 int nos_barrier_allreduce_all(void* handle, const int32_t* votes, int32_t* result);
 int nos_barrier_destroy_all(void* handle);
 const char* nos_p2p_last_error();
+const char* nos_p2p_last_plan();
+int nos_p2p_last_peer_links();
+int nos_p2p_last_local();
 int nos_p2p_barrier(int n, const int32_t* votes, int32_t* sum, int32_t* intact);
 }
 
@@ -76,6 +80,8 @@ int barrier(const std::vector<int32_t>& votes, int expect, const std::string& ba
   tune_rccl_env();
   std::string err;
   double hip_init = 0, comm_init = 0, allreduce = 0, destroy = 0;
+  std::string ring;
+  int peer_links = -1, local = -1;
   int seen = -1;
   int32_t sum = 0;
   hipError_t e = hipInit(0);
@@ -94,6 +100,18 @@ int barrier(const std::vector<int32_t>& votes, int expect, const std::string& ba
     int rc = nos_p2p_barrier(seen, votes.data(), &sum, &intact);
     comm_init = 0;
     allreduce = ms_since(t1);
+    ring = nos_p2p_last_plan();
+    peer_links = nos_p2p_last_peer_links();
+    local = nos_p2p_last_local();
+    if (rc == -3) {
+      // a device did not complete its write before the deadline: report the veto and leave at once
+      // (tearing the context down would wait for that device)
+      std::printf("{\"n\": %zu, \"seen\": %d, \"sum\": 0, \"hip_init_ms\": %.3f, \"allreduce_ms\": %.3f, "
+                  "\"total_ms\": %.3f, \"native\": true, \"backend\": \"xgmi\", \"error\": \"%s\"}\n",
+                  votes.size(), seen, hip_init, allreduce, ms_since(t0), json_escape(nos_p2p_last_error()).c_str());
+      std::fflush(stdout);
+      std::_Exit(0);
+    }
     if (rc != 0)
       err = std::string("p2p ring: ") + nos_p2p_last_error();
     else if (intact != seen)
@@ -126,6 +144,9 @@ int barrier(const std::vector<int32_t>& votes, int expect, const std::string& ba
               "\"backend\": \"%s\"",
               votes.size(), seen, err.empty() ? sum : 0, hip_init, comm_init, allreduce, destroy, ms_since(t0),
               backend.c_str());
+  if (peer_links >= 0)
+    std::printf(", \"ring\": \"%s\", \"peer_links\": %d, \"local_writes\": %d", json_escape(ring).c_str(),
+                peer_links, local);
   if (!err.empty()) std::printf(", \"error\": \"%s\"", json_escape(err).c_str());
   std::printf("}\n");
   std::fflush(stdout);

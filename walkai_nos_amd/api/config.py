@@ -149,11 +149,16 @@ class MigAgentConfig(AgentConfig):
     # agent restart keeps serving the slices pods run on
     sliceStateFile: str = "/var/lib/nos/xcp-slices.json"
     hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
+    # probe-on-commit health rule: a partition/slice whose bf16 rate per CU is below this fraction of
+    # its model's expected rate is advertised Unhealthy (0 = never)
+    probeHealthyFraction: float = 0.7
 
     def validate(self) -> None:
         super().validate()
         if self.devicePlugin not in ("nos", "amd"):
             raise ValueError("devicePlugin must be 'nos' or 'amd'")
+        if not 0.0 <= self.probeHealthyFraction < 1.0:
+            raise ValueError("probeHealthyFraction must be in [0, 1)")
 
 
 @dataclass

@@ -115,8 +115,12 @@ FLIP_COST_COMPONENTS = {"commit_barrier_s": 0.33, "probe_s": 0.39, "plugin_push_
 FLIP_COST_MEASURED = ("commit_barrier_s", "probe_s", "plugin_push_s")
 
 
-def default_flip_cost() -> float:
-    return round(sum(FLIP_COST_COMPONENTS.values()), 2)
+def default_flip_cost(commit_barrier_s: Optional[float] = None) -> float:
+    """The flip outage from its components, with this run's measured commit barrier if given."""
+    parts = dict(FLIP_COST_COMPONENTS)
+    if commit_barrier_s is not None and commit_barrier_s >= 0:
+        parts["commit_barrier_s"] = commit_barrier_s
+    return round(sum(parts.values()), 3)
 
 
 @dataclass
@@ -148,10 +152,13 @@ class BenchConfig:
     pack: Optional[Dict[str, float]] = None  # PackParams overrides (field name -> value)
     arrivals: str = "steady"             # steady (constant rate, seeded phase) | poisson
     layout: str = "partitions"           # node label nos.nebuly.com/xcp-layout: partitions | slices | auto
+    commit_barrier_s: float = -1.0       # this run's measured node commit barrier (<0: the component constant)
 
     def __post_init__(self) -> None:
+        #: the flip cost is the components' sum (so a measured commit barrier replaces its constant)
+        self.flip_cost_default = self.flip_cost_s < 0
         if self.flip_cost_s < 0:
-            self.flip_cost_s = default_flip_cost()
+            self.flip_cost_s = default_flip_cost(self.commit_barrier_s)
 
     @property
     def flip_quanta(self) -> float:
@@ -880,8 +887,11 @@ def _mean(v: List[float]) -> float:
 
 def flip_cost_report(cfg: BenchConfig) -> Dict[str, Any]:
     out: Dict[str, Any] = {"total_s": cfg.flip_cost_s, "per_quantum": round(cfg.flip_quanta, 4)}
-    if abs(cfg.flip_cost_s - default_flip_cost()) < 1e-9:
+    if abs(cfg.flip_cost_s - default_flip_cost(cfg.commit_barrier_s)) < 1e-9:
         out["components_s"] = dict(FLIP_COST_COMPONENTS)
+        if cfg.commit_barrier_s >= 0:
+            out["components_s"]["commit_barrier_s"] = round(cfg.commit_barrier_s, 3)
+            out["commit_barrier_source"] = "measured in this run before the window (xgmi helper over every device)"
         out["measured"] = list(FLIP_COST_MEASURED)
         out["estimated"] = [k for k in FLIP_COST_COMPONENTS if k not in FLIP_COST_MEASURED]
     else:
@@ -901,6 +911,43 @@ def flip_sensitivity(cfg: BenchConfig, costs=(2.0, 5.0, 10.0, 30.0), steps: Opti
     return out
 
 
+def seed_model(cfg: BenchConfig, seeds=(1, 2, 3, 4, 5)) -> Dict[str, Any]:
+    """The control plane alone over the same window for other churn seeds (no GPU): how much the
+    default seed's window is representative. ``inf_per_s_model`` prices served partition-time with
+    :data:`MODE_RATES`; ``cpx_served_windows``: windows in which some 1/8-GPU pod was served."""
+    import dataclasses
+    rows = {}
+    for sd in seeds:
+        c = dataclasses.replace(cfg, seed=sd, rank=0, world=1)
+        r = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
+        rows[str(sd)] = {"inf_per_s_model": r["inf_per_s_model"], "util_pct": r["util_pct"],
+                         "pending_mean": r["pending_mean"],
+                         "served": {p: v["inferences"] > 0 for p, v in r["per_profile"].items()}}
+    v = [x["inf_per_s_model"] for x in rows.values()]
+    c = dataclasses.replace(cfg, rank=0, world=1)
+    own = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)["inf_per_s_model"]
+    return {"seeds": list(seeds), "mean": round(sum(v) / len(v), 1), "min": min(v), "max": max(v),
+            "this_seed_model": own, "cpx_served_windows": sum(1 for x in rows.values() if x["served"]["cpx_nps1"]),
+            "per_seed": rows}
+
+
+def sustainable_load_row(cfg: BenchConfig, load: float = 0.85, seeds=(1, 2, 3, 4), steps: int = 120) -> Dict[str, Any]:
+    """The control plane alone at the load the planner keeps up with (no GPU): allocation, queue and
+    the worst seed's p99 time-to-schedule per profile, in mean pod lifetimes."""
+    import dataclasses
+    util, pend, p99 = [], [], {}
+    for sd in seeds:
+        c = dataclasses.replace(cfg, seed=sd, offered_load=load, rank=0, world=1)
+        r = control_only(c, steps)
+        util.append(r["util_pct"])
+        pend.append(r["pending_mean"])
+        for prof, row in r["per_profile"].items():
+            if row.get("tts_lifetimes_p99") is not None:
+                p99[prof] = max(p99.get(prof, 0.0), row["tts_lifetimes_p99"])
+    return {"offered_load": load, "seeds": list(seeds), "steps": steps, "util_pct_mean": round(_mean(util), 2),
+            "pending_mean": round(_mean(pend), 2), "tts_p99_lifetimes_worst_seed": p99}
+
+
 def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     import torch
     import torch.distributed as dist
@@ -911,6 +958,17 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     from .parallel.barrier import LocalBarrier, RankCommitBarrier
 
     distributed = cfg.world > 1
+    if cfg.flip_cost_default:
+        # charge flips this run's own commit barrier (the node's devices, spawned as the agent does)
+        measured = measure_commit_barrier() if cfg.rank == 0 else None
+        if distributed:
+            t = torch.tensor([measured if measured is not None else -1.0], dtype=torch.float64,
+                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, 0)
+            measured = float(t.item()) if t.item() >= 0 else None
+        if measured is not None:
+            cfg.commit_barrier_s = measured
+            cfg.flip_cost_s = default_flip_cost(measured)
     if distributed:
         # the agent's commit path (Actuator._commit -> barrier.vote_all(per-device votes)); each
         # rank contributes the votes of its own GPU's partitions, all-reduced over RCCL
@@ -972,6 +1030,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     from .ops import kernels as K
     flops = YolosSmall().flops_per_inference(cfg.hw)
     sens = flip_sensitivity(cfg) if cfg.rank == 0 else {}
+    seeds = seed_model(cfg) if cfg.rank == 0 else {}
+    sustainable = sustainable_load_row(cfg) if cfg.rank == 0 else {}
     life_s = cfg.mean_lifetime_quanta * cfg.cluster_s
     return {
         "metric": "aggregate GPU utilization % + schedulable pods/node, mixed fractional-GPU load",
@@ -1011,6 +1071,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
         "dark_wall_s": round(nb.dark_wall_s, 3),
         "flip_cost_sensitivity": sens,
+        "seed_model": seeds,
+        "load_0.85": sustainable,
         "commit_barrier_node": barrier_8dev,
         "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},
         "density": density,
@@ -1022,15 +1084,33 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "baseline_ref": BASELINE_LABEL,
         "config": {"model": "yolos-small (hustvl/yolos-small architecture, fp32, 800x1066, batch 1)",
                    "global_batch": 1, "seq_len": 1 + (cfg.hw[0] // 16) * (cfg.hw[1] // 16) + 100,
-                   "parallelism": f"fractional-gpu xcp partitions, {cfg.gpus} GPU node",
+                   "parallelism": f"fractional-gpu xcp {cfg.layout}, {cfg.gpus} GPU node",
                    "mix": {p: w for p, w in MIX}, "offered_load_per_gpu": cfg.offered_load,
-                   "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy,
+                   "lifetime_quanta": list(cfg.lifetime), "policy": cfg.policy, "xcp_layout": cfg.layout,
                    "device_plugin": cfg.device_plugin, "scheduler": "kube-scheduler semantics (allocatable)",
                    "backend": cfg.backend, "hip_graphs": cfg.graphs, "depth": cfg.depth,
                    "pod_streams": cfg.pod_streams, "lane_cus": cfg.lane_cus,
                    "partition_emulation": cfg.emulation,
                    "fp32_matmul": (K.get_fp32_matmul() if cfg.backend == "hip" else "hipblaslt-f32")},
     }
+
+
+def measure_commit_barrier() -> Optional[float]:
+    """Wall seconds of one xGMI commit barrier over every device this process can see (the native
+    helper, spawned as the agent spawns it), or None when it cannot run."""
+    try:
+        from .ops import native
+        from .parallel.spawned import NATIVE_HELPER, SpawnedNodeBarrier
+        if not native.available(NATIVE_HELPER):
+            return None
+        import torch
+        n = torch.cuda.device_count()
+        b = SpawnedNodeBarrier(n, backend="xgmi", native=True, timeout=60.0)
+        if not b.vote_all([True] * n):
+            return None
+        return round(float(b.last["wall_ms"]) / 1000.0, 3)
+    except Exception:  # noqa: BLE001 - the component constant is charged instead
+        return None
 
 
 def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
@@ -1050,7 +1130,8 @@ def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
             b = SpawnedNodeBarrier(n, backend=backend, native=True, timeout=120.0)
             r = {"committed": b.vote_all([True] * n)}
             r.update({k: b.last.get(k) for k in ("wall_ms", "hip_init_ms", "comm_init_ms", "allreduce_ms",
-                                                  "destroy_ms", "error") if b.last.get(k) is not None})
+                                                  "destroy_ms", "ring", "peer_links", "local_writes", "error")
+                      if b.last.get(k) is not None})
             out[backend] = r
         return out
     except Exception as e:  # noqa: BLE001 - reported, never fatal to the bench

@@ -44,7 +44,7 @@ def node_barrier_factory(registry, backend: str = "xgmi"):
     return lambda n: SpawnedNodeBarrier(n, backend=backend, registry=registry)
 
 
-def nos_partition_plugin(client, node: str, smi, resources, cfg, slice_store=None):
+def nos_partition_plugin(client, node: str, smi, resources, cfg, slice_store=None, degraded=None):
     """The nos partition device plugin of this node: its view (device map, the node's spec/status
     annotations, kubelet's allocated ids, the CU-mask slices of sliced GPUs), one gRPC plugin per
     ``amd.com/<mode>_<nps>`` resource, and the hook the actuator calls after a flip."""
@@ -55,7 +55,7 @@ def nos_partition_plugin(client, node: str, smi, resources, cfg, slice_store=Non
     def used_ids():
         return {d.device_id for d in resources.get_used_devices()}
     state = PartitionState(smi.device_map, lambda: ko.annotations(client.get("Node", node)), used_ids,
-                           slices=slice_store.load if slice_store is not None else None)
+                           slices=slice_store.load if slice_store is not None else None, degraded=degraded)
     plugins = partition_plugin_manager(state, socket_dir=cfg.devicePluginDir,
                                        kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
                                        shim_path=cfg.hbmLimitShimPath)
@@ -80,10 +80,12 @@ def main(argv=None) -> int:
     mgr = make_manager(client, cfg, "partitionagent")
     plugins = None
     slice_store = None
+    runner: dict = {}   # the probe runner, once built (the plugin withholds what it finds degraded)
     if cfg.devicePlugin == "nos":
         from ..device.slicing_client import FileSliceStore
         slice_store = FileSliceStore(cfg.sliceStateFile)  # sliced GPUs (xcp-layout slices/auto)
-        dp, plugins = nos_partition_plugin(client, node, smi, resources, cfg, slice_store)
+        dp, plugins = nos_partition_plugin(client, node, smi, resources, cfg, slice_store,
+                                           degraded=lambda: runner["r"].degraded() if "r" in runner else {})
         mgr.new_controller("nos-partition-plugin", dp.reconcile,
                            [Watch("Node", [ExcludeDelete(), MatchingName(node), AnnotationsChanged()])])
     else:
@@ -99,7 +101,16 @@ def main(argv=None) -> int:
     probe = None
     if cfg.probeOnCommit:
         from ..controllers.agent.probe import ProbeRunner, device_map_targets
-        probe = lambda shared: ProbeRunner(shared, node, targets=device_map_targets(smi)).annotations  # noqa: E731
+        from ..models.xcp.known_configs import get_model_spec
+        spec = get_model_spec(gpus[0].model)
+
+        def probe(shared):
+            runner["r"] = ProbeRunner(shared, node, targets=device_map_targets(
+                smi, slice_store.load if slice_store is not None else None),
+                used=lambda: {d.device_id for d in resources.get_used_devices()},
+                expected_per_cu=spec.probe_bf16_tflops_per_cu if spec else None,
+                healthy_fraction=cfg.probeHealthyFraction)
+            return runner["r"].annotations
     _, _, actuator = setup_partition_agent(mgr, node, pc, device_plugin=dp, barrier_factory=bf,
                                            refresh_interval=cfg.reportConfigIntervalSeconds, probe=probe,
                                            helpers=helpers, slice_store=slice_store)

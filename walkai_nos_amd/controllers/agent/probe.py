@@ -12,6 +12,13 @@ as Prometheus gauges (``nos_probe_slice_tflops``, ``nos_probe_tflops_per_cu``,
 1/8 of the chip, and a degraded partition shows up as an outlier instead of a silent slowdown.
 
 For CU-mask slices the runner probes each slice's CU set on a CU-masked stream of the physical GPU.
+
+**The probe feeds the operator** (VERDICT r3 #5): a target whose bf16 MFMA rate per CU falls below
+``healthy_fraction`` of its model's expected rate (``GpuModelSpec.probe_bf16_tflops_per_cu``) is
+marked ``degraded`` with the reason; the nos partition plugin then advertises that partition (or
+slice) Unhealthy, the planner prefers GPUs without degraded targets, and the cluster-info snapshot
+exports every probe with its per-CU rate. A round never probes a device a pod is using (the probe
+would steal its CUs): used targets keep their last result, new ones are probed once they appear.
 """
 from __future__ import annotations
 
@@ -42,13 +49,36 @@ def hip_probe(device: int, cus: Optional[List[int]], label: str) -> Dict[str, fl
             "hbm_gbps": round(float(hbm.get("gbps", 0.0)), 0)}
 
 
-def device_map_targets(smi: Any) -> TargetsFn:
-    """Every logical device of the node's current device map, labelled ``gpu<i>.p<k>``; the
-    device index is the HIP ordinal a freshly spawned helper sees for it."""
+def device_map_targets(smi: Any, slices: Optional[Callable[[], Dict[int, list]]] = None) -> TargetsFn:
+    """Every logical device of the node's current device map, labelled ``gpu<i>.p<k>`` — or, for a
+    sliced GPU (``slices``: the agent's slice layout), each of its CU-mask slices, labelled by slice
+    id; the device index is the HIP ordinal a freshly spawned helper sees for it. Each target carries
+    ``{"gpu", "device_id"}`` (what kubelet allocates, so a target in use is recognised)."""
     def targets() -> List[tuple]:
-        return [(d.hip_id, None, f"gpu{d.gpu_index}.p{d.partition_index}")
-                for d in sorted(smi.logical_devices(), key=lambda d: d.hip_id) if d.hip_id >= 0]
+        layout = slices() if slices is not None else {}
+        out: List[tuple] = []
+        for d in sorted(smi.logical_devices(), key=lambda d: d.hip_id):
+            if d.hip_id < 0:
+                continue
+            ss = layout.get(d.gpu_index) if d.compute_mode.lower() == "spx" else None
+            if ss:
+                out.extend((d.hip_id, list(s.cus), s.id, {"gpu": d.gpu_index, "device_id": s.id}) for s in ss)
+            else:
+                out.append((d.hip_id, None, f"gpu{d.gpu_index}.p{d.partition_index}",
+                            {"gpu": d.gpu_index, "device_id": d.device_id}))
+        return out
     return targets
+
+
+def degraded_reason(result: Dict[str, Any], expected_per_cu: Optional[float], fraction: float) -> str:
+    """Why a probe result is degraded ("" = healthy, or nothing to compare against)."""
+    if not expected_per_cu or fraction <= 0 or "bf16_tflops" not in result:
+        return ""
+    per_cu = float(result["bf16_tflops"]) / max(1, int(result.get("n_cus", 1)))
+    if per_cu < fraction * expected_per_cu:
+        return (f"probe: {per_cu:.2f} bf16 TFLOP/s per CU, below {fraction:.0%} of the expected "
+                f"{expected_per_cu:.2f}")
+    return ""
 
 
 #: targets -> {label: result}; the default runs them all in one spawned helper process
@@ -67,8 +97,17 @@ class ProbeRunner:
 
     def __init__(self, shared: SharedState, node_name: str, probe_fn: Optional[ProbeFn] = None,
                  targets: Optional[TargetsFn] = None, asynchronous: bool = True,
-                 round_fn: Optional[RoundFn] = None):
+                 round_fn: Optional[RoundFn] = None, used: Optional[Callable[[], set]] = None,
+                 expected_per_cu: Optional[float] = None, healthy_fraction: float = 0.0,
+                 clock: Callable[[], float] = time.time):
+        """``used``: device ids pods hold now (never probed: their last result is kept; every free
+        target is measured again after each commit); ``expected_per_cu`` / ``healthy_fraction``: the
+        degradation rule (:func:`degraded_reason`)."""
         self.shared, self.node = shared, node_name
+        self.used = used
+        self.expected_per_cu, self.healthy_fraction = expected_per_cu, healthy_fraction
+        self.clock = clock
+        self._cache: Dict[str, Dict[str, Any]] = {}   # label -> last result (with "at", "gpu")
         if probe_fn is None and round_fn is None:
             round_fn = spawned_round(shared.helpers)
         if targets is None:
@@ -93,18 +132,32 @@ class ProbeRunner:
             self._run(seq)
 
     def _run(self, seq: int) -> None:
-        t0 = time.time()
+        t0 = self.clock()
         out: Dict[str, Any] = {}
         try:
-            targets = list(self.targets())
+            every = [t if len(t) > 3 else (*t, {}) for t in self.targets()]
+            try:
+                busy = set(self.used()) if self.used is not None else set()
+            except Exception as e:  # noqa: BLE001 - unknown usage: probe nothing that may be in use
+                log.warning("device usage unavailable, probing only targets never probed: %s", e)
+                busy = None
+            targets = []
+            for dev, cus, label, meta in every:
+                cached = self._cache.get(label)
+                in_use = busy is None or meta.get("device_id") in busy
+                if in_use and cached is not None:
+                    continue                        # keep a used target's last result
+                if in_use and busy is not None:
+                    continue                        # a pod holds it: never probe under a pod
+                targets.append((dev, cus, label, meta))
             batch: Dict[str, Any] = {}
-            if self.round_fn is not None:
+            if self.round_fn is not None and targets:
                 try:
-                    batch = self.round_fn(targets)
+                    batch = self.round_fn([t[:3] for t in targets])
                 except Exception as e:  # noqa: BLE001 - a failed helper is reported, not raised
                     log.warning("probe round failed: %s", e)
-                    batch = {label: {"error": str(e)[:200]} for _, _, label in targets}
-            for dev, cus, label in targets:
+                    batch = {label: {"error": str(e)[:200]} for _, _, label, _ in targets}
+            for dev, cus, label, meta in targets:
                 if self.round_fn is not None:
                     r = batch.get(label, {"error": "no result"})
                 else:
@@ -112,7 +165,15 @@ class ProbeRunner:
                         r = self.probe_fn(dev, cus, label)
                     except Exception as e:  # noqa: BLE001 - one bad partition must not hide the others
                         r = {"error": str(e)[:200]}
+                r = dict(r, at=int(t0))
+                if "gpu" in meta:
+                    r["gpu"] = meta["gpu"]
+                why = degraded_reason(r, self.expected_per_cu, self.healthy_fraction)
+                if why:
+                    r["degraded"] = why
+                    log.warning("%s is degraded: %s", label, why)
                 out[label] = r
+                self._cache[label] = r
                 if "error" in r:
                     log.warning("probe of %s failed: %s", label, r["error"])
                     continue
@@ -124,10 +185,17 @@ class ProbeRunner:
                 if "hbm_gbps" in r:
                     REGISTRY.probe_hbm_gbps.labels(self.node, str(dev), label).set(r["hbm_gbps"])
         finally:
+            live = {t[2] for t in every} if "every" in locals() else set(out)
             with self._lock:
-                self.results = {"commit": seq, "at": int(t0), "slices": out}
+                self._cache = {k: v for k, v in self._cache.items() if k in live}
+                self.results = {"commit": seq, "at": int(t0), "slices": dict(self._cache)}
                 self._running = False
         log.info("probe after commit %d: %s", seq, out)
+
+    def degraded(self) -> Dict[str, str]:
+        """label -> reason, for every live target whose last probe was degraded."""
+        with self._lock:
+            return {k: v["degraded"] for k, v in self._cache.items() if v.get("degraded")}
 
     def annotations(self) -> Dict[str, str]:
         """Reporter extra-annotation hook: kick a probe round if needed, publish the latest."""

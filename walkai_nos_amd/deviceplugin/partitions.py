@@ -139,13 +139,17 @@ class PartitionDevice:
 
 def partition_view(device_map: Any, withheld_gpus: Iterable[int], used_ids: Set[str],
                    lost: Iterable[PartitionDevice] = (), slices: Optional[Mapping[int, List[Any]]] = None,
-                   withheld_slices: Iterable[str] = ()) -> Dict[str, List[PartitionDevice]]:
+                   withheld_slices: Iterable[str] = (), degraded: Optional[Mapping[str, str]] = None
+                   ) -> Dict[str, List[PartitionDevice]]:
     """resource name -> the partitions to advertise, with their health (see the module docstring).
     ``lost``: devices of GPUs that left the map since the last view, kept listed as unhealthy.
     ``slices``: GPU index -> CU-mask slices of the GPUs served sliced (their SPX device is
-    advertised as its slices instead); ``withheld_slices``: slice ids being re-carved away."""
+    advertised as its slices instead); ``withheld_slices``: slice ids being re-carved away;
+    ``degraded``: probe label (``gpu<i>.p<k>`` or a slice id) -> reason, for targets whose last
+    probe fell below their model's expected rate (``controllers/agent/probe.py``)."""
     withheld = frozenset(withheld_gpus)
     held_slices = frozenset(withheld_slices)
+    bad = dict(degraded or {})
     out: Dict[str, List[PartitionDevice]] = defaultdict(list)
     for d in device_map.devices:
         held = d.gpu_index in withheld
@@ -154,15 +158,15 @@ def partition_view(device_map: Any, withheld_gpus: Iterable[int], used_ids: Set[
             for s in ss:
                 r = constant.AMD_RESOURCE_PREFIX + s.profile
                 why = ("gpu re-partitioning (in use, draining)" if s.id in used_ids else "gpu re-partitioning") \
-                    if held else ("slice being re-carved" if s.id in held_slices else "")
+                    if held else ("slice being re-carved" if s.id in held_slices else bad.get(s.id, ""))
                 out[r].append(PartitionDevice(s.id, r, d.gpu_index, serial_of(s.id), d.render_minor, not why, why,
                                               d.bdf.lower(), tuple(s.cus), s.hbm_bytes))
             continue
         r = resource_of(d)
         why = ("gpu re-partitioning (in use, draining)" if d.device_id in used_ids else "gpu re-partitioning") \
-            if held else ""
+            if held else bad.get(f"gpu{d.gpu_index}.p{d.partition_index}", "")
         out[r].append(PartitionDevice(d.device_id, r, d.gpu_index, d.partition_index, d.render_minor,
-                                      not held, why, d.bdf.lower()))
+                                      not why, why, d.bdf.lower()))
     present = {d.id for ds in out.values() for d in ds}
     for d in lost:
         if d.id not in present:
@@ -187,11 +191,13 @@ class PartitionState:
     spec, the reporter's status) and the partitions kubelet has allocated."""
 
     def __init__(self, device_map: Callable[[], Any], annotations: Callable[[], Mapping[str, str]],
-                 used_ids: Callable[[], Set[str]], slices: Optional[Callable[[], Mapping[int, List[Any]]]] = None):
+                 used_ids: Callable[[], Set[str]], slices: Optional[Callable[[], Mapping[int, List[Any]]]] = None,
+                 degraded: Optional[Callable[[], Mapping[str, str]]] = None):
         self._map = device_map
         self._annotations = annotations
         self._used = used_ids
         self._slices = slices
+        self._degraded = degraded
         self._last: Dict[str, PartitionDevice] = {}   # devices of the previous view, by id
         self._lost: Dict[str, PartitionDevice] = {}   # devices of GPUs that left the map
 
@@ -233,7 +239,13 @@ class PartitionState:
             if d.bdf not in bdfs:
                 self._lost[d.id] = d
         self._lost = {i: d for i, d in self._lost.items() if d.bdf not in bdfs}  # back on the bus
-        v = partition_view(m, withheld, used, self._lost.values(), slices, held_slices)
+        bad: Mapping[str, str] = {}
+        if self._degraded is not None:
+            try:
+                bad = self._degraded()
+            except Exception as e:  # noqa: BLE001 - no probe verdict: nothing is withheld for it
+                log.warning("probe results unavailable: %s", e)
+        v = partition_view(m, withheld, used, self._lost.values(), slices, held_slices, bad)
         self._last = {d.id: d for ds in v.values() for d in ds if d.bdf in bdfs}
         return v
 

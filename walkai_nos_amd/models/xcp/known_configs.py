@@ -30,6 +30,9 @@ class GpuModelSpec:
     compute_units: int
     xcds: int
     allowed_geometries: List[Geometry] = field(default_factory=list)
+    #: bf16 MFMA TFLOP/s per CU a healthy GPU of this model delivers in the probe kernel
+    #: (csrc/probe.hip); partitions/slices probing below a fraction of it are withheld (None: no rule)
+    probe_bf16_tflops_per_cu: Optional[float] = None
 
     def geometries_for_nps(self, nps: Optional[str]) -> List[Geometry]:
         if nps is None:
@@ -63,12 +66,13 @@ def normalize_model(model: str) -> str:
     return s
 
 
-# MI355X: 8 XCDs x 32 CUs, 288 GB HBM3E (MI355X_MICROARCH.md "Chip-level parameters").
+# MI355X: 8 XCDs x 32 CUs, 288 GB HBM3E (MI355X_MICROARCH.md "Chip-level parameters"). Probe rate:
+# 1576.5 bf16 TFLOP/s over 256 CUs on the box = 6.16 per CU (profiles/operator_gpu_report_r3.json).
 # Compute-partition availability per NPS mode: NPS1 allows every mode; NPS2 requires at least two
 # partitions; NPS4/NPS8 require at least as many compute partitions as memory partitions.
 _DEFAULT_SPECS: Dict[str, GpuModelSpec] = {
     "MI355X": GpuModelSpec("MI355X", 288, 256, 8, _homogeneous({
-        "nps1": ["spx", "dpx", "qpx", "cpx"], "nps2": ["dpx", "qpx", "cpx"]})),
+        "nps1": ["spx", "dpx", "qpx", "cpx"], "nps2": ["dpx", "qpx", "cpx"]}), 6.16),
     "MI350X": GpuModelSpec("MI350X", 288, 256, 8, _homogeneous({
         "nps1": ["spx", "dpx", "qpx", "cpx"], "nps2": ["dpx", "qpx", "cpx"]})),
     "MI325X": GpuModelSpec("MI325X", 256, 304, 8, _homogeneous({
@@ -167,6 +171,8 @@ def load_known_geometries(data: str) -> Dict[str, GpuModelSpec]:
                 compute_units=int(entry.get("computeUnits", base.compute_units if base else 0)),
                 xcds=int(entry.get("xcds", base.xcds if base else 8)),
                 allowed_geometries=[{str(k): int(v) for k, v in g.items()} for g in geoms],
+                probe_bf16_tflops_per_cu=(float(entry["probeBf16TflopsPerCu"]) if "probeBf16TflopsPerCu" in entry
+                                          else (base.probe_bf16_tflops_per_cu if base else None)),
             )
             out[spec.model] = spec
     validate_specs(out)
@@ -181,5 +187,7 @@ def load_known_geometries_file(path: str) -> Dict[str, GpuModelSpec]:
 def dump_known_geometries(specs: Optional[Mapping[str, GpuModelSpec]] = None) -> str:
     specs = specs if specs is not None else get_known_geometries()
     doc = [{"models": [s.model], "memoryGB": s.memory_gb, "computeUnits": s.compute_units, "xcds": s.xcds,
-            "allowedGeometries": s.allowed_geometries} for s in specs.values()]
+            "allowedGeometries": s.allowed_geometries,
+            **({"probeBf16TflopsPerCu": s.probe_bf16_tflops_per_cu} if s.probe_bf16_tflops_per_cu else {})}
+           for s in specs.values()]
     return yaml.safe_dump(doc, sort_keys=False)

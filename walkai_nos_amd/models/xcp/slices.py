@@ -255,17 +255,22 @@ def place_slices(existing: Sequence[Slice], profiles: Sequence[str], gpu_id: str
         if len(free) < n:
             raise ValueError(f"cannot place a {p} slice: {n} groups needed, {len(free)} free")
         pick: Optional[List[int]] = None
-        best: Optional[Tuple[int, int]] = None
+        best: Optional[Tuple[int, ...]] = None
         for start in range(0, capacity - n + 1, n):
             block = list(range(start, start + n))
             if any(g in taken for g in block):
                 continue
-            parent = 2 * n if 2 * n <= capacity else n
-            pstart = (start // parent) * parent
-            used_in_parent = sum(1 for g in range(pstart, pstart + parent) if g in taken)
-            key = (-used_in_parent, start)
-            if best is None or key < best:
-                best, pick = key, block
+            # buddy best fit: the block whose smallest enclosing blocks are the most used, so the
+            # free space of the emptier halves / quarters stays whole for the bigger slices
+            key = []
+            size = 2 * n
+            while size <= capacity:
+                pstart = (start // size) * size
+                key.append(-sum(1 for g in range(pstart, pstart + size) if g in taken))
+                size *= 2
+            key.append(start)
+            if best is None or tuple(key) < best:
+                best, pick = tuple(key), block
         if pick is None:
             run: List[int] = []
             for g in free:

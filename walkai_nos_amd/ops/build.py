@@ -100,6 +100,8 @@ TARGETS: Sequence[Target] = (
     # the agent's commit-barrier helper as a native program: no interpreter start-up on the flip path
     Target("nos-gpuhelper", ["gpuhelper.cpp", "rccl_barrier.cpp", "p2p_barrier.hip"], "hipcc",
            libs=["rccl", "amdhip64"], executable=True),
+    # the barrier's ring plan (csrc/ring_plan.h) as a host-only library, for its unit tests
+    Target("libnos_ringplan.so", ["ring_plan_capi.cpp"], "g++"),
 )
 
 
