@@ -180,3 +180,63 @@ def test_device_plugin_keeps_a_two_slice_request_on_one_gpu():
     r = plug.Allocate(a, None).container_responses[0]
     assert dict(r.envs)["HSA_CU_MASK"] == "0:0-63"
     assert [x.host_path for x in r.devices] == ["/dev/kfd", "/dev/dri/renderD136"]
+
+
+def test_degraded_probe_withholds_the_partition_and_is_exported():
+    """a partition whose probe falls below its model's expected rate is advertised
+    Unhealthy with the reason, exported in the cluster-info snapshot, and the planner places new
+    work on the other GPU; a target in use is never probed."""
+    import json
+
+    from walkai_nos_amd.api import v1alpha1 as api
+    from walkai_nos_amd.controllers.agent.probe import ProbeRunner, device_map_targets
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    from walkai_nos_amd.controllers.partitioner.pod_controller import plan_cluster_pack
+    from walkai_nos_amd.deviceplugin.partitions import PartitionState
+    from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+    from walkai_nos_amd.exporters.clusterinfo import Collector
+    from walkai_nos_amd.kube.memory import InMemoryAPIServer
+    from walkai_nos_amd.models.xcp import node as xcp_node
+
+    smi = FakeAmdSmi(n_gpus=2)
+    smi.set_compute_partition(1, "CPX")
+    m = smi.device_map()
+    in_use = {m.partitions_of(1)[0].device_id}
+    probed = []
+
+    def probe(dev, cus, label):        # partition 3 of GPU 1 runs at 40% of the expected rate
+        probed.append(label)
+        n = 256 if label.startswith("gpu0") else 32
+        return {"n_cus": n, "bf16_tflops": (0.4 if label == "gpu1.p3" else 1.0) * 6.16 * n}
+    shared = SharedState()
+    r = ProbeRunner(shared, "n0", probe_fn=probe, targets=device_map_targets(smi), asynchronous=False,
+                    used=lambda: in_use, expected_per_cu=6.16, healthy_fraction=0.7)
+    shared.record_commit(True)
+    r.poll()
+    assert "gpu1.p0" not in probed and len(probed) == 8                 # never under a pod
+    assert set(r.degraded()) == {"gpu1.p3"} and "below 70%" in r.degraded()["gpu1.p3"]
+    st = PartitionState(smi.device_map, lambda: {}, lambda: in_use, degraded=r.degraded)
+    v = st.view()
+    cpx = {d.partition_index: d for d in v["amd.com/cpx_nps1"]}
+    assert not cpx[3].healthy and "probe" in cpx[3].reason and all(cpx[k].healthy for k in (0, 1, 2, 4))
+    # exported: the status-probe annotation feeds the snapshot and the node model
+    api_ = InMemoryAPIServer()
+    node = ko.new_node("n0", {api.LABEL_GPU_PARTITIONING: "xcp", "amd.com/gpu.product-name": "AMD_Instinct_MI355X",
+                              "amd.com/gpu.count": "2"})
+    node["metadata"]["annotations"] = {api.ANNOTATION_PROBE_RESULT: json.dumps(r.results),
+                                       "nos.nebuly.com/status-gpu-0-spx_nps1-free": "1",
+                                       "nos.nebuly.com/status-gpu-1-cpx_nps1-used": "1",
+                                       "nos.nebuly.com/status-gpu-1-cpx_nps1-free": "7"}
+    api_.create(node)
+    snap = Collector(api_).collect()
+    bad = [p for p in snap.probes if p.degraded]
+    assert [p.target for p in bad] == ["gpu1.p3"] and bad[0].gpu == 1
+    assert snap.utilization["degraded_targets"] == 1.0 and snap.utilization["probed_bf16_tflops"] > 1500
+    model = xcp_node.new_node(node)
+    assert model.gpus[1].degraded and not model.gpus[0].degraded
+    # planner: two idle GPUs, one degraded -> the healthy one is flipped for the waiting pods
+    for g in model.gpus:
+        g.used, g.free = {}, {"spx_nps1": 1}
+    changed = plan_cluster_pack({"n0": model}, [({"cpx_nps1": 1}, 700.0)] * 6)
+    flipped = [g.index for g in changed["n0"].gpus if g.geometry() != {"spx_nps1": 1}]
+    assert flipped == [0]

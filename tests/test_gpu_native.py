@@ -135,6 +135,33 @@ def test_probe_on_commit_with_real_kernels(gpu):
     assert 3 < whole["bf16_tflops"] / cpx["bf16_tflops"] < 12
 
 
+def test_real_probe_results_drive_partition_health(gpu):
+    """VERDICT r3 #5 on hardware: real probe results through the health rule. Against the MI355X's
+    expected rate (known_configs) a healthy whole GPU and a 32-CU slice pass; against an inflated
+    expectation the same measurements are withheld by the partition plugin with the reason."""
+    from walkai_nos_amd.controllers.agent.probe import ProbeRunner, hip_probe
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+    from walkai_nos_amd.deviceplugin.partitions import PartitionState
+    from walkai_nos_amd.models.xcp.known_configs import get_model_spec
+    expected = get_model_spec("MI355X").probe_bf16_tflops_per_cu
+    targets = lambda: [(0, None, "gpu0.p0"), (0, list(range(32)), "gpu1.p0")]  # noqa: E731
+    s = SharedState()
+    ok = ProbeRunner(s, "box", probe_fn=hip_probe, targets=targets, asynchronous=False, expected_per_cu=expected,
+                     healthy_fraction=0.7)
+    ok.poll()
+    per_cu = {k: v["bf16_tflops"] / v["n_cus"] for k, v in ok.results["slices"].items()}
+    assert ok.degraded() == {}, per_cu
+    bad = ProbeRunner(s, "box", probe_fn=hip_probe, targets=targets, asynchronous=False,
+                      expected_per_cu=4 * expected, healthy_fraction=0.7)
+    bad.poll()
+    assert set(bad.degraded()) == {"gpu0.p0", "gpu1.p0"}
+    smi = FakeAmdSmi(n_gpus=2)
+    v = PartitionState(smi.device_map, lambda: {}, lambda: set(), degraded=bad.degraded).view()
+    assert [d.healthy for d in v["amd.com/spx_nps1"]] == [False, False]
+    assert "bf16 TFLOP/s per CU" in v["amd.com/spx_nps1"][0].reason
+
+
 def test_torch_barrier_vote_does_not_wait_for_cu_masked_work(gpu):
     # the bench's multi-GPU commit vote (RCCL all-reduce, here a 1-rank communicator) must not queue
     # behind inference work on the partitions' CU-masked streams (which are blocking streams: an op

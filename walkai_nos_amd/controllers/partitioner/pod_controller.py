@@ -388,7 +388,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
     spx_gpus = [(n, g) for n in sorted(hw_nodes) for g in current[n].gpus if (_mode_of(g) or "").startswith("spx")]
     reserve = min(len(spx_gpus), int(round(spx_demand))) if (params.spx_reserve and total_gpus > 1) else 0
     # idle GPUs whose mode nobody is waiting for go first; SPX GPUs last (they are the reserve)
-    idle.sort(key=lambda ng: ((_mode_of(ng[1]) or "").startswith("spx"), ng[0], ng[1].index))
+    idle.sort(key=lambda ng: (bool(ng[1].degraded), (_mode_of(ng[1]) or "").startswith("spx"), ng[0], ng[1].index))
     spx_kept = sum(1 for n, g in spx_gpus if not g.is_idle())
     for name, g in idle:
         if not demand:

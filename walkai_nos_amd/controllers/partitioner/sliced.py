@@ -102,9 +102,11 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         need = q * groups_of(p)
         if need > 8:
             continue
-        cands = [(g.room(), name, g.index, g) for name, g in sliced if g.target is None and g.room() >= need]
+        cands = [(bool(g.degraded), g.room(), name, g.index, g) for name, g in sliced
+                 if g.target is None and g.room() >= need]
         if cands:
-            _, name, _, g = min(cands, key=lambda c: c[:3])
+            *_, g = min(cands, key=lambda c: c[:4])
+            name = next(n for n, x in sliced if x is g)
             for _ in range(q):
                 g.claim(p)
             claimed.add((name, g.index))
@@ -112,7 +114,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
             continue
         if reserved or params.slice_reserve_after <= 0 or age < params.slice_reserve_after:
             continue
-        victims = [(g.used_groups(), name, g.index, g) for name, g in sliced
+        victims = [(bool(g.degraded), g.used_groups(), name, g.index, g) for name, g in sliced
                    if g.target is None and (name, g.index) not in claimed]
         if not victims and any(g.target is None for _, g in sliced):
             continue  # every sliced GPU just took an older pod: reconsider on the next pass
@@ -127,7 +129,8 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
                 g.target, g.target_sliced = {p: q}, True
                 reserved = True
             continue
-        _, name, _, g = min(victims, key=lambda c: c[:3])
+        *_, g = min(victims, key=lambda c: c[:4])
+        name = next(n for n, x in sliced if x is g)
         want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
         want[p] = want.get(p, 0) + q
         g.used = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}

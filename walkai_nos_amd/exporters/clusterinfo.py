@@ -12,7 +12,10 @@ capped at capacity.  Pod summaries: only pods requesting partitions/slices, sort
 (namespace, name); status = first container waiting/terminated reason, then "Running", then the
 phase; finish time = latest container ``finishedAt`` once Succeeded/Failed; profiles rendered as
 ``"cpx_nps1 x2, spx_nps1"``.  MI355X additions: every snapshot also carries the node-level
-utilisation and pod density (the north-star metrics).
+utilisation and pod density (the north-star metrics), and ``probes``: what every partition or
+CU-mask slice measured in the agent's probe-on-commit (``status-probe``) — bf16/fp32 TFLOP/s,
+TFLOP/s per CU, HBM GB/s and, for one below its model's expected rate, why it is withheld — so the
+inventory says what the capacity can actually deliver, not only how much of it is allocated.
 """
 from __future__ import annotations
 
@@ -62,11 +65,25 @@ class PodSummary:
 
 
 @dataclass
+class ProbeSummary:
+    node: str
+    target: str                    # "gpu<i>.p<k>" (a partition) or a slice id
+    gpu: Optional[int]
+    n_cus: int
+    bf16_tflops: Optional[float]
+    fp32_tflops: Optional[float]
+    bf16_tflops_per_cu: Optional[float]
+    hbm_gbps: Optional[float]
+    degraded: str = ""
+
+
+@dataclass
 class Snapshot:
     ts: str
     gpus: List[GPUInventory] = field(default_factory=list)
     pods: List[PodSummary] = field(default_factory=list)
     utilization: Dict[str, float] = field(default_factory=dict)
+    probes: List[ProbeSummary] = field(default_factory=list)
 
     def to_json(self) -> str:
         return json.dumps(asdict(self), sort_keys=False)
@@ -173,6 +190,31 @@ def utilization(inventory: List[GPUInventory], nodes: List[Dict[str, Any]]) -> D
             "fractional_pods_per_node": round(pods / n_nodes, 3)}
 
 
+def probe_summaries(nodes: List[Dict[str, Any]]) -> List[ProbeSummary]:
+    from ..api import v1alpha1 as api
+    out: List[ProbeSummary] = []
+    for n in nodes:
+        try:
+            doc = json.loads(ko.annotations(n).get(api.ANNOTATION_PROBE_RESULT) or "{}")
+        except ValueError:
+            continue
+        for label, r in sorted((doc.get("slices") or {}).items()):
+            if not isinstance(r, dict) or "error" in r:
+                continue
+            cus = int(r.get("n_cus", 0) or 0)
+            bf = r.get("bf16_tflops")
+            out.append(ProbeSummary(ko.name(n), label, r.get("gpu"), cus, bf, r.get("fp32_tflops"),
+                                    round(bf / cus, 3) if bf is not None and cus else None, r.get("hbm_gbps"),
+                                    str(r.get("degraded") or "")))
+    return out
+
+
+def probe_totals(probes: List[ProbeSummary]) -> Dict[str, float]:
+    healthy = [p for p in probes if not p.degraded and p.bf16_tflops is not None]
+    return {"probed_bf16_tflops": round(sum(p.bf16_tflops for p in healthy), 1),
+            "degraded_targets": float(sum(1 for p in probes if p.degraded))}
+
+
 class Collector:
     def __init__(self, client: Any, clock: Callable[[], float] = time.time):
         self.client = client
@@ -182,7 +224,11 @@ class Collector:
         nodes = self.client.list("Node")
         pods = self.client.list("Pod")
         inv = inventory_from_annotations(nodes) or inventory_from_capacity(nodes, pods)
-        return Snapshot(ko.now_rfc3339(self.clock()), inv, pod_summaries(pods), utilization(inv, nodes))
+        probes = probe_summaries(nodes)
+        util = utilization(inv, nodes)
+        if probes:
+            util.update(probe_totals(probes))
+        return Snapshot(ko.now_rfc3339(self.clock()), inv, pod_summaries(pods), util, probes)
 
 
 class Exporter:

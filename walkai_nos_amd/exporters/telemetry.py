@@ -26,6 +26,24 @@ class NodeMetrics:
     capacity: Dict[str, Any] = field(default_factory=dict)
     labels: Dict[str, str] = field(default_factory=dict)
     nodeInfo: Dict[str, Any] = field(default_factory=dict)
+    #: MI355X: the node's probe-on-commit summary (bf16 TFLOP/s per CU of each partition or slice,
+    #: degraded targets) from the agent's ``status-probe`` annotation
+    probe: Dict[str, Any] = field(default_factory=dict)
+
+
+def probe_digest(raw: Any) -> Dict[str, Any]:
+    """``status-probe`` JSON -> {targets, bf16_tflops, bf16_tflops_per_cu (min/max), degraded}."""
+    try:
+        doc = json.loads(raw) if isinstance(raw, str) else (raw or {})
+    except ValueError:
+        return {}
+    rows = [r for r in (doc.get("slices") or {}).values() if isinstance(r, dict) and "bf16_tflops" in r]
+    if not rows:
+        return {}
+    per_cu = [r["bf16_tflops"] / max(1, int(r.get("n_cus", 1))) for r in rows]
+    return {"targets": len(rows), "bf16_tflops": round(sum(r["bf16_tflops"] for r in rows), 1),
+            "bf16_tflops_per_cu_min": round(min(per_cu), 3), "bf16_tflops_per_cu_max": round(max(per_cu), 3),
+            "degraded": sorted(str(r["degraded"]) for r in rows if r.get("degraded"))}
 
 
 @dataclass
@@ -45,8 +63,12 @@ class Metrics:
     @staticmethod
     def from_yaml(text: str) -> "Metrics":
         doc = yaml.safe_load(text) or {}
-        nodes = [NodeMetrics(**{k: v for k, v in (n or {}).items() if k in NodeMetrics.__dataclass_fields__})
-                 for n in doc.get("nodes") or []]
+        nodes = []
+        for n in doc.get("nodes") or []:
+            n = dict(n or {})
+            if "probe" in n:
+                n["probe"] = probe_digest(n["probe"])
+            nodes.append(NodeMetrics(**{k: v for k, v in n.items() if k in NodeMetrics.__dataclass_fields__}))
         comps = Components(**{k: bool(v) for k, v in (doc.get("components") or {}).items()
                               if k in Components.__dataclass_fields__})
         return Metrics(str(doc.get("installationUUID", "")), nodes, doc.get("chartValues"), comps)

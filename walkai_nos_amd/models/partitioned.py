@@ -38,6 +38,9 @@ class PartitionedGPU:
     target: Optional[Dict[str, int]] = None
     #: the drain target is a sliced layout (SPX + CU-mask slices, ``models/xcp/slices.py``)
     target_sliced: bool = False
+    #: why the agent's probe found a partition/slice of this GPU below its model's expected rate
+    #: ("" = healthy or not probed): the planner places new work on other GPUs first
+    degraded: str = ""
 
     #: served as CU-mask slices of an SPX GPU (``SlicedGPU``) rather than hardware partitions
     sliced = False
@@ -45,7 +48,7 @@ class PartitionedGPU:
     def clone(self) -> "PartitionedGPU":
         return PartitionedGPU(self.model, self.index, [dict(g) for g in self.allowed_geometries],
                               dict(self.used), dict(self.free), dict(self.target) if self.target else None,
-                              self.target_sliced)
+                              self.target_sliced, self.degraded)
 
     def spec_geometry(self) -> Geometry:
         """What the spec should say for this GPU: the drain target, else the geometry."""

@@ -45,6 +45,20 @@ def get_layout(node: Dict[str, Any]) -> str:
     return v
 
 
+def degraded_gpus(annotations: Mapping[str, str]) -> Dict[int, str]:
+    """GPU index -> the first degraded probe reason of the agent's ``status-probe`` annotation."""
+    import json
+    try:
+        doc = json.loads(annotations.get(api.ANNOTATION_PROBE_RESULT) or "{}")
+    except ValueError:
+        return {}
+    out: Dict[int, str] = {}
+    for label, r in sorted((doc.get("slices") or {}).items()):
+        if isinstance(r, dict) and r.get("degraded") and isinstance(r.get("gpu"), int):
+            out.setdefault(r["gpu"], f"{label}: {r['degraded']}")
+    return out
+
+
 def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode:
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
@@ -85,6 +99,9 @@ def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode
             want = {p: q for p, q in spec_by_gpu.get(idx, {}).items() if q > 0}
             if want and g.target is None and want != g.geometry():
                 g.target = want
+    for idx, why in degraded_gpus(anns).items():
+        if idx in gpus:
+            gpus[idx].degraded = why
     allocatable = res.from_k8s(ko.node_allocatable(node))
     return PartitionedNode(ko.name(node), [gpus[i] for i in sorted(gpus)], allocatable,
                            is_resource=is_xcp_resource, as_resource=as_resource_name, weight=SCORING[scoring],

@@ -88,7 +88,7 @@ class SlicedGPU(PartitionedGPU):
     def clone(self) -> "SlicedGPU":
         return SlicedGPU(self.model, self.index, [dict(g) for g in self.allowed_geometries], dict(self.used),
                          dict(self.free), dict(self.target) if self.target else None, self.target_sliced,
-                         self.capacity)
+                         self.degraded, self.capacity)
 
     # -- capacity ----------------------------------------------------------------------------
     def used_groups(self) -> int:
