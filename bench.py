@@ -53,6 +53,9 @@ def main() -> int:
     ap.add_argument("--no-density", action="store_true", help="skip the saturation/density phase")
     ap.add_argument("--emulation", default=None, choices=("pinned", "spread", "landing"),
                     help="compute-partition emulation on the SPX device (default: spread; bench_core.EMULATION)")
+    ap.add_argument("--erq", action="store_true",
+                    help="Elastic Resource Quota mode (BASELINE config 5): two quota'd namespaces borrow and "
+                         "reclaim on the real data plane; prints its own JSON line (walkai_nos_amd/bench_erq.py)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -82,7 +85,16 @@ def main() -> int:
                       device_plugin=args.device_plugin, layout=args.layout)
     if args.emulation:
         cfg.emulation = args.emulation
-    res = run_bench(cfg)
+    if args.erq:
+        from walkai_nos_amd.bench_core import DataPlane
+        from walkai_nos_amd.bench_erq import run_erq
+        data = DataPlane(cfg)
+        try:
+            res = run_erq(cfg, data)
+        finally:
+            data.close()
+    else:
+        res = run_bench(cfg)
     if rank == 0:
         line = json.dumps(res)
         print(line, flush=True)

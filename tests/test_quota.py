@@ -308,3 +308,19 @@ def test_preemption_waits_for_terminating_victims():
     s.reconcile(NosScheduler.KEY)
     assert all(ko.pod_node_name(mem.get("Pod", f"b{i}", "team-b")) == "n0" for i in range(2))
     assert api.deletes == 2
+
+
+def test_erq_bench_mode_reclaims_on_a_sliced_gpu_without_a_flip():
+    """VERDICT r3 #7 (control path of ``bench.py --erq``): team A borrows team B's half of a sliced
+    GPU with 1/8 pods; B's 1/2 pod reclaims it through 4 evictions of A's over-quota pods and a
+    re-carve — no mode flip — within the first reclaim quantum. On hardware partitions the same GPU
+    cannot be reclaimed without taking A's guaranteed pods, so B waits (the case slices fix)."""
+    from walkai_nos_amd.bench_core import BenchConfig
+    from walkai_nos_amd.bench_erq import run_erq
+    r = run_erq(BenchConfig(gpus=1, layout="slices"))
+    assert r["team_a_borrowed_gb"] == 144 and r["preemptions"] == 4 and r["team_b_bound"]
+    assert r["reclaim_quanta"] == 1 and r["flips"] == 0 and r["reclaim_latency_s"]["max"] <= 60
+    last = r["samples"][-1]
+    assert last["used_gb"] == {"team-a": 144, "team-b": 144} and last["running"] == {"team-a": 4, "team-b": 1}
+    p = run_erq(BenchConfig(gpus=1, layout="partitions"), max_reclaim_quanta=3, after_quanta=1)
+    assert not p["team_b_bound"] and p["preemptions"] == 0

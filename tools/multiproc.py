@@ -53,6 +53,7 @@ def main() -> int:
     ap.add_argument("--out", default="gpurun_out/multiproc.json")
     ap.add_argument("--env", default="{}", help="extra env for every pod, JSON (e.g. {\"NOS_POD_STREAMS\": \"4\"})")
     ap.add_argument("--tag", default="", help="suffix of the scenario names in the output")
+    ap.add_argument("--stagger", type=float, default=0.0, help="seconds between pod starts")
     args = ap.parse_args()
     extra = json.loads(args.env)
     todo = scenarios()
@@ -66,10 +67,12 @@ def main() -> int:
     for name, (profiles, shim) in todo.items():
         t0 = time.time()
         dedicated = all("cu." in p for p in profiles)
-        r = run_pods(profiles, seconds=args.seconds, shim=shim, census=dedicated, extra_env=extra)
+        r = run_pods(profiles, seconds=args.seconds, shim=shim, census=dedicated, extra_env=extra,
+                     stagger_s=args.stagger)
         r["profiles"] = profiles
         r["shim"] = shim
         r["env"] = extra
+        r["stagger_s"] = args.stagger
         r["wall_s"] = round(time.time() - t0, 1)
         rates = [p["inf_per_s"] for p in r["per_pod"]]
         r["per_pod_max_over_min"] = round(max(rates) / max(1e-9, min(rates)), 3) if rates else None

@@ -704,32 +704,8 @@ class NodeBench:
                 del self.outage[g]
 
     def my_pods(self) -> List[Tuple[Any, ...]]:
-        """Data-plane keys of the pods served on this rank's GPU this quantum: (profile, partition
-        index) of a partition, and of a CU-mask slice whose row groups are that partition's CU set
-        (slices are placed buddy-aligned, so they usually are); ("slice", profile, groups) of any
-        other slice."""
-        out: List[Tuple[Any, ...]] = []
-        slices = {s.id: s for ss in (self.sn.xcp_slices.load() if self.sn.xcp_slices is not None else {}).values()
-                  for s in ss}
-        for devs in self.sn.kubelet.allocations.values():
-            for r, dev_id in devs:
-                prof = extract_profile_name(r)
-                if prof is None:
-                    continue
-                d = self.sn.smi.resolve(dev_id)
-                if d.gpu_index != self.cfg.rank:
-                    continue
-                s = slices.get(dev_id)
-                if s is None:
-                    out.append((prof, d.partition_index))
-                    continue
-                groups = slice_groups(s)
-                n = len(groups)
-                if groups == list(range(groups[0], groups[0] + n)) and groups[0] % n == 0:
-                    out.append((prof, groups[0] // n))
-                else:
-                    out.append(("slice", prof, tuple(groups)))
-        return out
+        """Data-plane keys of the pods served on this rank's GPU this quantum (:func:`pod_keys`)."""
+        return list(pod_keys(self.sn, self.cfg.rank).values())
 
     def step(self, deadline: Optional[float] = None) -> int:
         """One quantum: control plane, then the dark part of the quantum idle (a flip in progress),
@@ -793,6 +769,34 @@ class NodeBench:
     def close(self) -> None:
         if self.data is not None:
             self.data.close()
+
+
+def pod_keys(sn: Any, gpu: int) -> Dict[Tuple[str, str], Tuple[Any, ...]]:
+    """(namespace, pod) -> data-plane key of every pod on GPU ``gpu`` of simulated node ``sn``:
+    (profile, partition index) of a partition, and of a CU-mask slice whose row groups are that
+    partition's CU set (slices are placed buddy-aligned, so they usually are); ("slice", profile,
+    groups) of any other slice."""
+    out: Dict[Tuple[str, str], Tuple[Any, ...]] = {}
+    slices = {s.id: s for ss in (sn.xcp_slices.load() if sn.xcp_slices is not None else {}).values() for s in ss}
+    for pod, devs in sn.kubelet.allocations.items():
+        for r, dev_id in devs:
+            prof = extract_profile_name(r)
+            if prof is None:
+                continue
+            d = sn.smi.resolve(dev_id)
+            if d.gpu_index != gpu:
+                continue
+            s = slices.get(dev_id)
+            if s is None:
+                out[pod] = (prof, d.partition_index)
+                continue
+            groups = slice_groups(s)
+            n = len(groups)
+            if groups == list(range(groups[0], groups[0] + n)) and groups[0] % n == 0:
+                out[pod] = (prof, groups[0] // n)
+            else:
+                out[pod] = ("slice", prof, tuple(groups))
+    return out
 
 
 # -- density --------------------------------------------------------------------------------

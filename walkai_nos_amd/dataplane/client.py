@@ -72,6 +72,13 @@ def main(argv=None) -> int:
     model = YolosSmall().to(dev).eval()
     x = demo_input(1, hw, dev, seed=int(os.environ.get("NOS_POD_SEED", "0")))
     streams = [torch.cuda.Stream() for _ in range(max(1, args.streams))]
+    if os.environ.get("NOS_POD_EAGER_QUEUES", "0") == "1":
+        # touch every stream back to back before anything else: HIP creates the process's hardware
+        # queues at first use, so they are created together (consecutive queues of one process)
+        for st in streams:
+            with torch.cuda.stream(st):
+                torch.zeros(1, device=dev).add_(1)
+        torch.cuda.synchronize()
     stream = streams[0]
     with torch.no_grad(), torch.cuda.stream(stream):
         for _ in range(2):

@@ -71,8 +71,9 @@ def allocate_envs(profiles: Sequence[str], cu_count: int = 256, shim: bool = Tru
 
 def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, census: bool = False,
              graphs: bool = True, ready_timeout: float = 600.0, extra_env: Optional[Dict[str, str]] = None,
-             cu_count: int = 256) -> Dict[str, Any]:
-    """Start one process per profile, release them together, collect their JSON lines."""
+             cu_count: int = 256, stagger_s: float = 0.0) -> Dict[str, Any]:
+    """Start one process per profile, release them together, collect their JSON lines.
+    ``stagger_s``: wait this long between pod starts (pods of a node start at different times)."""
     envs = allocate_envs(profiles, cu_count, shim)
     pods: List[PodProc] = []
     base = dict(os.environ)
@@ -93,6 +94,8 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
             p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                  stderr=log, text=True)
             pods.append(PodProc(PodSpec(prof, f"pod{i}"), env.get("NOS_SLICE_IDS", ""), env, p))
+            if stagger_s > 0:
+                time.sleep(stagger_s)
 
         def tail(i: int) -> str:
             logs[i].seek(0)

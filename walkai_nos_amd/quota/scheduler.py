@@ -24,6 +24,10 @@ with the same extension points:
   ``min``, preferring one the partitioner is already draining for that profile, then the fewest
   victims — and marks the pod ``quota-reclaim``; the partitioner flips the now idle GPU as for
   any pending pod;
+* **PostFilter, sliced GPUs** (MI355X, ``models/xcp/slices.py``) — a sliced GPU frees a slice for a
+  new profile by re-carving, not by a flip: the scheduler evicts only as many evictable pods of one
+  sliced GPU as free the row groups the reclaiming pod's slice needs (fewest victims, cheapest
+  first), marks it ``quota-reclaim``, and the partitioner re-carves the freed groups for it;
 * **Reserve** — the pod's request is added to its quota's ``used`` for the rest of the cycle.
   A pod that preemption was done for (nominated, or ``quota-reclaim``) holds its request against
   its quota while it waits, so borrowers cannot take the freed capacity back in the meantime.
@@ -172,6 +176,56 @@ class CapacityScheduling:
             return None   # a different NPS is a whole-node switch: the partitioner's alone
         status, spec = parse_node_annotations(anns)
         return profile, anns, status, spec
+
+    @staticmethod
+    def _sliced_room(anns: Dict[str, str], status: List[Any]) -> Dict[int, int]:
+        """Sliced GPU -> row groups not in use (free slices can be re-carved)."""
+        from ..models.xcp.slices import GROUPS, groups_of, parse_gpu_set
+        out = {g: GROUPS for g in parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_STATUS))}
+        for a in status:
+            if a.index in out and a.is_used():
+                out[a.index] -= groups_of(a.profile) * a.quantity
+        return out
+
+    def slice_victims(self, state: CycleState, pod: Dict[str, Any], node: str
+                      ) -> Optional[Tuple[Tuple[int, int], int, List[Dict[str, Any]]]]:
+        """The fewest evictable pods of one sliced GPU of ``node`` whose slices, with the groups
+        already free, make room for the pod's slice: ``(rank, gpu index, victims)``, or None."""
+        from ..models.xcp.slices import groups_of, is_slice_profile
+        view = self._xcp_view(state, pod, node)
+        if view is None or not is_slice_profile(view[0]):
+            return None
+        profile, anns, status, _ = view
+        need = groups_of(profile)
+        room = self._sliced_room(anns, status)
+        try:
+            pods_by_gpu = json.loads(anns.get(api.ANNOTATION_GPU_PODS_STATUS) or "{}")
+        except ValueError:
+            return None
+        cands = self.candidates(state, pod, node)
+        best = None
+        for g, free in sorted(room.items()):
+            if free >= need:
+                return None                    # room already: the partitioner re-carves it, no eviction
+            on_gpu = set(pods_by_gpu.get(str(g), []))
+            victims: List[Dict[str, Any]] = []
+            got = free
+            for v in cands:
+                if got >= need:
+                    break
+                if _pkey(v) not in on_gpu:
+                    continue
+                vp = next((extract_profile_name(r) for r in res.compute_pod_request(v) if is_xcp_resource(r)), None)
+                if vp is None or not is_slice_profile(vp):
+                    continue
+                victims.append(v)
+                got += groups_of(vp)
+            if got < need or not victims or not self._evictable_together(state, pod, victims):
+                continue
+            rank = (len(victims), g)
+            if best is None or rank < best[0]:
+                best = (rank, g, victims)
+        return best
 
     def gpu_available(self, state: CycleState, pod: Dict[str, Any], node: str) -> bool:
         """``node`` has a GPU already in the pod's profile, or an idle one the partitioner can flip."""
@@ -399,6 +453,18 @@ class NosScheduler:
         nodes = [n for n in sorted(state.nodes) if allowed is None or n in allowed]
         if not xcp or any(res.from_k8s(ko.node_allocatable(state.nodes[n])).get(r, 0) > 0 for n in nodes for r in xcp):
             return False   # some node offers the profile: ordinary preemption's case
+        sliced = None
+        for node in nodes:
+            cand = self.plugin.slice_victims(state, pod, node)
+            if cand is not None and (sliced is None or cand[0] < sliced[1][0]):
+                sliced = (node, cand)
+        if sliced is not None:
+            node, (_, gpu, victims) = sliced
+            log.info("freeing %d pod(s) of sliced GPU %d of %s for %s/%s", len(victims), gpu, node,
+                     ko.namespace(pod), ko.name(pod))
+            self._evict(state, pod, node, victims)
+            self._mark_reclaim(pod, node)
+            return True
         if any(self.plugin.gpu_available(state, pod, n) for n in nodes):
             return False   # an idle GPU (or one already flipped) will serve it without evictions
         best = None
@@ -411,12 +477,15 @@ class NosScheduler:
         node, (_, gpu, victims) = best
         log.info("freeing GPU %d of %s for %s/%s (%d pods)", gpu, node, ko.namespace(pod), ko.name(pod), len(victims))
         self._evict(state, pod, node, victims)
+        self._mark_reclaim(pod, node)
+        return True
+
+    def _mark_reclaim(self, pod: Dict[str, Any], node: str) -> None:
         try:
             self.client.patch("Pod", ko.name(pod), {"metadata": {"annotations": {api.ANNOTATION_QUOTA_RECLAIM: node}}},
                               ko.namespace(pod))
         except NotFound:
             pass
-        return True
 
     def _victims_terminating(self, state: CycleState, pod: Dict[str, Any]) -> bool:
         mine = self._victims_of.get(_pkey(pod))
