@@ -426,6 +426,7 @@ class DataPlane:
         torch.cuda.synchronize()
         self._layout: frozenset = frozenset()
         self.drains = 0
+        self._mask_streams: Dict[Tuple[int, ...], Tuple[Any, Any]] = {}  # row groups -> CU-masked stream
 
     def add_slots(self, slots: Dict[Any, List[int]]) -> None:
         import torch
@@ -446,18 +447,18 @@ class DataPlane:
         A different set of compute modes than in the last quantum means the GPU was re-partitioned:
         every queued inference of the old layout finishes first (the agent only flips an idle GPU),
         so slots of two layouts never overlap."""
-        missing = {k: [32 * g + i for g in k[2] for i in range(32)] for k in keys if k not in self.slots}
-        if missing:
-            self.add_slots(missing)  # an unaligned CU-mask slice: its own replica (warmed in the window)
+        remap: Dict[Any, Tuple[Any, Any]] = {}
+        if any(k not in self.slots for k in keys):
+            remap = self._unaligned(keys)
         layout = frozenset(k[0] for k in keys)
         if layout != self._layout:
             if any(s.in_flight for s in self.slots.values()):
                 self.drains += 1
             self.drain_all()
             self._layout = layout
-        active = [(k, self.slots[k]) for k in keys]
+        active = [(k, self.slots[remap[k][0]] if k in remap else self.slots[k]) for k in keys]
         if self.cfg.depth <= 1 and active:
-            return self._serve_loops(active, deadline)
+            return self._serve_loops(active, deadline, {k: v[1] for k, v in remap.items()})
         n: Dict[Any, int] = {k: 0 for k in keys}
         while True:
             now = time.perf_counter()
@@ -477,7 +478,34 @@ class DataPlane:
                 time.sleep(0.0002)
         return n
 
-    def _serve_loops(self, active: List[Tuple[Any, "Slot"]], deadline: float) -> Dict[Any, int]:
+    def _unaligned(self, keys: List[Any]) -> Dict[Any, Tuple[Any, Any]]:
+        """A CU-mask slice on row groups no pre-warmed slot covers (("slice", profile, groups)):
+        served by an idle slot of its profile — same CU count, so the same captured graph — replayed
+        on a stream masked to the slice's own CUs (a HIP graph runs on the stream it is replayed on,
+        profiles/graph_cu_mask_probe_r3.json). At most ``partitions`` slices of a profile exist at
+        once, so a slot is always free; only a stream is created, never a replica in the window."""
+        from .ops.probe import Stream
+        taken = {k for k in keys if k in self.slots}
+        out: Dict[Any, Tuple[Any, Any]] = {}
+        for k in keys:
+            if k in self.slots:
+                continue
+            prof, groups = k[1], k[2]
+            slot = next((sk for sk in sorted(self.slots, key=str) if sk[0] == prof and sk not in taken
+                         and len(self.slots[sk].lanes) == 1), None)
+            if slot is None:  # more slices of a profile than its partitions: a replica of its own
+                self.add_slots({k: [32 * g + i for g in groups for i in range(32)]})
+                taken.add(k)
+                continue
+            taken.add(slot)
+            if groups not in self._mask_streams:
+                st = Stream(self.device, [32 * g + i for g in groups for i in range(32)])
+                self._mask_streams[groups] = (st, st.torch_stream())
+            out[k] = (slot, self._mask_streams[groups][1])
+        return out
+
+    def _serve_loops(self, active: List[Tuple[Any, "Slot"]], deadline: float,
+                     streams: Optional[Dict[Any, Any]] = None) -> Dict[Any, int]:
         """The reference demo's loop (``client/main.py:23-25``), one per pod lane, each on its own
         thread: start one inference, wait for it (a blocking event wait, the GIL released), record
         its GPU time, start the next — until ``deadline``. A polling loop over every pod would leave
@@ -492,16 +520,17 @@ class DataPlane:
             K.set_slice_cus(lane.n_cus)
             K.set_slice_pin(slot.pin)
             done = 0
-            with torch.no_grad(), torch.cuda.stream(lane.stream):
+            stream = (streams or {}).get(key) or lane.stream
+            with torch.no_grad(), torch.cuda.stream(stream):
                 while time.perf_counter() < deadline:
                     st = torch.cuda.Event(enable_timing=True)
-                    st.record(lane.stream)
+                    st.record(stream)
                     if lane.graph is not None:
                         lane.graph.replay()
                     else:
                         lane.out = slot.model(lane.x)
                     ev = torch.cuda.Event(enable_timing=True)
-                    ev.record(lane.stream)
+                    ev.record(stream)
                     ev.synchronize()
                     slot.latency_ms.append(st.elapsed_time(ev))
                     done += 1
@@ -532,6 +561,9 @@ class DataPlane:
         for s in self.slots.values():
             s.close()
         self.slots.clear()
+        for st, _ in self._mask_streams.values():
+            st.close()
+        self._mask_streams.clear()
         gc.collect()
 
 

@@ -181,6 +181,8 @@ class PackParams:
                                     # single GPU cycle through the modes its pods ask for
     slice_reserve_after: float = 900.0  # seconds: sliced GPUs (xcp-layout slices/auto) — the oldest pod that
                                     # fits on no sliced GPU this long drains one for itself (0 = never)
+    slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
+    slice_reserve_stretch: float = 2.0  # ... at most this many times
     slice_fill: bool = True         # carve a sliced GPU's leftover groups into cpx slices
 
 

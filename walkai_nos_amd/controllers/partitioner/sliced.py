@@ -91,7 +91,14 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     for _, g in sliced:
         if g.target is not None and g.target_sliced:
             g.target = None
-    # 2./3. backfill and reservation, oldest first
+    # 2./3. backfill and reservation, oldest first. Under overload the threshold stretches with the
+    # backlog (GPUs of waiting work per sliced GPU): every drain idles groups, and when the queue is
+    # long anyway, batching whole-GPU pods less often serves more and shortens the waits behind them
+    backlog = sum(groups_of(s[0]) * s[1] / 8.0 for s in (_single(r) for r, _ in unserved)
+                  if s is not None and is_slice_profile(s[0])) / max(1, len(sliced))
+    reserve_after = params.slice_reserve_after
+    if params.slice_reserve_backlog > 0:
+        reserve_after *= min(params.slice_reserve_stretch, max(1.0, backlog / params.slice_reserve_backlog))
     reserved = False
     claimed = set()   # GPUs that took a pod in this pass: never drained for a younger one
     for req, age in list(unserved):
@@ -112,7 +119,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
             claimed.add((name, g.index))
             unserved.remove((req, age))
             continue
-        if reserved or params.slice_reserve_after <= 0 or age < params.slice_reserve_after:
+        if reserved or params.slice_reserve_after <= 0 or age < reserve_after:
             continue
         victims = [(bool(g.degraded), g.used_groups(), name, g.index, g) for name, g in sliced
                    if g.target is None and (name, g.index) not in claimed]
