@@ -25,6 +25,7 @@
 
 #include "epilogue.h"
 #include "pin.h"
+#include "streamk.h"
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -814,6 +815,132 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
   }
   return 0;
 }
+
+// ---- stream-K partials -------------------------------------------------------------------------
+// The N = 384 GEMMs of the model (projection, fc2) have 162 tiles of 128x64 for 256 CUs: whole-tile
+// grids leave a third of the chip idle (or a 27%-full second round), and split-K only moves the
+// ragged edge. Here the P workgroups split the tiles' K stages evenly (streamk.h): each runs one
+// continuous stage stream as gemm_x3s does (the DMA ring crosses tile boundaries), and at the end
+// of every tile segment stores its raw accumulators to fp32 partial plane `segment` — no epilogue;
+// the consumer (splitk_layernorm_f32 with the same SkMap) adds a tile's planes in order, then bias,
+// residuals and the LayerNorm. The kernel boundary is the hand-off between workgroups (no flags).
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3k(const __bf16* __restrict__ A, size_t a_plane,
+                                                              const __bf16* __restrict__ W, size_t w_plane,
+                                                              float* __restrict__ C, int M, int N, int K, int P,
+                                                              int ctl) {
+  static_assert(S >= 2 && S <= 4, "2-4 LDS stages");
+  constexpr int NW = WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int RPI = 512 / BKS;
+  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "row groups must divide over the waves");
+  constexpr int NLD = 3 * (BM / RPI / NW) + 3 * (BN / RPI / NW);
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * BKS], A1[3 * BM * BKS],
+      A2[S > 2 ? 3 * BM * BKS : 8], A3[S > 3 ? 3 * BM * BKS : 8];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS],
+      B2[S > 2 ? 3 * BN * BKS : 8], B3[S > 3 ? 3 * BN * BKS : 8];
+
+  const int ablate = (ctl >> 16) & 7;
+  const PinnedBlock pb = pinned_block(unsigned(ctl >> 20) & 0xffu);
+  if (pb.id < 0) return;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int nk = K / BKS, U = tiles_m * tiles_n * nk;
+  // logical workgroup: XCD x runs a contiguous band of ranges, so the workgroups sharing a tile
+  // (neighbouring ranges) mostly share an L2 too
+  const int w = xcd_major_n(pb.id, pb.n, pb.nx);
+  if (w >= P) return;
+  const int u0 = sk_first(w, P, U), total = sk_first(w + 1, P, U) - u0;
+  const size_t plane = size_t(M) * N;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int j = lane & 31, hf = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};
+
+#define X3K_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : (b) == 2 ? A2 : A3)
+#define X3K_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : (b) == 2 ? B2 : B3)
+#define X3K_ISSUE(H, BUF)                                                                 \
+  {                                                                                       \
+    const int u_ = u0 + (H), t_ = u_ / nk, ks_ = u_ - t_ * nk;                            \
+    const int mt_ = t_ / tiles_n, nt_ = t_ - mt_ * tiles_n;                               \
+    uint32_t va_[BM / RPI / NW], vb_[BN / RPI / NW];                                      \
+    dma_offsets<BM, NW, BKS>(va_, mt_ * BM, M - 1, K, wave, lane);                        \
+    dma_offsets<BN, NW, BKS>(vb_, nt_ * BN, N - 1, K, wave, lane);                        \
+    if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, va_, ks_ * BKS, X3K_A(BUF), wave); \
+    if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, vb_, ks_ * BKS, X3K_B(BUF), wave); \
+  }
+// a segment ends at its tile's last stage or at the end of this workgroup's range
+#define X3K_BODY(G, BUF)                                                                  \
+  {                                                                                       \
+    compute_stage_sw<BM, BN, WM, WN, BKS>(acc, X3K_A(BUF), X3K_B(BUF), wm, wn, j, hf);    \
+    const int u_ = u0 + (G), t_ = u_ / nk;                                                \
+    if (u_ - t_ * nk == nk - 1 || (G) == total - 1) {                                     \
+      const int seg_ = w - sk_owner(t_ * nk, P, U), mt_ = t_ / tiles_n, nt_ = t_ - mt_ * tiles_n; \
+      if (!(ablate & 4)) store_tile<TM, TN>(acc, mt_ * BM + wm * WM, nt_ * BN + wn * WN, j, hf, nullptr, nullptr, \
+                         nullptr, 0, C + size_t(seg_) * plane, nullptr, 0, M, N, 0);      \
+      _Pragma("unroll") for (int a = 0; a < TM; ++a)                                      \
+        _Pragma("unroll") for (int b = 0; b < TN; ++b) acc[a][b] = f32x16{0};             \
+    }                                                                                     \
+  }
+#define X3K_ITER(G, BUF)                                                                  \
+  {                                                                                       \
+    vm_wait<(S - 2) * NLD>();                                                             \
+    raw_barrier();                                                                        \
+    X3K_ISSUE((G) + S - 1, ((BUF) + S - 1) % S)                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    X3K_BODY(G, BUF)                                                                      \
+  }
+  for (int st = 0; st < S - 1; ++st)
+    if (st < total) X3K_ISSUE(st, st)
+  int g = 0;
+  for (; g + 2 * S - 1 <= total; g += S) {
+    X3K_ITER(g, 0)
+    X3K_ITER(g + 1, 1)
+    if constexpr (S > 2) X3K_ITER(g + 2, 2)
+    if constexpr (S > 3) X3K_ITER(g + 3, 3)
+  }
+  for (; g < total; ++g) {
+    const int buf = g % S;
+    vm_wait_stage<S, NLD>(total - 1 - g);
+    raw_barrier();
+    if (g + S - 1 < total) X3K_ISSUE(g + S - 1, (buf + S - 1) % S)
+    __builtin_amdgcn_sched_barrier(0);
+    X3K_BODY(g, buf)
+  }
+#undef X3K_BODY
+#undef X3K_ITER
+#undef X3K_ISSUE
+#undef X3K_B
+#undef X3K_A
+  vm_wait<0>();
+}
+
+// tile shape of stream-K config cfg (see nos_gemm_x3_streamk)
+constexpr int kSkCfg[6][2] = {{64, 64}, {128, 64}, {64, 128}, {128, 64}, {64, 64}, {128, 128}};
+
+template <int BM, int BN, int WGM, int WGN, int S, int BKS = 32>
+int launch_k(const __bf16* A, size_t ap, const __bf16* W, size_t wp, float* C, int M, int N, int K, int P, int ctl,
+             hipStream_t s) {
+  if (N % BN || K % BKS) {
+    g_err = "gemm_x3k: N % " + std::to_string(BN) + " and K % " + std::to_string(BKS) + " must be 0";
+    return -1;
+  }
+  hipLaunchKernelGGL((gemm_x3k<BM, BN, WGM, WGN, S, BKS>), dim3(pinned_grid(P, unsigned(ctl >> 20) & 0xffu)),
+                     dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, C, M, N, K, P, ctl);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("gemm_x3k: ") + hipGetErrorString(e);
+    return int(e);
+  }
+  return 0;
+}
 }  // namespace
 
 static int g_group_m = 1;
@@ -971,6 +1098,62 @@ int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, flo
   const int epi = (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20) | ((splits - 1) << 28);
   return dispatch(reinterpret_cast<const __bf16*>(A), ap, reinterpret_cast<const __bf16*>(W), wp, nullptr, nullptr,
                   nullptr, 0, C, nullptr, 0, M, N, K, epi, cfg, reinterpret_cast<hipStream_t>(stream));
+}
+
+// Stream-K configs: 0 = 64x64 S3 (4 waves), 1 = 128x64 S2 64-deep (8 waves), 2 = 64x128 S2 64-deep
+// (8 waves), 3 = 128x64 S3 (4 waves), 4 = 64x64 S2 64-deep (4 waves), 5 = 128x128 S3 (8 waves).
+static int sk_bks(int cfg) { return (cfg == 1 || cfg == 2 || cfg == 4) ? 64 : 32; }
+
+// The work split a stream-K launch of `P` workgroups uses (P clamped to the unit count):
+// out = {P, U, nk, bm, bn, tiles_n, planes}; planes = the most segments any tile has, the depth
+// of the fp32 partial buffer [planes][M][N] the launch writes.
+int nos_gemm_x3_streamk_map(int M, int N, int K, int cfg, int P, int* out) {
+  if (cfg < 0 || cfg > 5 || M <= 0 || P <= 0) {
+    g_err = "gemm_x3k: config 0..5, M > 0 and P > 0";
+    return -1;
+  }
+  const int bm = kSkCfg[cfg][0], bn = kSkCfg[cfg][1], bks = sk_bks(cfg);
+  if (N % bn || K % bks) {
+    g_err = "gemm_x3k: N % " + std::to_string(bn) + " and K % " + std::to_string(bks) + " must be 0";
+    return -1;
+  }
+  SkMap m{0, 0, K / bks, bm, bn, N / bn};
+  const long long tiles = (long long)((M + bm - 1) / bm) * m.tiles_n;
+  if (tiles * m.nk > (1LL << 30) / 4096) {
+    g_err = "gemm_x3k: too many units";
+    return -1;
+  }
+  m.U = int(tiles * m.nk);
+  m.P = std::min(P, m.U);
+  int planes = 1;
+  for (int t = 0; t < int(tiles); ++t) planes = std::max(planes, sk_segments(t, m));
+  const int v[7] = {m.P, m.U, m.nk, bm, bn, m.tiles_n, planes};
+  for (int i = 0; i < 7; ++i) out[i] = v[i];
+  return 0;
+}
+
+// Raw partial sums of C = A · W^T, stream-K over P workgroups (P from nos_gemm_x3_streamk_map):
+// C is the [planes][M][N] fp32 buffer; no epilogue (splitk_layernorm with the same map adds them).
+int nos_gemm_x3_streamk(const void* A, size_t ap, const void* W, size_t wp, float* C, int M, int N, int K, int cfg,
+                        int P, void* stream) {
+  int m[7];
+  if (nos_gemm_x3_streamk_map(M, N, K, cfg, P, m) != 0) return -1;
+  if (m[0] != P || ap % 8 || wp % 8 || !C) {
+    g_err = "gemm_x3k: P must be the map's (clamped) P; plane strides % 8; an output";
+    return -1;
+  }
+  const __bf16* a = reinterpret_cast<const __bf16*>(A);
+  const __bf16* w = reinterpret_cast<const __bf16*>(W);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int ctl = (g_ablate << 16) | int(nos_pin_mask() << 20);
+  switch (cfg) {
+    case 0: return launch_k<64, 64, 2, 2, 3>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+    case 1: return launch_k<128, 64, 4, 2, 2, 64>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+    case 2: return launch_k<64, 128, 2, 4, 2, 64>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+    case 3: return launch_k<128, 64, 2, 2, 3>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+    case 4: return launch_k<64, 64, 2, 2, 2, 64>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+    default: return launch_k<128, 128, 2, 4, 3>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+  }
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "pin.h"
+#include "streamk.h"
 
 #include <cmath>
 #include <cstdint>
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
 // residual stream xout, and, when w is given, LayerNorm(x) stored as x3 planes yp (the next GEMM's
 // operand). One wave per row, grid-stride, lanes on column pairs as layernorm_f32.
 template <int NPL>
-__global__ __launch_bounds__(256) void splitk_layernorm_f32(const float* __restrict__ part, int splits,
+__global__ __launch_bounds__(256) void splitk_layernorm_f32(const float* __restrict__ part, int splits, SkMap sk,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ res,
                                                             const float* __restrict__ r2, int r2_rows,
@@ -158,6 +159,26 @@ __global__ __launch_bounds__(256) void splitk_layernorm_f32(const float* __restr
     float2 v[NP];
 #pragma unroll
     for (int i = 0; i < NP; ++i) v[i] = p2[r2i + i * 64 + lane];
+    if (sk.P > 0) {
+      // stream-K partials: tile t of this row and column pair holds sk_segments(t) planes
+      int ns[NP], most = 1;
+      const int tr = (row / sk.bm) * sk.tiles_n;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        ns[i] = sk_segments(tr + (2 * (i * 64 + lane)) / sk.bn, sk);
+        most = max(most, ns[i]);
+      }
+      for (int sp = 1; sp < most; ++sp) {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          if (sp < ns[i]) {
+            const float2 q = p2[sp * pstride + r2i + i * 64 + lane];
+            v[i].x += q.x;
+            v[i].y += q.y;
+          }
+        }
+      }
+    }
     for (int sp = 1; sp < splits; ++sp) {
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
@@ -1639,9 +1660,9 @@ int nos_layernorm_f32_grid(const float* x, const float* w, const float* b, float
 // Split-K combine (+ bias, residual, broadcast residual r2 or null) into xout, and LayerNorm(xout) as
 // x3 planes into yp when w/b/yp are given; part = [splits][rows][D] fp32; D in {384, 768}; `wgs`
 // workgroups of 4 rows (grid-stride), 0 = one per 4 rows.
-int nos_splitk_layernorm_f32(const float* part, int splits, const float* bias, const float* res, const float* r2,
-                             int r2_rows, float* xout, const float* w, const float* b, void* yp, int rows, int D,
-                             float eps, int wgs, void* stream) {
+static int splitk_layernorm(const float* part, int splits, SkMap sk, const float* bias, const float* res,
+                            const float* r2, int r2_rows, float* xout, const float* w, const float* b, void* yp,
+                            int rows, int D, float eps, int wgs, void* stream) {
   if (!part || splits < 1 || !bias || !res || !xout || (r2 && r2_rows <= 0) || ((w == nullptr) != (yp == nullptr)) ||
       ((w == nullptr) != (b == nullptr))) {
     g_err = "splitk_layernorm: partials, bias, residual and output required; LayerNorm needs w, b and yp";
@@ -1655,11 +1676,11 @@ int nos_splitk_layernorm_f32(const float* part, int splits, const float* bias, c
   __bf16* p = reinterpret_cast<__bf16*>(yp);
   switch (D) {
     case 384:
-      hipLaunchKernelGGL(splitk_layernorm_f32<6>, grid, block, 0, s, part, splits, bias, res, r2, r2_rows, xout, w,
+      hipLaunchKernelGGL(splitk_layernorm_f32<6>, grid, block, 0, s, part, splits, sk, bias, res, r2, r2_rows, xout, w,
                          b, p, rows, eps, pin);
       break;
     case 768:
-      hipLaunchKernelGGL(splitk_layernorm_f32<12>, grid, block, 0, s, part, splits, bias, res, r2, r2_rows, xout, w,
+      hipLaunchKernelGGL(splitk_layernorm_f32<12>, grid, block, 0, s, part, splits, sk, bias, res, r2, r2_rows, xout, w,
                          b, p, rows, eps, pin);
       break;
     default:
@@ -1667,6 +1688,27 @@ int nos_splitk_layernorm_f32(const float* part, int splits, const float* bias, c
       return -1;
   }
   return check_launch("splitk_layernorm_f32");
+}
+
+int nos_splitk_layernorm_f32(const float* part, int splits, const float* bias, const float* res, const float* r2,
+                             int r2_rows, float* xout, const float* w, const float* b, void* yp, int rows, int D,
+                             float eps, int wgs, void* stream) {
+  return splitk_layernorm(part, splits, SkMap{0, 0, 0, 1, 1, 1}, bias, res, r2, r2_rows, xout, w, b, yp, rows, D, eps,
+                          wgs, stream);
+}
+
+// The same over stream-K partials (gemm_x3k): map = {P, U, nk, bm, bn, tiles_n} from
+// nos_gemm_x3_streamk_map; tile t's planes 0 .. sk_segments(t)-1 are added in order.
+int nos_streamk_layernorm_f32(const float* part, const int* map, const float* bias, const float* res, const float* r2,
+                              int r2_rows, float* xout, const float* w, const float* b, void* yp, int rows, int D,
+                              float eps, int wgs, void* stream) {
+  if (!map || map[0] <= 0 || map[1] < map[0] || map[2] <= 0 || map[3] <= 0 || map[4] <= 0 || map[4] % 2 ||
+      map[5] * map[4] != D) {
+    g_err = "streamk_layernorm: map must be {P <= U, U, nk, bm, bn (even), tiles_n} with tiles_n * bn = D";
+    return -1;
+  }
+  return splitk_layernorm(part, 1, SkMap{map[0], map[1], map[2], map[3], map[4], map[5]}, bias, res, r2, r2_rows,
+                          xout, w, b, yp, rows, D, eps, wgs, stream);
 }
 
 int nos_layernorm_f32(const float* x, const float* w, const float* b, float* y, void* yp, int rows, int D,

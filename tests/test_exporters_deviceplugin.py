@@ -121,12 +121,17 @@ def test_device_plugin_list_and_watch_allocate_and_register():
                 assert envs["HSA_CU_MASK"] == "0:32-63"
                 assert envs["NOS_HBM_LIMIT_BYTES"] == str(36 * 10**9)
                 assert envs["LD_PRELOAD"].endswith("libnos_hbmlimit.so")
+                assert "GPU_MAX_HW_QUEUES" not in envs  # dedicated CUs: HIP's default queues
                 assert [x.host_path for x in resp.container_responses[0].devices] == ["/dev/kfd", "/dev/dri/renderD128"]
             shared = SliceDevicePlugin("amd.com/gpu-10gb", store, {}, socket_dir=d)
             req = dp.AllocateRequest()
             req.container_requests.add(devicesIDs=["g0::s2"])
             envs = dict(shared.Allocate(req, None).container_responses[0].envs)
             assert envs["HSA_CU_MASK"] == "0:64-255"  # shared pool = rows no dedicated slice owns
+            assert envs["GPU_MAX_HW_QUEUES"] == "1"   # memory-only: one queue per pod (sharedSliceHwQueues)
+            envs = dict(SliceDevicePlugin("amd.com/gpu-10gb", store, {}, socket_dir=d, shared_hw_queues=0)
+                        .Allocate(req, None).container_responses[0].envs)
+            assert "GPU_MAX_HW_QUEUES" not in envs
         finally:
             mgr.stop()
             reg.stop()

@@ -447,6 +447,39 @@ def test_splitk_partials_and_combine_layernorm(K, M, N, Kd):
         assert (x_only.double() - (hb + b.double() + r.double())).abs().max().item() < 1e-4, (cfg, sp)
 
 
+@pytest.mark.parametrize("M,N,Kd", [(3401, 384, 1536), (3401, 384, 384), (300, 768, 256)])
+def test_streamk_partials_and_combine_layernorm(K, M, N, Kd):
+    # stream-K partials over every config and grids that cut tiles into 1..many segments (P = 1,
+    # a prime, the chip's slots, more workgroups than units) + the combine/LayerNorm vs fp64
+    import torch.nn.functional as F
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(18)
+    x3 = K.split3(torch.randn(M, Kd, device="cuda"))
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    r = torch.randn(M, N, device="cuda")
+    r2 = torch.randn(1, 97, N, device="cuda")
+    lw, lb = torch.randn(N, device="cuda"), torch.randn(N, device="cuda")
+    hb = x3.double().sum(0) @ G.weight_planes(w).double().sum(0).t()
+    ref_x = hb + b.double() + r.double() + r2.double().reshape(97, N)[torch.arange(M) % 97]
+    ref_ln = F.layer_norm(ref_x, (N,), lw.double(), lb.double(), 1e-12)
+    ran = 0
+    for cfg, (bm, bn, bk, _) in G.X3K_TILES.items():
+        if N % bn or Kd % bk:
+            continue
+        for P in (1, 7, 256, 512, 1 << 20):
+            m = G.streamk_map(M, N, Kd, cfg, P)
+            # planes a tile does not own stay NaN: the combine must never read them
+            part, m2 = G.gemm_x3_streamk(x3, w, cfg, P, out=torch.full((m[6], M, N), float("nan"), device="cuda"))
+            assert m2 == m
+            x, planes = K.streamk_layernorm(part, m, b, r, r2, (lw, lb, 1e-12))
+            torch.cuda.synchronize()
+            assert (x.double() - ref_x).abs().max().item() < 1e-4, (cfg, P, m)
+            assert (planes.double().sum(0) - ref_ln).abs().max().item() < 1e-4, (cfg, P, m)
+            ran += 1
+    assert ran >= 10
+
+
 def test_linear_residual_ln_x3_tuned_pipeline(K):
     # whichever pipeline the tuner picks, the result matches the unfused ops
     from walkai_nos_amd.ops import gemm as G

@@ -3,6 +3,7 @@ state): python tools/model_replay.py [--slice spx] [--replays 40]. Prints ms per
 from __future__ import annotations
 
 import argparse
+import json
 import os
 import sys
 import time
@@ -21,6 +22,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--slice", default="spx")
     ap.add_argument("--replays", type=int, default=40)
+    ap.add_argument("--tables", action="store_true", help="print the GEMM tiles / split-K choices the tuner made")
     a = ap.parse_args()
     cus = slice_cus(f"{a.slice}_nps1", 0)
     with Stream(0, cus) as hs:
@@ -45,6 +47,9 @@ def main() -> int:
             s.synchronize()
             dt = (time.perf_counter() - t0) / a.replays
         print(f"{a.slice}: {dt * 1e3:.3f} ms per inference over {a.replays} replays", flush=True)
+        if a.tables:
+            from walkai_nos_amd.ops import gemm as G
+            print(json.dumps({"x3": G.x3_table(), "linear_residual_ln": G.fused_table()}, indent=1), flush=True)
         del g
     return 0
 

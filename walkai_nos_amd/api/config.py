@@ -163,8 +163,20 @@ class MigAgentConfig(AgentConfig):
 
 @dataclass
 class GpuAgentConfig(AgentConfig):
-    """CU-mask slice agent configuration (kind kept from the reference)."""
+    """CU-mask slice agent configuration (kind kept from the reference).
+
+    ``sharedSliceHwQueues``: hardware queues a memory-only slice's container may create
+    (``GPU_MAX_HW_QUEUES`` in ``Allocate``; 0 leaves HIP's default of 4). Memory-only slices share
+    every CU, and the command processor arbitrates dispatch per hardware pipe, so with HIP's four
+    queues per process a pod's share of the GPU follows where its queues land, not the pod count
+    (docs/partitioning-modes-comparison.md); one queue per pod evens the shares."""
     hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
+    sharedSliceHwQueues: int = 1
+
+    def validate(self) -> None:
+        super().validate()
+        if not 0 <= self.sharedSliceHwQueues <= 4:
+            raise ValueError("sharedSliceHwQueues must be 0 (HIP default) .. 4")
 
 
 @dataclass

@@ -48,7 +48,8 @@ def main(argv=None) -> int:
     # Unhealthy); the sysfs listing is only the fallback for a map without render minors
     plugins = PluginManager(store, render_nodes_from_sysfs(), socket_dir=cfg.devicePluginDir,
                             kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
-                            cu_count=gpus[0].cu_count or 256, shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map)
+                            cu_count=gpus[0].cu_count or 256, shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map,
+                            shared_hw_queues=cfg.sharedSliceHwQueues)
 
     class Notify:
         def restart(self, node_name, timeout=60):

@@ -38,6 +38,8 @@ LABEL_AMD_MEMORY_PARTITION = "amd.com/memory-partitioning-mode"
 ENV_NODE_NAME = "NODE_NAME"
 ENV_HSA_CU_MASK = "HSA_CU_MASK"
 ENV_HBM_LIMIT = "NOS_HBM_LIMIT_BYTES"
+#: HIP's per-process hardware queue count (memory-only slices: sharedSliceHwQueues)
+ENV_GPU_MAX_HW_QUEUES = "GPU_MAX_HW_QUEUES"
 ENV_SLICE_CU_MASK = "NOS_SLICE_CU_MASK"  # hex CU bitmap (consumed by the stream shim)
 
 # defaults

@@ -218,13 +218,14 @@ class SliceDevicePlugin(PluginServer):
     def __init__(self, resource_name: str, store: SliceStore, gpu_render_nodes: Dict[int, str],
                  cu_count: int = 256, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so",
                  socket_dir: str = DEVICE_PLUGIN_DIR, poll_interval: float = 1.0,
-                 device_map: Optional[Callable[[], Any]] = None):
+                 device_map: Optional[Callable[[], Any]] = None, shared_hw_queues: int = 1):
         super().__init__(resource_name, socket_dir, poll_interval)
         self.store = store
         self.render = gpu_render_nodes
         self.cu_count = cu_count
         self.shim_path = shim_path
         self.device_map = device_map
+        self.shared_hw_queues = shared_hw_queues
 
     # -- device view ------------------------------------------------------------------------
     def _map(self) -> Any:
@@ -279,6 +280,7 @@ class SliceDevicePlugin(PluginServer):
             cus: List[int] = []
             hbm = 0
             gpus: Dict[int, str] = {}
+            shared = True
             for did in cr.devicesIDs:
                 if did not in by_id:
                     if ctx is not None:
@@ -293,7 +295,12 @@ class SliceDevicePlugin(PluginServer):
                     raise ValueError(msg)
                 cus.extend(cus_of(s, slices[g], self.cu_count))
                 hbm += s.hbm_bytes
+                shared = shared and not s.rows
             car.envs[constant.ENV_HSA_CU_MASK] = hsa_cu_mask(cus, 0)
+            if shared and self.shared_hw_queues > 0:
+                # memory-only: every pod on the shared CUs gets the same number of queues, so the
+                # per-pipe dispatch arbitration splits the GPU by pod (sharedSliceHwQueues)
+                car.envs[constant.ENV_GPU_MAX_HW_QUEUES] = str(self.shared_hw_queues)
             car.envs[constant.ENV_HBM_LIMIT] = str(hbm)
             car.envs["LD_PRELOAD"] = self.shim_path
             car.envs["NOS_SLICE_IDS"] = ",".join(cr.devicesIDs)
@@ -355,8 +362,9 @@ class PluginManager:
                  shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so", device_map: Optional[Callable[[], Any]] = None,
                  resources: Optional[Callable[[], List[str]]] = None,
                  factory: Optional[Callable[[str], PluginServer]] = None,
-                 register_attempts: int = 5, register_backoff: float = 0.5):
+                 register_attempts: int = 5, register_backoff: float = 0.5, shared_hw_queues: int = 1):
         self.store = store
+        self.shared_hw_queues = shared_hw_queues
         self.render = gpu_render_nodes or {}
         self.socket_dir = socket_dir
         self.kubelet_socket = kubelet_socket
@@ -375,7 +383,7 @@ class PluginManager:
 
     def _slice_plugin(self, r: str) -> PluginServer:
         return SliceDevicePlugin(r, self.store, self.render, self.cu_count, self.shim_path, self.socket_dir,
-                                 device_map=self.device_map)
+                                 device_map=self.device_map, shared_hw_queues=self.shared_hw_queues)
 
     def sync(self, attempts: Optional[int] = None) -> None:
         """``attempts``: registration attempts per plugin this call (default: the manager's); the

@@ -247,6 +247,8 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         L.nos_gemm_x3_partials.argtypes = [vp, sz, vp, sz, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_set_group.argtypes = [i32]
+        L.nos_gemm_x3_streamk_map.argtypes = [i32, i32, i32, i32, i32, vp]
+        L.nos_gemm_x3_streamk.argtypes = [vp, sz, vp, sz, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_set_ablate.argtypes = [i32]
         ablate = int(os.environ.get("NOS_X3_ABLATE", "0"))  # timing studies only: results are invalid
         if ablate:
@@ -473,6 +475,55 @@ def gemm_x3_partials(a3: torch.Tensor, w: torch.Tensor, cfg: int, splits: int,
     return out
 
 
+# ---- stream-K partials --------------------------------------------------------------------------
+#: stream-K configs (csrc/gemm_x3.hip gemm_x3k) -> (BM, BN, K stage depth, resident workgroups per CU)
+X3K_TILES = {0: (64, 64, 32, 2), 1: (128, 64, 64, 1), 2: (64, 128, 64, 1), 3: (128, 64, 32, 1), 4: (64, 64, 64, 1),
+             5: (128, 128, 32, 1)}
+
+
+def streamk_map(M: int, N: int, Kd: int, cfg: int, P: int) -> Tuple[int, ...]:
+    """The work split of a stream-K launch: ``(P, U, nk, bm, bn, tiles_n, planes)`` (P clamped to
+    the unit count; ``planes`` = depth of the partial buffer)."""
+    out = (ctypes.c_int * 7)()
+    if _lib_x3().nos_gemm_x3_streamk_map(M, N, Kd, cfg, P, out) != 0:
+        raise ValueError(_lib_x3().nos_gemm_x3_last_error().decode())
+    return tuple(out)
+
+
+def gemm_x3_streamk(a3: torch.Tensor, w: torch.Tensor, cfg: int, P: int,
+                    out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Tuple[int, ...]]:
+    """Stream-K partial sums of ``a @ w^T`` over ``P`` workgroups: ``([planes, M, N] fp32, map)``;
+    plane s of tile t holds its s-th K segment for s < segments(t) (``csrc/streamk.h``), the rest is
+    never written. ``kernels.streamk_layernorm`` with the same map is the consumer."""
+    Kd = a3.shape[-1]
+    a3 = a3.reshape(3, -1, Kd)
+    if not a3.is_contiguous():
+        a3 = a3.contiguous()
+    M = a3.shape[1]
+    w3 = w if w.dim() == 3 else weight_planes(w)
+    N = w3.shape[1]
+    m = streamk_map(M, N, Kd, cfg, P)
+    if out is not None and (tuple(out.shape) != (m[6], M, N) or not out.is_contiguous()):
+        raise ValueError(f"gemm_x3_streamk: out must be a contiguous [{m[6]}, {M}, {N}] buffer")
+    part = out if out is not None else torch.empty(m[6], M, N, dtype=torch.float32, device=a3.device)
+    rc = _lib_x3().nos_gemm_x3_streamk(a3.data_ptr(), a3[0].numel(), w3.data_ptr(), w3[0].numel(), part.data_ptr(),
+                                       M, N, Kd, cfg, m[0], torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"nos gemm_x3 stream-K failed: {_lib_x3().nos_gemm_x3_last_error().decode()} (rc={rc})")
+    return part, m
+
+
+def streamk_candidates(N: int, Kd: int, cus: int) -> list:
+    """(config, P) pairs that can run this shape: P = the slice's resident workgroup slots (and,
+    for two-slot tiles, one per CU)."""
+    out = []
+    for c, (bm, bn, bk, slots) in X3K_TILES.items():
+        if N % bn or Kd % bk:
+            continue
+        out += [(c, s * cus) for s in range(slots, 0, -1)]
+    return out
+
+
 def split_candidates(N: int, Kd: int) -> list:
     """(tile, splits) pairs that can run this shape in the partials mode."""
     out = []
@@ -512,6 +563,10 @@ def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, re
     def split(cfg, sp):
         part = gemm_x3_partials(a3, w, cfg, sp)
         return K.splitk_layernorm(part, b, residual, residual2, ln, lead)
+
+    def streamk(cfg, P):
+        part, m = gemm_x3_streamk(a3, w, cfg, P)
+        return K.streamk_layernorm(part, m, b, residual, residual2, ln, lead)
     if choice is None:
         if torch.cuda.is_current_stream_capturing() or os.environ.get("NOS_SPLITK", "1") == "0" \
                 or K.slice_cus() < SPLITK_MIN_CUS:
@@ -524,10 +579,22 @@ def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, re
             times = {("unsplit",): _gpu_time(unsplit, stream)}
             for c, sp in split_candidates(N, Kd):
                 times[("split", c, sp)] = _gpu_time(lambda c=c, sp=sp: split(c, sp), stream)
+            if os.environ.get("NOS_STREAMK", "1") != "0":
+                for c, P in streamk_candidates(N, Kd, K.slice_cus()):
+                    times[("streamk", c, P)] = _gpu_time(lambda c=c, P=P: streamk(c, P), stream)
             choice = min(times, key=times.get)
             with _lock:
                 _fused_cache[key] = choice
+    if choice[0] == "streamk":
+        return streamk(choice[1], choice[2])
     return unsplit() if choice[0] == "unsplit" else split(choice[1], choice[2])
+
+
+def x3_table() -> Dict[str, str]:
+    """The x3 tiles picked so far: shape/epilogue/outputs/slice -> ``BMxBN/<kind>`` (tile id)."""
+    with _lock:
+        return {f"M{m}_N{n}_K{k}_epi{e}_out{o}_cus{c}_pin{p}": "x".join(map(str, X3_TILES[v][:2])) + f"/{X3_TILES[v][3]}"
+                + f" ({v})" for (m, n, k, e, o, c, p), v in sorted(_x3_cache.items())}
 
 
 def fused_table() -> Dict[str, str]:

@@ -366,6 +366,7 @@ def _L() -> ctypes.CDLL:
             L.nos_kernels_last_error.restype = ctypes.c_char_p
             L.nos_set_pin.argtypes = [ctypes.c_uint]
             L.nos_splitk_layernorm_f32.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, f32, i32, vp]
+            L.nos_streamk_layernorm_f32.argtypes = [vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, i32, f32, i32, vp]
             L.nos_pin_mask.restype = ctypes.c_uint
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
@@ -446,6 +447,27 @@ def splitk_layernorm(part: torch.Tensor, bias: torch.Tensor, res: torch.Tensor, 
                                          ln[1].data_ptr() if ln is not None else None,
                                          planes.data_ptr() if planes is not None else None, M, N,
                                          float(ln[2]) if ln is not None else 0.0, layernorm_wgs(M), _stream()))
+    return x, planes
+
+
+def streamk_layernorm(part: torch.Tensor, sk_map, bias: torch.Tensor, res: torch.Tensor,
+                      res2: Optional[torch.Tensor], ln=None, shape=None):
+    """:func:`splitk_layernorm` over stream-K partials (``gemm.gemm_x3_streamk``): ``sk_map`` is the
+    launch's ``(P, U, nk, bm, bn, tiles_n, planes)``; tile t's first ``segments(t)`` planes are added
+    in order (``csrc/streamk.h``)."""
+    _, M, N = part.shape
+    shape = tuple(shape if shape is not None else res.shape)
+    x = torch.empty(shape, dtype=torch.float32, device=part.device)
+    planes = torch.empty((3,) + shape, dtype=torch.bfloat16, device=part.device) if ln is not None else None
+    r2 = res2.reshape(-1, N).contiguous() if res2 is not None else None
+    res = res.contiguous()
+    m = (ctypes.c_int * 6)(*[int(v) for v in sk_map[:6]])
+    _check(_L().nos_streamk_layernorm_f32(part.data_ptr(), m, bias.data_ptr(), res.data_ptr(),
+                                          r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+                                          x.data_ptr(), ln[0].data_ptr() if ln is not None else None,
+                                          ln[1].data_ptr() if ln is not None else None,
+                                          planes.data_ptr() if planes is not None else None, M, N,
+                                          float(ln[2]) if ln is not None else 0.0, layernorm_wgs(M), _stream()))
     return x, planes
 
 
