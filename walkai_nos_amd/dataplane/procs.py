@@ -88,7 +88,7 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
     logs = []
     try:
         for i, (prof, env) in enumerate(zip(profiles, envs)):
-            e = dict(base, **env, NOS_POD_SEED=str(i), **(extra_env or {}))
+            e = {**base, **env, "NOS_POD_SEED": str(i), **(extra_env or {})}  # extra_env overrides Allocate's
             log = tempfile.TemporaryFile(mode="w+")  # a full stderr pipe would stall the pod
             logs.append(log)
             p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,

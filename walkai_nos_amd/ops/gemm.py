@@ -537,6 +537,8 @@ def split_candidates(N: int, Kd: int) -> list:
 
 
 _fused_cache: Dict[tuple, tuple] = {}
+#: the tuner's timings per key (ms for 3 graph-replayed calls), for tools/model_replay.py --tables
+_fused_times: Dict[tuple, Dict[tuple, float]] = {}
 
 
 def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, residual: torch.Tensor,
@@ -585,6 +587,7 @@ def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, re
             choice = min(times, key=times.get)
             with _lock:
                 _fused_cache[key] = choice
+                _fused_times[key] = times
     if choice[0] == "streamk":
         return streamk(choice[1], choice[2])
     return unsplit() if choice[0] == "unsplit" else split(choice[1], choice[2])
@@ -595,6 +598,14 @@ def x3_table() -> Dict[str, str]:
     with _lock:
         return {f"M{m}_N{n}_K{k}_epi{e}_out{o}_cus{c}_pin{p}": "x".join(map(str, X3_TILES[v][:2])) + f"/{X3_TILES[v][3]}"
                 + f" ({v})" for (m, n, k, e, o, c, p), v in sorted(_x3_cache.items())}
+
+
+def fused_timings() -> Dict[str, Dict[str, float]]:
+    """Every pipeline the projection/fc2 tuner timed, per key: ``/``-joined choice -> µs per call."""
+    with _lock:
+        return {f"M{m}_N{n}_K{k}_r2{int(r2)}_ln{int(ln)}_cus{c}_pin{p}":
+                {"/".join(map(str, ch)): round(t * 1000 / 3, 2) for ch, t in sorted(v.items(), key=lambda x: x[1])}
+                for (m, n, k, r2, ln, c, p), v in sorted(_fused_times.items())}
 
 
 def fused_table() -> Dict[str, str]:
