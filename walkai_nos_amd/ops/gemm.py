@@ -581,7 +581,9 @@ def linear_residual_ln_x3(a3: torch.Tensor, w: torch.Tensor, b: torch.Tensor, re
             times = {("unsplit",): _gpu_time(unsplit, stream)}
             for c, sp in split_candidates(N, Kd):
                 times[("split", c, sp)] = _gpu_time(lambda c=c, sp=sp: split(c, sp), stream)
-            if os.environ.get("NOS_STREAMK", "1") != "0":
+            # stream-K partials (gemm_x3k): opt-in — on the model's shapes it is 15-25% slower than
+            # the best split-K / unsplit pipeline (profiles/gemm_tuner_r4_streamk.json)
+            if os.environ.get("NOS_STREAMK", "0") == "1":
                 for c, P in streamk_candidates(N, Kd, K.slice_cus()):
                     times[("streamk", c, P)] = _gpu_time(lambda c=c, P=P: streamk(c, P), stream)
             choice = min(times, key=times.get)
