@@ -128,10 +128,22 @@ def test_device_plugin_list_and_watch_allocate_and_register():
             req.container_requests.add(devicesIDs=["g0::s2"])
             envs = dict(shared.Allocate(req, None).container_responses[0].envs)
             assert envs["HSA_CU_MASK"] == "0:64-255"  # shared pool = rows no dedicated slice owns
-            assert envs["GPU_MAX_HW_QUEUES"] == "1"   # memory-only: one queue per pod (sharedSliceHwQueues)
+            # memory-only: the queue count decides the per-pipe split (sharedSliceHwQueues auto:
+            # two queues while <= 3 memory-only slices share the GPU, one beyond)
+            assert envs["GPU_MAX_HW_QUEUES"] == "2"
             envs = dict(SliceDevicePlugin("amd.com/gpu-10gb", store, {}, socket_dir=d, shared_hw_queues=0)
                         .Allocate(req, None).container_responses[0].envs)
             assert "GPU_MAX_HW_QUEUES" not in envs
+            envs = dict(SliceDevicePlugin("amd.com/gpu-10gb", store, {}, socket_dir=d, shared_hw_queues=3)
+                        .Allocate(req, None).container_responses[0].envs)
+            assert envs["GPU_MAX_HW_QUEUES"] == "3"
+            many = MemorySliceStore()
+            many.save({0: [Slice(f"g0::m{i}", "10gb", [], 10 * 10**9) for i in range(5)]})
+            req5 = dp.AllocateRequest()
+            req5.container_requests.add(devicesIDs=["g0::m4"])
+            envs = dict(SliceDevicePlugin("amd.com/gpu-10gb", many, {}, socket_dir=d)
+                        .Allocate(req5, None).container_responses[0].envs)
+            assert envs["GPU_MAX_HW_QUEUES"] == "1"
         finally:
             mgr.stop()
             reg.stop()

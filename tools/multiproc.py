@@ -36,7 +36,7 @@ def split_groups(n: int, groups: int = 8):
 
 def scenarios():
     out = {}
-    for n in (1, 3, 5, 7):
+    for n in (1, 3, 4, 5, 7):
         out[f"shared_{n}"] = (["16gb"] * n, True)
     for n in (3, 5, 7):
         out[f"cumask_{n}"] = (split_groups(n), True)

@@ -166,17 +166,18 @@ class GpuAgentConfig(AgentConfig):
     """CU-mask slice agent configuration (kind kept from the reference).
 
     ``sharedSliceHwQueues``: hardware queues a memory-only slice's container may create
-    (``GPU_MAX_HW_QUEUES`` in ``Allocate``; 0 leaves HIP's default of 4). Memory-only slices share
-    every CU, and the command processor arbitrates dispatch per hardware pipe, so with HIP's four
-    queues per process a pod's share of the GPU follows where its queues land, not the pod count
-    (docs/partitioning-modes-comparison.md); one queue per pod evens the shares."""
+    (``GPU_MAX_HW_QUEUES`` in ``Allocate``): 1-4 fixed, 0 leaves HIP's default of 4, -1 (default)
+    = 2 while at most 3 memory-only slices share the GPU, else 1. Memory-only slices share every
+    CU and the command processor arbitrates dispatch per hardware pipe, so a pod's share of the GPU
+    follows where its queues land, not the pod count; the auto rule is the measured best per pod
+    count (docs/partitioning-modes-comparison.md, ``profiles/fairness_r4_repeat.json``)."""
     hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
-    sharedSliceHwQueues: int = 1
+    sharedSliceHwQueues: int = -1
 
     def validate(self) -> None:
         super().validate()
-        if not 0 <= self.sharedSliceHwQueues <= 4:
-            raise ValueError("sharedSliceHwQueues must be 0 (HIP default) .. 4")
+        if not -1 <= self.sharedSliceHwQueues <= 4:
+            raise ValueError("sharedSliceHwQueues must be -1 (auto), 0 (HIP default) or 1..4")
 
 
 @dataclass
