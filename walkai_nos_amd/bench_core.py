@@ -832,6 +832,15 @@ def pod_keys(sn: Any, gpu: int) -> Dict[Tuple[str, str], Tuple[Any, ...]]:
 
 
 # -- density --------------------------------------------------------------------------------
+def _per_pod_spread(got: Dict[Any, int], keys: List[Any], dt: float) -> Dict[str, Any]:
+    """Per-pod inferences/s of one density serve: min, max, max/min (how evenly the pods shared)."""
+    rates = sorted(got.get(k, 0) / max(dt, 1e-9) for k in keys)
+    if not rates:
+        return {}
+    return {"min": round(rates[0], 1), "max": round(rates[-1], 1),
+            "max_over_min": round(rates[-1] / rates[0], 2) if rates[0] > 0 else None}
+
+
 def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 1.0) -> Dict[str, Any]:
     """Saturate a fresh node through the control plane, then serve every pod on this rank's GPU
     at once: 8 CPX pods per GPU, then a CU-mask node with dedicated-CU + memory-only slices."""
@@ -857,10 +866,12 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
         keys = [("cpx_nps1", sn.smi.resolve(d).partition_index) for devs in sn.kubelet.allocations.values()
                 for _, d in devs if sn.smi.resolve(d).gpu_index == cfg.rank]
         t0 = time.perf_counter()
-        n = sum(data.serve(keys, t0 + serve_s).values())
+        got = data.serve(keys, t0 + serve_s)
         data.drain_all()
         torch.cuda.synchronize()
-        out["xcp"]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
+        dt = time.perf_counter() - t0
+        out["xcp"]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
+        out["xcp"]["per_pod"] = _per_pod_spread(got, keys, dt)
     # CU-mask slices beyond 8 per GPU
     for variant, mix in CUMASK_DENSITY.items():
         c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
@@ -889,10 +900,12 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
             wanted = {(variant, s.id): cus_of(s, slices, 256) for s in slices if s.id in mine}
             data.add_slots(wanted)
             t0 = time.perf_counter()
-            n = sum(data.serve(list(wanted), t0 + serve_s).values())
+            got = data.serve(list(wanted), t0 + serve_s)
             data.drain_all()
             torch.cuda.synchronize()
-            out[variant]["inf_per_s_per_gpu"] = round(n / (time.perf_counter() - t0), 1)
+            dt = time.perf_counter() - t0
+            out[variant]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
+            out[variant]["per_pod"] = _per_pod_spread(got, list(wanted), dt)
     return out
 
 
