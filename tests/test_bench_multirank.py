@@ -87,3 +87,11 @@ def test_one_rank_veto_rolls_back_on_every_rank():
     assert any(c[0] == "compute" for c in r0[6])
     assert r0[5] == r1[5] and r0[2] == r1[2]
     assert any(r0[2][1:]), "the retried plan must commit once the veto is gone"
+
+
+def test_density_per_pod_spread():
+    from walkai_nos_amd.bench_core import _per_pod_spread
+    r = _per_pod_spread({"a": 10, "b": 20, "c": 0}, ["a", "b"], 2.0)
+    assert r == {"min": 5.0, "max": 10.0, "max_over_min": 2.0}
+    assert _per_pod_spread({}, ["a"], 1.0)["max_over_min"] is None   # a pod that served nothing
+    assert _per_pod_spread({}, [], 1.0) == {}

@@ -7,8 +7,9 @@ first — plus a reservation: the oldest pod that fits nowhere, once it has wait
 blocks everything behind it until it starts (without it whole-GPU pods starve). This is what the
 sliced-GPU planner does (``controllers/partitioner/sliced.py``) with none of the real system's
 costs, so its p99 waits are a floor for that policy family: swept over ``T`` it shows that on one GPU
-at load 0.85 no threshold brings the worst profile's p99 time-to-schedule below ~5 mean pod
-lifetimes (a whole-GPU pod must wait for the GPU to empty of pods that cannot be preempted).
+at load 0.85 no threshold brings the worst profile's p99 time-to-schedule below 6 mean pod
+lifetimes (a whole-GPU pod must wait for the GPU to empty of pods that cannot be preempted;
+``profiles/queue_bound_r4.json``); on two GPUs its best is 3.25-4.5 (the real planner: 3.75).
 
     python tools/queue_bound.py [--gpus 1] [--loads 0.85,1.0] [--thresholds 0,8,16,24,32,48]
         [--seeds 1,2,3,4] [--steps 400] [--out profiles/queue_bound_r4.json]
