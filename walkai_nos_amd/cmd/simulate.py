@@ -32,6 +32,8 @@ def main(argv=None) -> int:
     ap.add_argument("--cluster-s", type=float, default=60.0, help="cluster seconds per step")
     ap.add_argument("--preroll", type=int, default=60)
     ap.add_argument("--scenario", default="churn", choices=("churn", "erq"))
+    ap.add_argument("--layout", default="partitions", choices=("partitions", "slices", "auto"),
+                    help="xcp-layout label of the nodes (churn scenario): hardware modes, sliced GPUs or auto")
     ap.add_argument("--quiet", action="store_true", help="print only the summary line")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.WARNING)
@@ -45,7 +47,8 @@ def main(argv=None) -> int:
         print(json.dumps(r))
         return 0
     nb = NodeBench(BenchConfig(gpus=args.gpus, nodes=args.nodes, offered_load=args.load, seed=args.seed,
-                               policy=args.policy, flip_cost_s=args.flip_cost, cluster_s=args.cluster_s),
+                               policy=args.policy, flip_cost_s=args.flip_cost, cluster_s=args.cluster_s,
+                               layout=args.layout),
                    gpu_data_plane=False)
     for _ in range(args.preroll):
         nb.control_step()
@@ -59,7 +62,7 @@ def main(argv=None) -> int:
             print(json.dumps({"epoch": e, "util_pct": round(nb.util_samples[-1], 2), "pods": nb.pods_samples[-1],
                               "pending": nb.pending_samples[-1]}))
     dt = time.perf_counter() - t0
-    print(json.dumps({"policy": args.policy, "nodes": args.nodes, "gpus_per_node": args.gpus, "load": args.load,
+    print(json.dumps({"policy": args.policy, "layout": args.layout, "nodes": args.nodes, "gpus_per_node": args.gpus, "load": args.load,
                       "mean_util_pct": round(sum(nb.util_samples) / len(nb.util_samples), 2),
                       "mean_pods_per_node": round(sum(nb.pods_samples) / len(nb.pods_samples) / args.nodes, 2),
                       "pending_mean": round(sum(nb.pending_samples) / len(nb.pending_samples), 2),
