@@ -74,7 +74,8 @@ class GpuPartitionerConfig(ManagerConfig):
     #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
     #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds,
     #: reserveBreakFill, minStintSeconds, unservedAfterSeconds; sliced GPUs (xcp-layout slices /
-    #: auto): sliceReserveAfterSeconds, sliceFill
+    #: auto): sliceReserveAfterSeconds, sliceReserveBacklog (GPUs of waiting work per sliced GPU
+    #: above which the threshold stretches; 0 = never), sliceReserveStretch (its largest factor), sliceFill
     packing: Dict[str, Any] = field(default_factory=dict)
 
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
@@ -82,6 +83,7 @@ class GpuPartitionerConfig(ManagerConfig):
                     "drainGain": "drain_gain", "drainGainAfterSeconds": "drain_gain_after", "minStintSeconds": "min_stint",
                     "unservedAfterSeconds": "unserved_after", "replanEverySeconds": "replan_every",
                     "reserveBreakFill": "reserve_break_fill", "sliceReserveAfterSeconds": "slice_reserve_after",
+                    "sliceReserveBacklog": "slice_reserve_backlog", "sliceReserveStretch": "slice_reserve_stretch",
                     "sliceFill": "slice_fill"}
     BOOL_PACKING_KEYS = ("spxReserve", "sliceFill")
 
