@@ -816,6 +816,155 @@ int launch_s(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
   return 0;
 }
 
+// ---- staggered 8-wave 16x16x32 tiles -----------------------------------------------------------
+// Two waves share each SIMD in a 512-thread workgroup, and with one barrier per stage and the same
+// program they run in lockstep: both issue their LDS fragment reads, wait on them and reach the
+// barrier together, so neither covers the other's stall (MI355X_MICROARCH.md, "Two waves per SIMD",
+// item 9). Here the second half of the workgroup (waves NW/2.., the SIMD partners of the first
+// half) runs half a stage behind: in stage ks it finishes the second half of its accumulator rows
+// for stage ks-1, then the first half for stage ks, so while one wave of a SIMD waits on its reads
+// its partner is in the middle of its MFMAs. A stage buffer is therefore read one stage longer:
+// three LDS buffers, one stage of DMA in flight (as the two-buffer tiles). Same math and epilogue
+// as gemm_x3d<..., M16>; ``rows [R0, R1)`` of the wave's 16-row blocks per call.
+template <int BM, int BN, int WM, int WN, int R0, int R1>
+__device__ __forceinline__ void compute_rows16(f32x4 (&acc)[WM / 16][WN / 16], const __bf16* __restrict__ as,
+                                               const __bf16* __restrict__ bs, int wm, int wn, int lane) {
+  constexpr int TN = WN / 16;
+  const int r16 = lane & 15;
+  const int ch = (lane >> 4) ^ dma_swz<32, true>(r16);
+  bf16x8 af[R1 - R0][3], bfr[TN][3];
+#pragma unroll
+  for (int a = R0; a < R1; ++a)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      af[a - R0][q] = *reinterpret_cast<const bf16x8*>(&as[q * BM * 32 + (wm * WM + 16 * a + r16) * 32 + 8 * ch]);
+#pragma unroll
+  for (int b = 0; b < TN; ++b)
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      bfr[b][q] = *reinterpret_cast<const bf16x8*>(&bs[q * BN * 32 + (wn * WN + 16 * b + r16) * 32 + 8 * ch]);
+#pragma unroll
+  for (int a = R0; a < R1; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+      acc[a][b] = mfma_x3_16(af[a - R0][0], af[a - R0][1], af[a - R0][2], bfr[b][0], bfr[b][1], bfr[b][2], acc[a][b]);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3t(const __bf16* __restrict__ A, size_t a_plane,
+                                                              const __bf16* __restrict__ W, size_t w_plane,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ R,
+                                                              const float* __restrict__ R2, int r2_rows,
+                                                              float* __restrict__ C, __bf16* __restrict__ Cp,
+                                                              size_t c_plane, int M, int N, int K, int epi) {
+  constexpr int NW = WGM * WGN, BKS = 32, RPI = 16;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM16 = WM / 16, TN16 = WN / 16, HM = TM16 / 2;
+  static_assert(NW == 8 && TM16 % 2 == 0, "8 waves, an even number of 16-row blocks per wave");
+  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "row groups must divide over the waves");
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * BKS], A1[3 * BM * BKS], A2[3 * BM * BKS];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS], B2[3 * BN * BKS];
+
+  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7, splits = 1 + ((epi >> 28) & 7);
+  const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
+  epi &= 0xff;
+  if (pb.id < 0) return;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int tiles = tiles_m * tiles_n;
+  const int u = xcd_major_n(pb.id, pb.n, pb.nx);
+  if (u >= tiles * splits) return;
+  const int t = u / splits, sp = u - t * splits;
+  if (splits > 1) C += size_t(sp) * M * N;
+  int mt, nt;
+  tile_rc(t, tiles_m, tiles_n, group, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+  const bool lag = wave >= NW / 2;  // wave-uniform
+
+  f32x4 acc[TM16][TN16];
+#pragma unroll
+  for (int a = 0; a < TM16; ++a)
+#pragma unroll
+    for (int b = 0; b < TN16; ++b) acc[a][b] = f32x4{0};
+
+  const int nk_all = K / BKS, kb = sp * nk_all / splits;
+  const int nk = (sp + 1) * nk_all / splits - kb;
+  uint32_t voff_a[BM / RPI / NW], voff_b[BN / RPI / NW];
+  dma_offsets<BM, NW, BKS, true>(voff_a, m0, M - 1, K, wave, lane);
+  dma_offsets<BN, NW, BKS, true>(voff_b, n0, N - 1, K, wave, lane);
+#define X3T_A(b) ((b) == 0 ? A0 : (b) == 1 ? A1 : A2)
+#define X3T_B(b) ((b) == 0 ? B0 : (b) == 1 ? B1 : B2)
+#define X3T_ISSUE(STAGE, BUF)                                                      \
+  {                                                                                \
+    const int k0_ = (kb + (STAGE)) * BKS;                                          \
+    if (!(ablate & 1)) dma_stage<BM, NW, BKS>(A, a_plane, voff_a, k0_, X3T_A(BUF), wave); \
+    if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3T_B(BUF), wave); \
+  }
+// stage KS in buffer BUF (= KS % 3): every wave's DMA of it has landed after the wait + barrier, and
+// every wave is done with buffer (KS+1) % 3 (read last in stage KS-1 by the lagging half), which
+// stage KS+1 then fills
+#define X3T_ITER(KS, BUF)                                                          \
+  {                                                                                \
+    vm_wait<0>();                                                                  \
+    raw_barrier();                                                                 \
+    if ((KS) + 1 < nk) X3T_ISSUE((KS) + 1, ((BUF) + 1) % 3)                        \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    if (!lag) {                                                                    \
+      compute_rows16<BM, BN, WM, WN, 0, TM16>(acc, X3T_A(BUF), X3T_B(BUF), wm, wn, lane); \
+    } else {                                                                       \
+      if ((KS) > 0)                                                                \
+        compute_rows16<BM, BN, WM, WN, HM, TM16>(acc, X3T_A(((BUF) + 2) % 3), X3T_B(((BUF) + 2) % 3), wm, wn, lane); \
+      compute_rows16<BM, BN, WM, WN, 0, HM>(acc, X3T_A(BUF), X3T_B(BUF), wm, wn, lane); \
+    }                                                                              \
+  }
+  if (nk > 0) X3T_ISSUE(0, 0)
+  for (int ks = 0; ks < nk; ks += 3) {
+    X3T_ITER(ks, 0)
+    if (ks + 1 < nk) X3T_ITER(ks + 1, 1)
+    if (ks + 2 < nk) X3T_ITER(ks + 2, 2)
+  }
+  // the lagging half's last half-stage: no DMA is issued any more, so its buffer is still intact
+  if (lag && nk > 0) {
+    const int last = (nk - 1) % 3;
+    if (last == 0)
+      compute_rows16<BM, BN, WM, WN, HM, TM16>(acc, A0, B0, wm, wn, lane);
+    else if (last == 1)
+      compute_rows16<BM, BN, WM, WN, HM, TM16>(acc, A1, B1, wm, wn, lane);
+    else
+      compute_rows16<BM, BN, WM, WN, HM, TM16>(acc, A2, B2, wm, wn, lane);
+  }
+#undef X3T_ITER
+#undef X3T_ISSUE
+#undef X3T_B
+#undef X3T_A
+  vm_wait<0>();
+  if (!(ablate & 4))
+    store_tile16<TM16, TN16>(acc, m0 + wm * WM, n0 + wn * WN, lane, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+int launch_t(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float* bias, const float* R,
+             const float* R2, int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi,
+             hipStream_t s) {
+  if (N % BN || K % 32) {
+    g_err = "gemm_x3t: N % " + std::to_string(BN) + " and K % 32 must be 0";
+    return -1;
+  }
+  const int tiles = ((M + BM - 1) / BM) * (N / BN) * (1 + ((epi >> 28) & 7));
+  hipLaunchKernelGGL((gemm_x3t<BM, BN, WGM, WGN>), dim3(pinned_grid(tiles, unsigned(epi >> 20) & 0xffu)),
+                     dim3(64 * WGM * WGN), 0, s, A, ap, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("gemm_x3t: ") + hipGetErrorString(e);
+    return int(e);
+  }
+  return 0;
+}
+
 // ---- stream-K partials -------------------------------------------------------------------------
 // The N = 384 GEMMs of the model (projection, fc2) have 162 tiles of 128x64 for 256 CUs: whole-tile
 // grids leave a third of the chip idle (or a 27%-full second round), and split-K only moves the
@@ -976,8 +1125,9 @@ int nos_gemm_x3_set_group(int g) {
 // tiles (three 32-column blocks per wave), so N = 384 / 1536 split into 216 tiles at M = 3401 — one
 // round on 256 CUs instead of 1.3-2.5: 128x192 S2, 64x96 S2 (2 waves), 64x192 S2 (2 waves);
 // 35-37 = 8 waves of 64x64 each (a third fewer LDS fragment bytes per MFMA than 64x32 waves;
-// 144 KB of LDS for two stages): 256x128 S2, 256x128 S2 on 16x16x32, 128x256 S2.
-static const int kCfgX3[38][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// 144 KB of LDS for two stages): 256x128 S2, 256x128 S2 on 16x16x32, 128x256 S2;
+// 38 = the staggered 8-wave 16x16x32 128x128 tile (gemm_x3t, three LDS buffers).
+static const int kCfgX3[39][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
@@ -986,7 +1136,8 @@ static const int kCfgX3[38][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128,
                                   {128, 64, 2}, {64, 128, 2}, {128, 64, 4}, {64, 128, 4},
                                   {64, 64, 2}, {64, 64, 3}, {128, 128, 2}, {32, 64, 2}, {64, 32, 2},
                                   {128, 192, 2}, {64, 96, 2}, {64, 192, 2},
-                                  {256, 128, 2}, {256, 128, 2}, {128, 256, 2}};
+                                  {256, 128, 2}, {256, 128, 2}, {128, 256, 2},
+                                  {128, 128, 3}};
 
 }  // extern "C"
 
@@ -1033,6 +1184,7 @@ static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, cons
     case 36: return launch_d<256, 128, 4, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi,
                                                          s);
     case 37: return launch_d<128, 256, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 38: return launch_t<128, 128, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;
@@ -1041,7 +1193,7 @@ static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, cons
 
 extern "C" {
 
-int nos_gemm_x3_num_configs() { return 38; }
+int nos_gemm_x3_num_configs() { return 39; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
@@ -1082,7 +1234,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
   }
 }
 
-// Split-K partial sums of C = A · W^T (LDS-DMA configs 7..37): plane s of C [splits][M][N] fp32
+// Split-K partial sums of C = A · W^T (LDS-DMA configs 7..38): plane s of C [splits][M][N] fp32
 // holds the K stages [s*nk/splits, (s+1)*nk/splits); no epilogue (the consumer adds the planes in
 // order, then bias and residuals: splitk_layernorm in kernels.hip). 2 <= splits <= min(8, K/stage).
 int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, float* C, int M, int N, int K, int cfg,
@@ -1091,8 +1243,8 @@ int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, flo
     g_err = "gemm_x3 partials: K % 32, plane strides % 8 and an output";
     return -1;
   }
-  if (cfg < 7 || cfg > 37 || splits < 2 || splits > 8 || splits > K / BK) {
-    g_err = "gemm_x3 partials: an LDS-DMA config (7..37) and 2..8 splits";
+  if (cfg < 7 || cfg > 38 || splits < 2 || splits > 8 || splits > K / BK) {
+    g_err = "gemm_x3 partials: an LDS-DMA config (7..38) and 2..8 splits";
     return -1;
   }
   const int epi = (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20) | ((splits - 1) << 28);
@@ -1157,7 +1309,7 @@ int nos_gemm_x3_streamk(const void* A, size_t ap, const void* W, size_t wp, floa
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 37) return -1;
+  if (cfg < 0 || cfg > 38) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];

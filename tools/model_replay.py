@@ -49,7 +49,7 @@ def main() -> int:
         print(f"{a.slice}: {dt * 1e3:.3f} ms per inference over {a.replays} replays", flush=True)
         if a.tables:
             from walkai_nos_amd.ops import gemm as G
-            print(json.dumps({"x3": G.x3_table(), "linear_residual_ln": G.fused_table(),
+            print(json.dumps({"x3": G.x3_table(), "x3_us": G.x3_timings(), "linear_residual_ln": G.fused_table(),
                               "linear_residual_ln_us": G.fused_timings()}, indent=1), flush=True)
         del g
     return 0

@@ -223,16 +223,21 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             # persistent stream-of-stages (grid = resident slots of the slice)
             100: (64, 64, 3, "p"), 101: (64, 64, 2, "p"), 102: (128, 128, 3, "p8"), 103: (64, 128, 3, "p"),
             104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
-            108: (128, 64, 4, "p"), 109: (64, 128, 4, "p"), 110: (256, 128, 2, "p8")}
+            108: (128, 64, 4, "p"), 109: (64, 128, 4, "p"), 110: (256, 128, 2, "p8"),
+            # 8 waves on 16x16x32, the second half of the workgroup half a stage behind its SIMD
+            # partners (gemm_x3t): three LDS buffers, one stage of DMA in flight
+            38: (128, 128, 3, "t16w8")}
 #: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
 X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
                    18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 3, 28: 2, 29: 1, 30: 4, 31: 4,
-                   32: 1, 33: 2, 34: 1, 35: 1, 36: 1, 37: 1,
+                   32: 1, 33: 2, 34: 1, 35: 1, 36: 1, 37: 1, 38: 1,
                    100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1, 110: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int, int], int] = {}
+#: the x3 tuner's timings per key (ms for 3 graph-replayed calls), for tools/model_replay.py --tables
+_x3_times: Dict[Tuple[int, int, int, int, int, int, int], Dict[int, float]] = {}
 _x3_bound = False
 
 
@@ -435,6 +440,7 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
                 tile = min(times, key=times.get)
                 with _lock:
                     _x3_cache[key] = tile
+                    _x3_times[key] = times
     _launch_x3(tile, a3, w3, bias, res, r2, o, o3, epi)
     rf = None if o is None else (o.view(*lead, N) if out is None else out)
     r3 = None if o3 is None else o3.view(3, *lead, N)
@@ -445,7 +451,7 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
 
 # ---- split-K partials + combine-and-LayerNorm --------------------------------------------------
 #: LDS-DMA tiles offered to the split-K partial path (32x32 MFMA and 16x16 MFMA, 4 and 8 waves)
-SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36)
+SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36, 38)
 SPLIT_COUNTS = (2, 3, 4)
 #: smallest slice that times split-K against the fused path: on 32-CU (CPX) slices the isolated
 #: timing picks split-K, but with all eight partitions busy the fused path serves 2% more
@@ -600,6 +606,15 @@ def x3_table() -> Dict[str, str]:
     with _lock:
         return {f"M{m}_N{n}_K{k}_epi{e}_out{o}_cus{c}_pin{p}": "x".join(map(str, X3_TILES[v][:2])) + f"/{X3_TILES[v][3]}"
                 + f" ({v})" for (m, n, k, e, o, c, p), v in sorted(_x3_cache.items())}
+
+
+def x3_timings(top: int = 6) -> Dict[str, Dict[str, float]]:
+    """The fastest ``top`` tiles the x3 tuner timed per key: ``BMxBN/<kind> (id)`` -> µs per call."""
+    with _lock:
+        return {f"M{m}_N{n}_K{k}_epi{e}_out{o}_cus{c}_pin{p}":
+                {"x".join(map(str, X3_TILES[t][:2])) + f"/{X3_TILES[t][3]} ({t})": round(ms * 1000 / 3, 2)
+                 for t, ms in sorted(v.items(), key=lambda x: x[1])[:top]}
+                for (m, n, k, e, o, c, p), v in sorted(_x3_times.items())}
 
 
 def fused_timings() -> Dict[str, Dict[str, float]]:
