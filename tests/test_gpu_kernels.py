@@ -280,9 +280,11 @@ def test_attention_x3_asymmetric_values(K):
 
 @pytest.mark.parametrize("M,N,Kd", [(3401, 384, 384), (3401, 1152, 384), (3401, 1536, 384), (3401, 384, 1536),
                                     (3300, 384, 768), (100, 128, 64), (1, 128, 32)])
-def test_gemm_x3_every_tile_epilogue_and_output(K, M, N, Kd):
-    # fp32-accurate: the x3 GEMM's error vs fp64 stays within 2x the f32-input MFMA GEMM's
+def test_gemm_x3_every_tile_epilogue_and_output(K, M, N, Kd, monkeypatch):
+    # fp32-accurate: the x3 GEMM's error vs fp64 stays within 2x the f32-input MFMA GEMM's (every
+    # tile, the opt-in staggered one included)
     from walkai_nos_amd.ops import gemm as G
+    monkeypatch.setenv("NOS_X3_STAGGER", "1")
     torch.manual_seed(0)
     x = torch.randn(M, Kd, device="cuda")
     w = torch.randn(N, Kd, device="cuda") * 0.05
@@ -416,11 +418,12 @@ def test_patch_planes_equal_im2col_split(K):
 
 
 @pytest.mark.parametrize("M,N,Kd", [(3401, 384, 1536), (3401, 384, 384), (300, 768, 256)])
-def test_splitk_partials_and_combine_layernorm(K, M, N, Kd):
-    # split-K partial GEMM (every offered tile x split count) + the combine/residual/LayerNorm kernel
-    # vs fp64; the partial planes sum to the unsplit product
+def test_splitk_partials_and_combine_layernorm(K, M, N, Kd, monkeypatch):
+    # split-K partial GEMM (every offered tile x split count, the opt-in staggered tile included) +
+    # the combine/residual/LayerNorm kernel vs fp64; the partial planes sum to the unsplit product
     import torch.nn.functional as F
     from walkai_nos_amd.ops import gemm as G
+    monkeypatch.setenv("NOS_X3_STAGGER", "1")
     torch.manual_seed(8)
     x3 = K.split3(torch.randn(M, Kd, device="cuda"))
     w = torch.randn(N, Kd, device="cuda") * 0.05

@@ -225,7 +225,8 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             104: (128, 64, 3, "p"), 105: (64, 64, 2, "p64"), 106: (64, 32, 2, "p64"), 107: (128, 64, 2, "p864"),
             108: (128, 64, 4, "p"), 109: (64, 128, 4, "p"), 110: (256, 128, 2, "p8"),
             # 8 waves on 16x16x32, the second half of the workgroup half a stage behind its SIMD
-            # partners (gemm_x3t): three LDS buffers, one stage of DMA in flight
+            # partners (gemm_x3t): three LDS buffers, one stage of DMA in flight. Opt-in
+            # (NOS_X3_STAGGER=1): measured 1-5% slower than tile 29 (profiles/gemm_stagger_ab_r4.json)
             38: (128, 128, 3, "t16w8")}
 #: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
 X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
@@ -306,9 +307,10 @@ def x3_eligible(N: int, Kd: int) -> list:
     skip = tuple(x for x in os.environ.get("NOS_X3_EXCLUDE", "").split(",") if x)
     drop = {int(x) for x in os.environ.get("NOS_X3_DROP", "").split(",") if x}
     min_area = int(os.environ.get("NOS_X3_MIN_TILE", "0"))
+    stagger = os.environ.get("NOS_X3_STAGGER", "0") == "1"  # the staggered tile: measured slower, opt-in
     return [c for c, (bm, bn, _, kind) in X3_TILES.items()
             if N % bn == 0 and (not kind.endswith("64") or Kd % 64 == 0) and not (skip and kind.startswith(skip))
-            and bm * bn >= min_area and c not in drop]
+            and bm * bn >= min_area and c not in drop and (stagger or not kind.startswith("t"))]
 
 
 #: tiles at least this large (BM*BN) on a partition that shares the GPU with sibling partitions
@@ -535,6 +537,8 @@ def split_candidates(N: int, Kd: int) -> list:
     out = []
     for c in SPLIT_TILES:
         bm, bn, _, kind = X3_TILES[c]
+        if kind.startswith("t") and os.environ.get("NOS_X3_STAGGER", "0") != "1":
+            continue
         bk = 64 if kind.endswith("64") else 32
         if N % bn or Kd % bk:
             continue
