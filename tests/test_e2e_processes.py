@@ -263,6 +263,61 @@ def test_quota_reclaim_that_needs_a_mode_flip_over_processes():
             c.stop()
 
 
+def test_quota_reclaim_on_a_sliced_gpu_over_processes():
+    """ERQ on a sliced GPU with every component a process: team A borrows team B's half of the one
+    GPU (8 x 1/8 pods, min 144 GB each); team B's 1/2 pod reclaims it. nos-scheduler evicts only the
+    A pods whose row groups B's slice needs (4 of them: an aligned half), the agent re-carves the
+    freed groups into B's slice without a mode switch, and A keeps its guaranteed half running."""
+    import json
+    from walkai_nos_amd.api import v1alpha1 as api
+    from walkai_nos_amd.cmd.devcluster import fast_partitioner_config
+
+    def quota(ns):
+        return {"apiVersion": api.API_VERSION, "kind": api.KIND_ELASTIC_QUOTA,
+                "metadata": {"name": f"q-{ns}", "namespace": ns},
+                "spec": {"min": {api.RESOURCE_GPU_MEMORY: "144"}}}
+
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=1, quota=True, bookmark_every=2.0, layout="slices",
+                       partitioner=fast_partitioner_config(sliceReserveAfterSeconds=1))
+        try:
+            c.start()
+            kubelet = c.kubelets[NODE]
+            c.run_until(lambda: ko.annotations(c.client.get("Node", NODE)).get(api.ANNOTATION_SLICED_GPUS_STATUS) == "0",
+                        30, "the GPU to be served sliced")
+            for ns in ("team-a", "team-b"):
+                c.client.create(quota(ns))
+            for i in range(8):
+                c.submit(f"a{i}", "cpx_nps1", namespace="team-a", scheduler_name="nos-scheduler")
+            c.run_until(lambda: all(c.phase(f"a{i}", "team-a") == "Running" for i in range(8)), 90,
+                        "team A on the whole GPU in 1/8 slices")
+            c.submit("b0", "dpx_nps1", namespace="team-b", scheduler_name="nos-scheduler")
+            c.run_until(lambda: c.phase("b0", "team-b") == "Running", 120, "team B's half of the GPU")
+            running_a = [ko.name(p) for p in c.client.list("Pod", "team-a")
+                         if p.get("status", {}).get("phase") == "Running"]
+            assert len(running_a) == 4, running_a            # only the pods on B's half were evicted
+            mask = kubelet.envs[("team-b", "b0")]["HSA_CU_MASK"]
+            b_cus = set()
+            for r in mask.split(":", 1)[1].split(","):
+                lo, _, hi = r.partition("-")
+                b_cus.update(range(int(lo), int(hi or lo) + 1))
+            assert len(b_cus) == 128
+            for n in running_a:                              # B's CUs are disjoint from A's survivors
+                m = kubelet.envs[("team-a", n)]["HSA_CU_MASK"]
+                a_cus = set()
+                for r in m.split(":", 1)[1].split(","):
+                    lo, _, hi = r.partition("-")
+                    a_cus.update(range(int(lo), int(hi or lo) + 1))
+                assert not (a_cus & b_cus), (n, m, mask)
+            path = os.path.join(d, NODE, "fake-amdsmi.json")
+            if os.path.exists(path):                         # written on every amd-smi mode change
+                with open(path) as f:
+                    assert [g["compute"].upper() for g in json.load(f)] == ["SPX"]
+            assert kubelet.admission_failures == []
+        finally:
+            c.stop()
+
+
 def test_slice_agent_process_serves_cu_mask_slices():
     """A cumask node: the partitioner plans CU-mask slices for pending slice pods, the slice agent
     process materialises them in its slice store and its device plugin serves them; kubelet's
