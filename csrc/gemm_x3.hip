@@ -1126,10 +1126,8 @@ int nos_gemm_x3_set_group(int g) {
 // round on 256 CUs instead of 1.3-2.5: 128x192 S2, 64x96 S2 (2 waves), 64x192 S2 (2 waves);
 // 35-37 = 8 waves of 64x64 each (a third fewer LDS fragment bytes per MFMA than 64x32 waves;
 // 144 KB of LDS for two stages): 256x128 S2, 256x128 S2 on 16x16x32, 128x256 S2;
-// 38 = the staggered 8-wave 16x16x32 128x128 tile (gemm_x3t, three LDS buffers);
-// 39-42 = two-buffer 4-wave tiles small enough for two workgroups per CU (74 KB of LDS: four waves
-// per SIMD to hide the operand stream's latency): 128x64, 64x128, and the same on 16x16x32.
-static const int kCfgX3[43][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
+// 38 = the staggered 8-wave 16x16x32 128x128 tile (gemm_x3t, three LDS buffers).
+static const int kCfgX3[39][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128, 128, 2},
                                   {64, 64, 1}, {128, 64, 1}, {64, 128, 1},
                                   {64, 64, 3}, {64, 64, 4}, {128, 64, 3}, {64, 128, 3},
                                   {128, 128, 3}, {64, 64, 2}, {128, 128, 3}, {128, 128, 2},
@@ -1139,7 +1137,7 @@ static const int kCfgX3[43][3] = {{64, 64, 2}, {128, 64, 2}, {64, 128, 2}, {128,
                                   {64, 64, 2}, {64, 64, 3}, {128, 128, 2}, {32, 64, 2}, {64, 32, 2},
                                   {128, 192, 2}, {64, 96, 2}, {64, 192, 2},
                                   {256, 128, 2}, {256, 128, 2}, {128, 256, 2},
-                                  {128, 128, 3}, {128, 64, 2}, {64, 128, 2}, {128, 64, 2}, {64, 128, 2}};
+                                  {128, 128, 3}};
 
 }  // extern "C"
 
@@ -1187,10 +1185,6 @@ static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, cons
                                                          s);
     case 37: return launch_d<128, 256, 2, 4, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     case 38: return launch_t<128, 128, 2, 4>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 39: return launch_d<128, 64, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 40: return launch_d<64, 128, 2, 2, 2>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 41: return launch_d<128, 64, 2, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
-    case 42: return launch_d<64, 128, 2, 2, 2, 32, true>(a, ap, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
     default:
       g_err = "gemm_x3: unknown tile config";
       return -1;
@@ -1199,7 +1193,7 @@ static int dispatch(const __bf16* a, size_t ap, const __bf16* w, size_t wp, cons
 
 extern "C" {
 
-int nos_gemm_x3_num_configs() { return 43; }
+int nos_gemm_x3_num_configs() { return 39; }
 
 // Persistent stream-of-stages GEMM (same operands/epilogue as nos_gemm_x3) with an explicit grid
 // (workgroups; the caller sizes it to the slice: CUs x resident workgroups per CU).
@@ -1240,7 +1234,7 @@ int nos_gemm_x3_persistent(const void* A, size_t ap, const void* W, size_t wp, c
   }
 }
 
-// Split-K partial sums of C = A · W^T (LDS-DMA configs 7..42): plane s of C [splits][M][N] fp32
+// Split-K partial sums of C = A · W^T (LDS-DMA configs 7..38): plane s of C [splits][M][N] fp32
 // holds the K stages [s*nk/splits, (s+1)*nk/splits); no epilogue (the consumer adds the planes in
 // order, then bias and residuals: splitk_layernorm in kernels.hip). 2 <= splits <= min(8, K/stage).
 int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, float* C, int M, int N, int K, int cfg,
@@ -1249,8 +1243,8 @@ int nos_gemm_x3_partials(const void* A, size_t ap, const void* W, size_t wp, flo
     g_err = "gemm_x3 partials: K % 32, plane strides % 8 and an output";
     return -1;
   }
-  if (cfg < 7 || cfg > 42 || splits < 2 || splits > 8 || splits > K / BK) {
-    g_err = "gemm_x3 partials: an LDS-DMA config (7..42) and 2..8 splits";
+  if (cfg < 7 || cfg > 38 || splits < 2 || splits > 8 || splits > K / BK) {
+    g_err = "gemm_x3 partials: an LDS-DMA config (7..38) and 2..8 splits";
     return -1;
   }
   const int epi = (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20) | ((splits - 1) << 28);
@@ -1315,7 +1309,7 @@ int nos_gemm_x3_streamk(const void* A, size_t ap, const void* W, size_t wp, floa
 }
 
 int nos_gemm_x3_tile(int cfg, int* bm, int* bn, int* nbuf) {
-  if (cfg < 0 || cfg > 42) return -1;
+  if (cfg < 0 || cfg > 38) return -1;
   *bm = kCfgX3[cfg][0];
   *bn = kCfgX3[cfg][1];
   *nbuf = kCfgX3[cfg][2];

@@ -19,3 +19,6 @@ for rep in a b; do
     done
   done
 done
+rm -f gpurun_out/multiproc_fair.json gpurun_out/multiproc_fair.log
+NOS_FAIR_ONLY=shared_5,shared_7 NOS_FAIR_VARIANTS='_q3a|{"GPU_MAX_HW_QUEUES":"3"}|0 _q3b|{"GPU_MAX_HW_QUEUES":"3"}|0' \
+  bash tools/gpu_fair.sh

@@ -227,16 +227,14 @@ X3_TILES = {0: (64, 64, 2, "r"), 1: (128, 64, 2, "r"), 2: (64, 128, 2, "r"), 3: 
             # 8 waves on 16x16x32, the second half of the workgroup half a stage behind its SIMD
             # partners (gemm_x3t): three LDS buffers, one stage of DMA in flight. Opt-in
             # (NOS_X3_STAGGER=1): measured 1-5% slower than tile 29 (profiles/gemm_stagger_ab_r4.json)
-            38: (128, 128, 3, "t16w8"),
-            # two-buffer 4-wave tiles at 74 KB of LDS: two workgroups (four waves per SIMD) per CU
-            39: (128, 64, 2, "d2wg"), 40: (64, 128, 2, "d2wg"), 41: (128, 64, 2, "m16x2"), 42: (64, 128, 2, "m16x2")}
+            38: (128, 128, 3, "t16w8")}
 #: persistent (stream-of-stages) configs: the grid is the slice's resident workgroup slots
 X3_PERSISTENT = frozenset(c for c, t in X3_TILES.items() if t[3].startswith("p"))
 #: resident workgroups per CU (LDS- or VGPR-limited)
 X3_SLOTS_PER_CU = {0: 2, 1: 1, 2: 1, 3: 1, 4: 5, 5: 3, 6: 3, 7: 2, 8: 1, 9: 1, 10: 1, 11: 1, 12: 3,
                    13: 1, 14: 1, 15: 2, 16: 4, 17: 4,
                    18: 1, 19: 1, 20: 2, 21: 2, 22: 1, 23: 1, 24: 1, 25: 1, 26: 1, 27: 3, 28: 2, 29: 1, 30: 4, 31: 4,
-                   32: 1, 33: 2, 34: 1, 35: 1, 36: 1, 37: 1, 38: 1, 39: 2, 40: 2, 41: 2, 42: 2,
+                   32: 1, 33: 2, 34: 1, 35: 1, 36: 1, 37: 1, 38: 1,
                    100: 2, 101: 3, 102: 1, 103: 1, 104: 1, 105: 1, 106: 2, 107: 1, 108: 1, 109: 1, 110: 1}
 _x3_cache: Dict[Tuple[int, int, int, int, int, int, int], int] = {}
 #: the x3 tuner's timings per key (ms for 3 graph-replayed calls), for tools/model_replay.py --tables
@@ -455,7 +453,7 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
 
 # ---- split-K partials + combine-and-LayerNorm --------------------------------------------------
 #: LDS-DMA tiles offered to the split-K partial path (32x32 MFMA and 16x16 MFMA, 4 and 8 waves)
-SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36, 38, 39, 40, 41, 42)
+SPLIT_TILES = (7, 9, 10, 11, 12, 13, 14, 18, 23, 24, 29, 32, 35, 36, 38)
 SPLIT_COUNTS = (2, 3, 4)
 #: smallest slice that times split-K against the fused path: on 32-CU (CPX) slices the isolated
 #: timing picks split-K, but with all eight partitions busy the fused path serves 2% more
