@@ -465,6 +465,38 @@ def test_component_restarts_and_a_kubelet_restart():
             c.stop()
 
 
+def test_sliced_agent_restart_keeps_the_slices_over_processes():
+    """A sliced GPU across a partition-agent restart: the slice layout lives in the agent's state
+    file (``sliceStateFile``), so the restarted agent reports the same sliced GPU and serves the
+    same slice ids — the running pods' devices stay healthy, no slice is re-carved under them — and
+    a pod submitted afterwards is carved into the free groups next to them."""
+    from walkai_nos_amd.api import v1alpha1 as api
+    from walkai_nos_amd.cmd.devcluster import fast_partitioner_config
+    with tempfile.TemporaryDirectory() as d:
+        c = DevCluster(d, nodes=1, gpus=1, bookmark_every=2.0, layout="slices",
+                       partitioner=fast_partitioner_config(sliceReserveAfterSeconds=1))
+        try:
+            c.start()
+            k = c.kubelets[NODE]
+            c.run_until(lambda: ko.annotations(c.client.get("Node", NODE)).get(api.ANNOTATION_SLICED_GPUS_STATUS) == "0",
+                        30, "the GPU to be served sliced")
+            c.submit("half", "dpx_nps1")
+            c.submit("e0", "cpx_nps1")
+            c.run_until(lambda: c.phase("half") == "Running" and c.phase("e0") == "Running", 60, "the first pods")
+            ids = {n: k.used[("default", n)][1] for n in ("half", "e0")}
+            c.restart("partitionagent-node-0")
+            c.run_until(lambda: ko.annotations(c.client.get("Node", NODE)).get(api.ANNOTATION_SLICED_GPUS_STATUS) == "0"
+                        and set(ids.values()) <= set(k.healthy("amd.com/dpx_nps1") + k.healthy("amd.com/cpx_nps1")),
+                        30, "the restarted agent to serve the same slices")
+            c.submit("quarter", "qpx_nps1")
+            c.run_until(lambda: c.phase("quarter") == "Running", 60, "a 1/4 pod next to the running ones")
+            assert all(c.phase(n) == "Running" for n in ("half", "e0"))
+            assert {n: k.used[("default", n)][1] for n in ("half", "e0")} == ids
+            assert k.admission_failures == []
+        finally:
+            c.stop()
+
+
 def test_partitioner_leader_election_failover_over_rest():
     """Two partitioner replicas with leader election (a coordination.k8s.io Lease over the REST
     API): one holds the lease; the leader is killed; the standby takes the lease over once it
