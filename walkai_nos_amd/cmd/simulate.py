@@ -39,7 +39,8 @@ def main(argv=None) -> int:
     logging.basicConfig(level=logging.WARNING)
     if args.scenario == "erq":
         from ..sim.erq import run_erq_churn
-        r = run_erq_churn(gpus=args.gpus, epochs=args.epochs, seed=args.seed, cluster_s=args.cluster_s)
+        r = run_erq_churn(gpus=args.gpus, epochs=args.epochs, seed=args.seed, cluster_s=args.cluster_s,
+                          layout=args.layout)
         samples = r.pop("samples")
         if not args.quiet:
             for x in samples:

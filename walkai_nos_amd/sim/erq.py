@@ -43,9 +43,13 @@ def _stats(v: List[float]) -> Dict[str, float]:
 
 
 def run_erq_churn(gpus: int = 8, epochs: int = 60, b_start: int = 20, seed: int = 1, cluster_s: float = 60.0,
-                  lifetime=(2, 6), load_a: float = 1.0, load_b: float = 0.5, memory_gb: int = 288) -> Dict[str, Any]:
+                  lifetime=(2, 6), load_a: float = 1.0, load_b: float = 0.5, memory_gb: int = 288,
+                  layout: str = "partitions") -> Dict[str, Any]:
+    """``layout``: the node's ``xcp-layout`` (partitions: hardware modes, a reclaim may need a flip;
+    slices: sliced GPUs, a reclaim evicts only the pods on the row groups it needs)."""
     rng = random.Random(seed)
-    c = SimCluster(n_nodes=1, gpus_per_node=gpus, kind=api.PARTITIONING_KIND_XCP, elastic_quota=True, policy="pack")
+    c = SimCluster(n_nodes=1, gpus_per_node=gpus, kind=api.PARTITIONING_KIND_XCP, elastic_quota=True, policy="pack",
+                   xcp_layout=layout)
     c.run(30)
     share = gpus * memory_gb // 2
     for team in ("team-a", "team-b"):
