@@ -843,35 +843,37 @@ def _per_pod_spread(got: Dict[Any, int], keys: List[Any], dt: float) -> Dict[str
 
 def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 1.0) -> Dict[str, Any]:
     """Saturate a fresh node through the control plane, then serve every pod on this rank's GPU
-    at once: 8 CPX pods per GPU, then a CU-mask node with dedicated-CU + memory-only slices."""
+    at once: 8 CPX pods per GPU (as partitions, then on sliced GPUs), then a CU-mask node with
+    dedicated-CU + memory-only slices."""
     import torch
 
     from .api import v1alpha1 as api
     from .models.slicing.cumask import cus_of
     from .sim.cluster import SimCluster
     out: Dict[str, Any] = {}
-    # compute partitions: 8 x 1/8-GPU pods per GPU
-    c = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy)
-    c.run(30)
-    for i in range(8 * cfg.gpus):
-        c.submit({"amd.com/cpx_nps1": 1}, name=f"d{i}")
-    c.run(120)
-    sn = next(iter(c.nodes.values()))
-    per_gpu = collections.Counter(sn.smi.resolve(d).gpu_index for devs in sn.kubelet.allocations.values()
-                                  for _, d in devs)
-    out["xcp"] = {"pods_per_gpu": round(sum(per_gpu.values()) / cfg.gpus, 2),
-                  "pods_per_gpu_min": min(per_gpu.get(g, 0) for g in range(cfg.gpus)),
-                  "pods_per_node": sum(per_gpu.values()), "pending": len(c.pending_pods())}
-    if data is not None:
-        keys = [("cpx_nps1", sn.smi.resolve(d).partition_index) for devs in sn.kubelet.allocations.values()
-                for _, d in devs if sn.smi.resolve(d).gpu_index == cfg.rank]
-        t0 = time.perf_counter()
-        got = data.serve(keys, t0 + serve_s)
-        data.drain_all()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        out["xcp"]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
-        out["xcp"]["per_pod"] = _per_pod_spread(got, keys, dt)
+    # 8 x 1/8-GPU pods per GPU: as CPX compute partitions (a flip) and on sliced GPUs (no flip)
+    for name, layout in (("xcp", "partitions"), ("xcp_slices", "slices")):
+        c = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, policy=cfg.policy, xcp_layout=layout)
+        c.run(30)
+        for i in range(8 * cfg.gpus):
+            c.submit({"amd.com/cpx_nps1": 1}, name=f"d{i}")
+        c.run(120)
+        sn = next(iter(c.nodes.values()))
+        per_gpu = collections.Counter(sn.smi.resolve(d).gpu_index for devs in sn.kubelet.allocations.values()
+                                      for _, d in devs)
+        out[name] = {"pods_per_gpu": round(sum(per_gpu.values()) / cfg.gpus, 2),
+                     "pods_per_gpu_min": min(per_gpu.get(g, 0) for g in range(cfg.gpus)),
+                     "pods_per_node": sum(per_gpu.values()), "pending": len(c.pending_pods()),
+                     "flips": len(sn.smi.set_calls)}
+        if data is not None:
+            keys = sorted(set(pod_keys(sn, cfg.rank).values()), key=str)
+            t0 = time.perf_counter()
+            got = data.serve(keys, t0 + serve_s)
+            data.drain_all()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            out[name]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
+            out[name]["per_pod"] = _per_pod_spread(got, keys, dt)
     # CU-mask slices beyond 8 per GPU
     for variant, mix in CUMASK_DENSITY.items():
         c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
