@@ -965,6 +965,155 @@ int launch_t(const __bf16* A, size_t ap, const __bf16* W, size_t wp, const float
   return 0;
 }
 
+// ---- fp32 A operand, split in the kernel -------------------------------------------------------
+// The x3 GEMMs are bound by the latency of their operand stream (profiles/pmc_r4_gemm_spx.json:
+// waves wait 40-49% of their cycles, the matrix pipe is 16-26% busy). Three bf16 planes are 6 B per
+// element where fp32 is 4: here the activation operand arrives as fp32 rows and each thread splits
+// its 8-value chunk into the three planes in registers (round to nearest even, the same split the
+// producers use, so the planes — and the result — are bit-identical to the planes-in kernel) and
+// stores them into the swizzled LDS image the 16x16x32 fragment reads expect. The weight planes
+// still come by LDS-DMA. Register-staged A: the next stage's loads are issued before the MFMAs and
+// stashed after them, one stage in flight, as the two-buffer tiles.
+__device__ __forceinline__ void split3_8(const float4& lo, const float4& hi, bf16x8& a, bf16x8& b, bf16x8& c) {
+  typedef float f32x8_t __attribute__((ext_vector_type(8)));
+  const f32x8_t x = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  a = __builtin_convertvector(x, bf16x8);
+  const f32x8_t r = x - __builtin_convertvector(a, f32x8_t);
+  b = __builtin_convertvector(r, bf16x8);
+  c = __builtin_convertvector(r - __builtin_convertvector(b, f32x8_t), bf16x8);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_x3a(const float* __restrict__ A,
+                                                              const __bf16* __restrict__ W, size_t w_plane,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ R,
+                                                              const float* __restrict__ R2, int r2_rows,
+                                                              float* __restrict__ C, __bf16* __restrict__ Cp,
+                                                              size_t c_plane, int M, int N, int K, int epi) {
+  constexpr int NW = WGM * WGN, BKS = 32, RPI = 16;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
+  constexpr int TM16 = WM / 16, TN16 = WN / 16;
+  constexpr int AC = BM * 4 / (64 * NW);  // 16-B chunks (8 k-values) of the A stage per thread
+  static_assert(AC >= 1 && BM * 4 % (64 * NW) == 0, "A stage chunks must divide over the threads");
+  static_assert(BN % (RPI * NW) == 0, "row groups must divide over the waves");
+  __shared__ __attribute__((aligned(16))) __bf16 A0[3 * BM * BKS], A1[3 * BM * BKS];
+  __shared__ __attribute__((aligned(16))) __bf16 B0[3 * BN * BKS], B1[3 * BN * BKS];
+
+  const int group = (epi >> 8) & 0xff, ablate = (epi >> 16) & 7, splits = 1 + ((epi >> 28) & 7);
+  const PinnedBlock pb = pinned_block(unsigned(epi >> 20) & 0xffu);
+  epi &= 0xff;
+  if (pb.id < 0) return;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM;
+  const int tiles = tiles_m * tiles_n;
+  const int u = xcd_major_n(pb.id, pb.n, pb.nx);
+  if (u >= tiles * splits) return;
+  const int t = u / splits, sp = u - t * splits;
+  if (splits > 1) C += size_t(sp) * M * N;
+  int mt, nt;
+  tile_rc(t, tiles_m, tiles_n, group, mt, nt);
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WGN, wn = wave % WGN;
+
+  f32x4 acc[TM16][TN16];
+#pragma unroll
+  for (int a = 0; a < TM16; ++a)
+#pragma unroll
+    for (int b = 0; b < TN16; ++b) acc[a][b] = f32x4{0};
+
+  const int nk_all = K / BKS, kb = sp * nk_all / splits;
+  const int nk = (sp + 1) * nk_all / splits - kb;
+  uint32_t voff_b[BN / RPI / NW];
+  dma_offsets<BN, NW, BKS, true>(voff_b, n0, N - 1, K, wave, lane);
+  // this thread's A chunks: chunk f = tid + 64*NW*v -> local row f/4, k-chunk f%4; LDS slot
+  // (f%4) ^ swz(row), the layout the DMA writes for the 16x16x32 fragment reads
+  const float* ap[AC];
+  int aoff[AC];
+#pragma unroll
+  for (int v = 0; v < AC; ++v) {
+    const int f = tid + 64 * NW * v, rl = f >> 2, c = f & 3;
+    ap[v] = A + size_t(min(m0 + rl, M - 1)) * K + 8 * c;
+    aoff[v] = rl * BKS + 8 * (c ^ dma_swz<32, true>(rl));
+  }
+  float4 ra[AC][2];
+#define X3A_A(b) ((b) == 0 ? A0 : A1)
+#define X3A_B(b) ((b) == 0 ? B0 : B1)
+#define X3A_LOAD(STAGE)                                                                 \
+  {                                                                                     \
+    const int k0_ = (kb + (STAGE)) * BKS;                                               \
+    if (!(ablate & 2)) dma_stage<BN, NW, BKS>(W, w_plane, voff_b, k0_, X3A_B((STAGE) & 1), wave); \
+    _Pragma("unroll") for (int v = 0; v < AC; ++v) {                                    \
+      ra[v][0] = *reinterpret_cast<const float4*>(ap[v] + k0_);                         \
+      ra[v][1] = *reinterpret_cast<const float4*>(ap[v] + k0_ + 4);                     \
+    }                                                                                   \
+  }
+#define X3A_STASH(BUF)                                                                  \
+  {                                                                                     \
+    __bf16* as_ = X3A_A(BUF);                                                           \
+    _Pragma("unroll") for (int v = 0; v < AC; ++v) {                                    \
+      bf16x8 h0, h1, h2;                                                                \
+      split3_8(ra[v][0], ra[v][1], h0, h1, h2);                                         \
+      *reinterpret_cast<bf16x8*>(as_ + aoff[v]) = h0;                                   \
+      *reinterpret_cast<bf16x8*>(as_ + BM * BKS + aoff[v]) = h1;                        \
+      *reinterpret_cast<bf16x8*>(as_ + 2 * BM * BKS + aoff[v]) = h2;                    \
+    }                                                                                   \
+  }
+// stage KS in buffer BUF: the barrier publishes every thread's A stash and B DMA of it and frees
+// buffer BUF^1 (read in stage KS-1), which stage KS+1 then fills: B by DMA, A loaded into
+// registers now and stashed after this stage's MFMAs
+#define X3A_ITER(KS, BUF)                                                               \
+  {                                                                                     \
+    vm_wait<0>();                                                                       \
+    raw_barrier();                                                                      \
+    const bool next_ = (KS) + 1 < nk;                                                   \
+    if (next_) X3A_LOAD((KS) + 1)                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    compute_rows16<BM, BN, WM, WN, 0, TM16>(acc, X3A_A(BUF), X3A_B(BUF), wm, wn, lane); \
+    if (next_) {                                                                        \
+      vm_wait<0>();                                                                     \
+      X3A_STASH((BUF) ^ 1)                                                              \
+    }                                                                                   \
+  }
+  if (nk > 0) {
+    X3A_LOAD(0)
+    vm_wait<0>();
+    X3A_STASH(0)
+  }
+  for (int ks = 0; ks < nk; ks += 2) {
+    X3A_ITER(ks, 0)
+    if (ks + 1 < nk) X3A_ITER(ks + 1, 1)
+  }
+#undef X3A_ITER
+#undef X3A_STASH
+#undef X3A_LOAD
+#undef X3A_B
+#undef X3A_A
+  vm_wait<0>();
+  if (!(ablate & 4))
+    store_tile16<TM16, TN16>(acc, m0 + wm * WM, n0 + wn * WN, lane, bias, R, R2, r2_rows, C, Cp, c_plane, M, N, epi);
+}
+
+template <int BM, int BN, int WGM, int WGN>
+int launch_a(const float* A, const __bf16* W, size_t wp, const float* bias, const float* R, const float* R2,
+             int r2_rows, float* C, __bf16* Cp, size_t cp, int M, int N, int K, int epi, hipStream_t s) {
+  if (N % BN || K % 32) {
+    g_err = "gemm_x3a: N % " + std::to_string(BN) + " and K % 32 must be 0";
+    return -1;
+  }
+  const int tiles = ((M + BM - 1) / BM) * (N / BN) * (1 + ((epi >> 28) & 7));
+  hipLaunchKernelGGL((gemm_x3a<BM, BN, WGM, WGN>), dim3(pinned_grid(tiles, unsigned(epi >> 20) & 0xffu)),
+                     dim3(64 * WGM * WGN), 0, s, A, W, wp, bias, R, R2, r2_rows, C, Cp, cp, M, N, K, epi);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string("gemm_x3a: ") + hipGetErrorString(e);
+    return int(e);
+  }
+  return 0;
+}
+
 // ---- stream-K partials -------------------------------------------------------------------------
 // The N = 384 GEMMs of the model (projection, fc2) have 162 tiles of 128x64 for 256 CUs: whole-tile
 // grids leave a third of the chip idle (or a 27%-full second round), and split-K only moves the
@@ -1305,6 +1454,32 @@ int nos_gemm_x3_streamk(const void* A, size_t ap, const void* W, size_t wp, floa
     case 3: return launch_k<128, 64, 2, 2, 3>(a, ap, w, wp, C, M, N, K, P, ctl, s);
     case 4: return launch_k<64, 64, 2, 2, 2, 64>(a, ap, w, wp, C, M, N, K, P, ctl, s);
     default: return launch_k<128, 128, 2, 4, 3>(a, ap, w, wp, C, M, N, K, P, ctl, s);
+  }
+}
+
+// C = A · W^T with A as fp32 rows [M][K] (split into planes in the kernel) and W as three bf16
+// planes; epilogue and outputs as nos_gemm_x3. cfg: 0 = 128x128 (8 waves, 16x16x32), 1 = 256x128.
+int nos_gemm_x3_f32a(const float* A, const void* W, size_t wp, const float* bias, const float* R, const float* R2,
+                     int r2_rows, float* C, void* Cp, size_t cp, int M, int N, int K, int epi, int cfg,
+                     void* stream) {
+  if (!A || K % 32 || wp % 8 || cp % 8 || (!C && !Cp)) {
+    g_err = "gemm_x3a: an fp32 A, K % 32, plane strides % 8 and an output are required";
+    return -1;
+  }
+  if (((epi & EPI_BIAS) && !bias) || ((epi & EPI_RES) && !R) || ((epi & EPI_RES2) && (!R2 || r2_rows <= 0))) {
+    g_err = "gemm_x3a: epilogue operand missing";
+    return -1;
+  }
+  const __bf16* w = reinterpret_cast<const __bf16*>(W);
+  __bf16* cpp = reinterpret_cast<__bf16*>(Cp);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  epi |= (g_group_m << 8) | (g_ablate << 16) | int(nos_pin_mask() << 20);
+  switch (cfg) {
+    case 0: return launch_a<128, 128, 2, 4>(A, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    case 1: return launch_a<256, 128, 4, 2>(A, w, wp, bias, R, R2, r2_rows, C, cpp, cp, M, N, K, epi, s);
+    default:
+      g_err = "gemm_x3a: unknown config";
+      return -1;
   }
 }
 

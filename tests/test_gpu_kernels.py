@@ -483,6 +483,24 @@ def test_streamk_partials_and_combine_layernorm(K, M, N, Kd):
     assert ran >= 10
 
 
+@pytest.mark.parametrize("M,N,Kd", [(3401, 1152, 384), (3401, 1536, 384), (300, 256, 64), (1, 128, 32)])
+def test_gemm_x3_fp32_activation_matches_the_planes_kernel(K, M, N, Kd):
+    # the fp32-A kernel splits the activation in registers exactly as split3 does: bit-identical
+    # to the planes-in 16x16x32 8-wave tile of the same shape (29: 128x128, 36: 256x128)
+    from walkai_nos_amd.ops import gemm as G
+    torch.manual_seed(21)
+    x = torch.randn(M, Kd, device="cuda")
+    w = torch.randn(N, Kd, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    for cfg, tile in ((0, 29), (1, 36)):
+        if N % G.X3A_TILES[cfg][1]:
+            continue
+        y, y3 = G.gemm_x3_f32a(x, w, b, gelu=True, out_x3=True, cfg=cfg)
+        r, r3 = G.gemm_x3(K.split3(x), w, b, gelu=True, out_f32=True, out_x3=True, tile=tile)
+        torch.cuda.synchronize()
+        assert torch.equal(y, r) and torch.equal(y3, r3), (cfg, (y - r).abs().max().item())
+
+
 def test_linear_residual_ln_x3_tuned_pipeline(K):
     # whichever pipeline the tuner picks, the result matches the unfused ops
     from walkai_nos_amd.ops import gemm as G

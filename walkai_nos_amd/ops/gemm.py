@@ -253,6 +253,7 @@ def _lib_x3() -> ctypes.CDLL:
         L.nos_gemm_x3_last_error.restype = ctypes.c_char_p
         L.nos_gemm_x3_partials.argtypes = [vp, sz, vp, sz, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_set_group.argtypes = [i32]
+        L.nos_gemm_x3_f32a.argtypes = [vp, vp, sz, vp, vp, vp, i32, vp, vp, sz, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_streamk_map.argtypes = [i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_streamk.argtypes = [vp, sz, vp, sz, vp, i32, i32, i32, i32, i32, vp]
         L.nos_gemm_x3_set_ablate.argtypes = [i32]
@@ -445,6 +446,47 @@ def gemm_x3(a3: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
                     _x3_times[key] = times
     _launch_x3(tile, a3, w3, bias, res, r2, o, o3, epi)
     rf = None if o is None else (o.view(*lead, N) if out is None else out)
+    r3 = None if o3 is None else o3.view(3, *lead, N)
+    if out_f32 and out_x3:
+        return rf, r3
+    return rf if out_f32 else r3
+
+
+# ---- fp32 activation operand (csrc/gemm_x3.hip gemm_x3a) ---------------------------------------
+#: fp32-A configs -> (BM, BN): 8 waves on 16x16x32, A split into planes in the kernel
+X3A_TILES = {0: (128, 128), 1: (256, 128)}
+
+
+def gemm_x3_f32a(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, gelu: bool = False,
+                 residual: Optional[torch.Tensor] = None, residual2: Optional[torch.Tensor] = None,
+                 out_f32: bool = True, out_x3: bool = False, cfg: int = 0):
+    """:func:`gemm_x3` with the activation as fp32 rows ``[..., K]`` (4 B per element instead of
+    three 2-B planes): the kernel splits it into the same planes in registers, so the result is
+    bit-identical to ``gemm_x3(K.split3(x), ...)`` on the 16x16x32 8-wave tile of the same shape."""
+    lead = x.shape[:-1]
+    Kd = x.shape[-1]
+    x2 = x.reshape(-1, Kd)
+    if not x2.is_contiguous():
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    w3 = w if w.dim() == 3 else weight_planes(w)
+    N = w3.shape[1]
+    o = torch.empty(M, N, dtype=torch.float32, device=x.device) if out_f32 else None
+    o3 = torch.empty(3, M, N, dtype=torch.bfloat16, device=x.device) if out_x3 else None
+    res = residual.reshape(M, N).contiguous() if residual is not None else None
+    r2 = residual2.reshape(-1, N).contiguous() if residual2 is not None else None
+    epi = (EPI_BIAS if bias is not None else 0) | (EPI_GELU if gelu else 0) | (EPI_RES if residual is not None else 0) \
+        | (EPI_RES2 if residual2 is not None else 0)
+    rc = _lib_x3().nos_gemm_x3_f32a(x2.data_ptr(), w3.data_ptr(), w3[0].numel(),
+                                    bias.data_ptr() if bias is not None else None,
+                                    res.data_ptr() if res is not None else None,
+                                    r2.data_ptr() if r2 is not None else None, r2.shape[0] if r2 is not None else 0,
+                                    o.data_ptr() if o is not None else None,
+                                    o3.data_ptr() if o3 is not None else None, o3[0].numel() if o3 is not None else 0,
+                                    M, N, Kd, epi, cfg, torch.cuda.current_stream().cuda_stream)
+    if rc != 0:
+        raise RuntimeError(f"nos gemm_x3 f32a failed: {_lib_x3().nos_gemm_x3_last_error().decode()} (rc={rc})")
+    rf = None if o is None else o.view(*lead, N)
     r3 = None if o3 is None else o3.view(3, *lead, N)
     if out_f32 and out_x3:
         return rf, r3
