@@ -233,6 +233,34 @@ int nos_smi_process_count(uint32_t idx) {
   return int(n);
 }
 
+// Per-process VRAM on this processor (the HBM budget guard's input): fills up to cap (pid, bytes)
+// pairs and returns how many processes hold a context (may exceed cap), or -1.
+int nos_smi_process_memory(uint32_t idx, uint32_t* pids, uint64_t* vram, uint32_t cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (handle(idx, &h)) return -1;
+  uint32_t n = 0;
+  amdsmi_status_t st = amdsmi_get_gpu_process_list(h, &n, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) {
+    map_status(st, "amdsmi_get_gpu_process_list");
+    return -1;
+  }
+  if (n == 0 || cap == 0) return int(n);
+  std::vector<amdsmi_proc_info_t> list(n);
+  uint32_t got = n;
+  st = amdsmi_get_gpu_process_list(h, &got, list.data());
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) {
+    map_status(st, "amdsmi_get_gpu_process_list");
+    return -1;
+  }
+  uint32_t k = got < n ? got : n;
+  for (uint32_t i = 0; i < k && i < cap; ++i) {
+    pids[i] = uint32_t(list[i].pid);
+    vram[i] = list[i].memory_usage.vram_mem ? list[i].memory_usage.vram_mem : list[i].mem;
+  }
+  return int(got);
+}
+
 int nos_smi_activity(uint32_t idx, uint32_t* gfx, uint32_t* umc, uint32_t* mm) {
   std::lock_guard<std::mutex> lk(g_mu);
   amdsmi_processor_handle h;

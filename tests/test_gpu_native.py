@@ -359,3 +359,69 @@ def test_agent_process_serves_the_real_gpu(gpu):
             assert "libamdhip64" not in maps
         finally:
             c.stop()
+
+
+def test_hbm_guard_sees_a_process_that_bypasses_the_budget_shim(gpu, tmp_path):
+    """The HBM guard's input is amd-smi's per-process VRAM, not the container's own interposer: a
+    process given a 1 GiB slice budget that runs WITHOUT the shim and holds 3 GiB is found over
+    budget (attributed by the NOS_SLICE_IDS Allocate set), and a neighbour that runs with the shim
+    inside a 4 GiB budget is not. Prints the VRAM amd-smi charges beyond torch's allocation (the
+    guard's slack).
+
+    amd-smi reports host PIDs (the KFD's); this test runs in the box's PID namespace, where they do
+    not resolve (the agent DaemonSet runs with hostPID: true instead). So the test maps them itself:
+    the two processes that appear in amd-smi's list after the children start, told apart by size,
+    get a stand-in /proc entry holding the child's real environment."""
+    import time
+    from types import SimpleNamespace
+
+    from walkai_nos_amd.controllers.hbmguard import HbmGuard
+    from walkai_nos_amd.device.amdsmi import NativeAmdSmi
+    shim = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
+    code = ("import sys, torch\n"
+            "a = torch.empty(int(sys.argv[1]), dtype=torch.uint8, device='cuda')\n"
+            "a.fill_(1); torch.cuda.synchronize()\n"
+            "print('READY', flush=True)\n"
+            "sys.stdin.read()\n")
+    env0 = {k: v for k, v in os.environ.items() if k != "LD_PRELOAD"}
+    smi = NativeAmdSmi()
+    before = set(smi.process_memory(0))
+    rogue = subprocess.Popen([sys.executable, "-c", code, str(3 * 2**30)], stdin=subprocess.PIPE,
+                             stdout=subprocess.PIPE, text=True, env=dict(env0, NOS_SLICE_IDS="gpu0::s0"))
+    good = subprocess.Popen([sys.executable, "-c", code, str(2**30)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                            text=True, env=dict(env0, NOS_SLICE_IDS="gpu0::s1", LD_PRELOAD=shim,
+                                                NOS_HBM_LIMIT_BYTES=str(4 * 2**30)))
+    try:
+        for p in (rogue, good):
+            t0 = time.time()
+            line = p.stdout.readline()
+            assert "READY" in line, (line, time.time() - t0)
+        seen = smi.process_memory(0)
+        new = {pid: b for pid, b in seen.items() if pid not in before and b > 0}
+        print("amd-smi per-process VRAM of the children:", new)
+        assert len(new) == 2, seen
+        host_rogue, host_good = sorted(new, key=new.get, reverse=True)
+        assert new[host_rogue] >= 3 * 2**30 > new[host_good] >= 2**30, new
+        print("beyond torch's allocation (B):", new[host_rogue] - 3 * 2**30, new[host_good] - 2**30)
+        proc = tmp_path / "proc"
+        for host, child in ((host_rogue, rogue), (host_good, good)):
+            (proc / str(host)).mkdir(parents=True)
+            (proc / str(host) / "cgroup").write_text("0::/\n")
+            (proc / str(host) / "environ").write_bytes(open(f"/proc/{child.pid}/environ", "rb").read())
+        slices = {0: [SimpleNamespace(id="gpu0::s0", hbm_bytes=2**30), SimpleNamespace(id="gpu0::s1", hbm_bytes=4 * 2**30)]}
+        g = HbmGuard(smi, lambda: slices, "box", action="report", slack_bytes=1 << 30, strikes=1, proc_root=str(proc))
+        found = g.check()
+        assert [v.account.slice_ids for v in found] == [("gpu0::s0",)], found
+        assert found[0].account.pids == [host_rogue] and found[0].account.used >= 3 * 2**30
+        ok = [a for a in g.last if a.slice_ids == ("gpu0::s1",)]
+        assert ok and ok[0].used < 4 * 2**30, g.last
+    finally:
+        for p in (rogue, good):
+            try:
+                p.stdin.close()
+            except OSError:
+                pass
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()

@@ -1,0 +1,154 @@
+"""HBM budget guard (controllers/hbmguard.py): per-process VRAM attributed to pods by cgroup or by
+the environment Allocate set, held against the slices' budgets; report / evict after N strikes."""
+from __future__ import annotations
+
+import os
+from types import SimpleNamespace
+
+import pytest
+
+from walkai_nos_amd.api.config import GpuAgentConfig, MigAgentConfig
+from walkai_nos_amd.controllers.hbmguard import HbmGuard, pod_uid_of, slice_ids_of
+from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+from walkai_nos_amd.models.device import STATUS_USED, Device
+
+GB = 10**9
+UID_A = "0b5c2a7e-1111-4f0e-9c1a-8d2e3f4a5b6c"
+UID_B = "1c6d3b8f-2222-4a1f-8d2b-9e3f4a5b6c7d"
+
+
+def _proc(root, pid, uid=None, env=None):
+    d = root / str(pid)
+    d.mkdir()
+    cg = "0::/\n" if uid is None else \
+        f"0::/kubepods.slice/kubepods-burstable.slice/kubepods-burstable-pod{uid.replace('-', '_')}.slice/cri-containerd-abc.scope\n"
+    (d / "cgroup").write_text(cg)
+    (d / "environ").write_bytes(b"\0".join(f"{k}={v}".encode() for k, v in (env or {}).items()) + b"\0")
+
+
+@pytest.fixture
+def node(tmp_path):
+    smi = FakeAmdSmi(n_gpus=2)
+    slices = {0: [SimpleNamespace(id="gpu0::s0", hbm_bytes=36 * GB), SimpleNamespace(id="gpu0::s1", hbm_bytes=36 * GB),
+                  SimpleNamespace(id="gpu0::s2", hbm_bytes=72 * GB)],
+              1: []}
+    used = [("team-a", "pod-a", Device("amd.com/cpx_nps1", "gpu0::s0", STATUS_USED)),
+            ("team-b", "pod-b", Device("amd.com/cpx_nps1", "gpu0::s1", STATUS_USED))]
+    evicted = []
+    g = HbmGuard(smi, lambda: slices, "n1", pods_by_device=lambda: used,
+                 pods_by_uid=lambda: {UID_A: ("team-a", "pod-a"), UID_B: ("team-b", "pod-b")},
+                 evict=lambda ns, name, why: evicted.append((ns, name, why)), action="evict",
+                 slack_bytes=GB, strikes=2, proc_root=str(tmp_path))
+    return SimpleNamespace(smi=smi, guard=g, evicted=evicted, root=tmp_path, slices=slices, used=used)
+
+
+def test_proc_readers(tmp_path):
+    _proc(tmp_path, 10, UID_A, {"NOS_SLICE_IDS": "gpu0::s0,gpu0::s1", "PATH": "/bin"})
+    assert pod_uid_of(10, str(tmp_path)) == UID_A
+    assert slice_ids_of(10, str(tmp_path)) == ("gpu0::s0", "gpu0::s1")
+    assert pod_uid_of(11, str(tmp_path)) is None and slice_ids_of(11, str(tmp_path)) == ()
+
+
+def test_pod_within_budget_is_left_alone(node):
+    _proc(node.root, 100, UID_A, {"NOS_SLICE_IDS": "gpu0::s0"})
+    node.smi.set_process_memory(0, 100, 30 * GB)
+    for _ in range(3):
+        assert node.guard.check() == []
+    (a,) = node.guard.last
+    assert a.pod == ("team-a", "pod-a") and a.budget == 36 * GB and a.used == 30 * GB and a.pids == [100]
+    assert node.evicted == []
+
+
+def test_pod_over_budget_is_evicted_after_the_strikes_even_without_its_env(node):
+    # pod-a's process cleared its environment (no LD_PRELOAD, no NOS_SLICE_IDS): the cgroup still
+    # names the pod, and kubelet's PodResources its slice
+    _proc(node.root, 100, UID_A, {})
+    _proc(node.root, 101, UID_A, {})
+    node.smi.set_process_memory(0, 100, 20 * GB)
+    node.smi.set_process_memory(0, 101, 20 * GB)   # two processes: 40 GB against 36 + 1
+    v1 = node.guard.check()
+    assert [v.action for v in v1] == [] and node.evicted == []       # first strike
+    (v,) = node.guard.check()
+    assert v.action == "evicted" and v.account.used == 40 * GB and sorted(v.account.pids) == [100, 101]
+    assert [(ns, n) for ns, n, _ in node.evicted] == [("team-a", "pod-a")]
+    assert "budget 36000000000" in node.evicted[0][2]
+    (v,) = node.guard.check()                                           # still there: not evicted twice
+    assert v.action == "evict" and len(node.evicted) == 1
+
+
+def test_strikes_reset_when_the_pod_frees_memory(node):
+    _proc(node.root, 100, UID_A, {})
+    node.smi.set_process_memory(0, 100, 40 * GB)
+    node.guard.check()
+    node.smi.set_process_memory(0, 100, 10 * GB)
+    node.guard.check()
+    node.smi.set_process_memory(0, 100, 40 * GB)
+    assert node.guard.check() == [] and node.evicted == []
+
+
+def test_report_only_never_evicts(node):
+    node.guard.action = "report"
+    _proc(node.root, 100, UID_B, {})
+    node.smi.set_process_memory(0, 100, 50 * GB)
+    node.guard.check()
+    (v,) = node.guard.check()
+    assert v.action == "report" and v.account.pod == ("team-b", "pod-b") and node.evicted == []
+
+
+def test_environment_attribution_outside_kubernetes(node):
+    # no pod cgroup (a bare process given the Allocate env): the slice ids account for it, and
+    # PodResources still names the pod holding those slices
+    _proc(node.root, 200, None, {"NOS_SLICE_IDS": "gpu0::s2"})
+    node.smi.set_process_memory(0, 200, 80 * GB)
+    node.guard.check()
+    (v,) = node.guard.check()
+    assert v.account.slice_ids == ("gpu0::s2",) and v.account.budget == 72 * GB and v.account.pod is None
+    assert v.action == "evict" and node.evicted == []                  # nothing to evict without a pod
+
+
+def test_unattributed_processes_are_reported_not_evicted(node):
+    _proc(node.root, 300, None, {})
+    node.smi.set_process_memory(0, 300, 5 * GB)
+    assert node.guard.check() == [] and node.guard.unattributed == {0: 5 * GB}
+
+
+def test_slices_of_another_gpu_do_not_attribute(node):
+    # a process on GPU 0 whose env names a slice of another GPU is not that slice's account
+    node.slices[1] = [SimpleNamespace(id="gpu1::s0", hbm_bytes=36 * GB)]
+    _proc(node.root, 400, None, {"NOS_SLICE_IDS": "gpu1::s0"})
+    node.smi.set_process_memory(0, 400, 2 * GB)
+    node.guard.check()
+    assert node.guard.unattributed == {0: 2 * GB} and node.guard.last == []
+
+
+def test_process_list_failure_skips_the_gpu(node):
+    def boom(i):
+        raise RuntimeError("gpu mid-flip")
+    node.smi.process_memory = boom
+    assert node.guard.check() == []
+
+
+def test_config_validation():
+    for cls in (GpuAgentConfig, MigAgentConfig):
+        c = cls()
+        c.validate()
+        assert c.hbmGuard == "report"
+        c.hbmGuard = "kill"
+        with pytest.raises(ValueError):
+            c.validate()
+    with pytest.raises(ValueError):
+        HbmGuard(FakeAmdSmi(n_gpus=1), dict, action="kill")
+
+
+def test_register_on_the_manager():
+    calls = []
+    mgr = SimpleNamespace(add_runnable=lambda *a, **k: calls.append((a, k)))
+    HbmGuard(FakeAmdSmi(n_gpus=1), dict, action="off").register(mgr)
+    assert calls == []
+    HbmGuard(FakeAmdSmi(n_gpus=1), dict, action="report").register(mgr, 5.0)
+    assert calls[0][0][0] == "hbm-guard" and calls[0][0][2] == 5.0 and calls[0][1] == {"needs_leader": False}
+
+
+def test_native_proc_root_is_this_process(tmp_path):
+    # the real /proc: this test process has no pod cgroup, and its env has no slice ids unless set
+    assert slice_ids_of(os.getpid()) == tuple(i for i in os.environ.get("NOS_SLICE_IDS", "").split(",") if i)

@@ -124,9 +124,21 @@ class AgentConfig(ManagerConfig):
     commitBarrier: str = "xgmi"             # xgmi (P2P token ring) | rccl (communicator all-reduce) | none
     probeOnCommit: bool = True
     devicePluginDir: str = "/var/lib/kubelet/device-plugins"  # kubelet's plugin dir (kubelet.sock + our sockets)
+    #: pods over their slices' HBM budget (amd-smi per-process VRAM, controllers/hbmguard.py):
+    #: off | report (metric + log) | evict (delete the pod)
+    hbmGuard: str = "report"
+    hbmGuardIntervalSeconds: float = 10.0
+    #: VRAM a process maps beyond what the budget interposer counts (HIP runtime, code objects)
+    hbmGuardSlackBytes: int = 1 << 30
 
     def validate(self) -> None:
         super().validate()
+        if self.hbmGuard not in ("off", "report", "evict"):
+            raise ValueError("hbmGuard must be 'off', 'report' or 'evict'")
+        if self.hbmGuardIntervalSeconds <= 0:
+            raise ValueError("hbmGuardIntervalSeconds must be greater than 0")
+        if self.hbmGuardSlackBytes < 0:
+            raise ValueError("hbmGuardSlackBytes must be >= 0")
         if self.reportConfigIntervalSeconds <= 0:
             raise ValueError("reportConfigIntervalSeconds must be greater than 0")
         if self.amdSmiBackend not in ("native", "fake"):

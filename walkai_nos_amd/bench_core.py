@@ -1190,10 +1190,10 @@ def node_barrier_probe(cfg: BenchConfig) -> Optional[Dict[str, Any]]:
 
 
 #: inferences/s per GPU with every partition of the mode busy, one serving thread per pod — the
-#: final round-3 tree (``profiles/kbench_r3_modes_final.json``, free-running): a CU-mask slice runs
-#: the same kernels on the same CU set as the emulated partition of its size, so slices are priced
-#: with the rate of that mode per partition
-MODE_RATES = {"spx": 359.9, "dpx": 415.9, "qpx": 433.0, "cpx": 404.2}
+#: round-4 tree (``profiles/kbench_r4_modes.json``, free-running; round 3: 359.9 / 415.9 / 433.0 /
+#: 404.2): a CU-mask slice runs the same kernels on the same CU set as the emulated partition of
+#: its size, so slices are priced with the rate of that mode per partition
+MODE_RATES = {"spx": 368.5, "dpx": 418.5, "qpx": 427.5, "cpx": 404.9}
 
 
 def control_only(cfg: BenchConfig, steps: int, skip: int = 0) -> Dict[str, Any]:

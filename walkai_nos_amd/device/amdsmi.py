@@ -83,6 +83,9 @@ class AmdSmi:
     def _process_count(self, proc: ProcInfo) -> int:
         raise NotImplementedError
 
+    def _process_memory(self, proc: ProcInfo) -> Dict[int, int]:
+        raise NotImplementedError
+
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         raise NotImplementedError
 
@@ -185,6 +188,15 @@ class AmdSmi:
         """Processes holding any partition of physical GPU ``index`` (a flip destroys them all)."""
         return sum(self._process_count(p) for p in self._members(index))
 
+    def process_memory(self, index: int) -> Dict[int, int]:
+        """pid -> VRAM bytes of every process holding a context on physical GPU ``index`` (the
+        input of :class:`~walkai_nos_amd.controllers.hbmguard.HbmGuard`)."""
+        out: Dict[int, int] = {}
+        for p in self._members(index):
+            for pid, b in self._process_memory(p).items():
+                out[pid] = out.get(pid, 0) + b
+        return out
+
     def activity(self, index: int) -> Dict[str, float]:
         acts = [self._activity(p) for p in self._members(index)]
         return {k: sum(a[k] for a in acts) / len(acts) for k in ("gfx", "umc", "mm")}
@@ -211,6 +223,7 @@ class _FakeGpu:
     compute: str = "SPX"
     memory: str = "NPS1"
     processes: Dict[int, int] = field(default_factory=dict)  # partition -> process count
+    vram: Dict[int, Dict[int, int]] = field(default_factory=dict)  # partition -> {pid: VRAM bytes}
 
 
 class FakeAmdSmi(AmdSmi):
@@ -329,6 +342,10 @@ class FakeAmdSmi(AmdSmi):
         g = self._gpu_of(proc)
         return g.processes.get(proc.partition_id if proc.partition_id != NO_PARTITION else 0, 0)
 
+    def _process_memory(self, proc: ProcInfo) -> Dict[int, int]:
+        g = self._gpu_of(proc)
+        return dict(g.vram.get(proc.partition_id if proc.partition_id != NO_PARTITION else 0, {}))
+
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         return {"gfx": 100.0 if self._process_count(proc) else 0.0, "umc": 0.0, "mm": 0.0}
 
@@ -349,6 +366,16 @@ class FakeAmdSmi(AmdSmi):
                 g.processes[partition] = n
             else:
                 g.processes.pop(partition, None)
+
+    def set_process_memory(self, index: int, pid: int, nbytes: int, partition: int = 0) -> None:
+        """Pretend process ``pid`` holds ``nbytes`` of VRAM on partition ``partition`` of GPU
+        ``index`` (0 bytes: the process exits)."""
+        with self._lock:
+            per = self._gpu(index).vram.setdefault(partition, {})
+            if nbytes:
+                per[pid] = nbytes
+            else:
+                per.pop(pid, None)
 
     def attach(self, device_id: str, n: int = 1) -> None:
         """Pretend ``n`` more processes opened the partition behind ``device_id``."""
@@ -399,6 +426,8 @@ class NativeAmdSmi(AmdSmi):
         L.nos_smi_get_memory_partition.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
         L.nos_smi_set_memory_partition.argtypes = [ctypes.c_uint32, ctypes.c_char_p]
         L.nos_smi_process_count.argtypes = [ctypes.c_uint32]
+        L.nos_smi_process_memory.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                             ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
         L.nos_smi_activity.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.nos_smi_vram.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.nos_smi_power_clock.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 4
@@ -457,6 +486,18 @@ class NativeAmdSmi(AmdSmi):
         if n < 0:
             raise GpuError(f"process list: {self._err()}")
         return n
+
+    def _process_memory(self, proc: ProcInfo) -> Dict[int, int]:
+        cap = 64
+        while True:
+            pids, vram = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+            with self._lock:
+                n = self._lib.nos_smi_process_memory(proc.ordinal, pids, vram, cap)
+            if n < 0:
+                raise GpuError(f"process list: {self._err()}")
+            if n <= cap:
+                return {int(pids[i]): int(vram[i]) for i in range(n)}
+            cap = n + 16
 
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         a, b, c = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
