@@ -12,14 +12,14 @@ import socket
 import pytest
 
 
-def _worker(rank, world, port, q, veto_rank, veto_commits):
+def _worker(rank, world, port, q, veto_rank, veto_commits, layout="partitions"):
     import torch.distributed as dist
 
     from walkai_nos_amd.bench_core import BenchConfig, NodeBench
     from walkai_nos_amd.parallel.barrier import RankCommitBarrier
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        cfg = BenchConfig(gpus=world, steps=6, warmup=1, rank=rank, world=world, preroll=10)
+        cfg = BenchConfig(gpus=world, steps=6, warmup=1, rank=rank, world=world, preroll=10, layout=layout)
         results = []
         checks = [0]
 
@@ -51,14 +51,14 @@ def _worker(rank, world, port, q, veto_rank, veto_commits):
         dist.destroy_process_group()
 
 
-def _run(world, veto_rank=-1, veto_commits=0):
+def _run(world, veto_rank=-1, veto_commits=0, layout="partitions"):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, veto_rank, veto_commits)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, veto_rank, veto_commits, layout)) for r in range(world)]
     [p.start() for p in ps]
     [p.join(240) for p in ps]
     assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
@@ -73,6 +73,15 @@ def test_bench_control_plane_lockstep_gloo(world):
     assert len({len(o[2]) for o in out}) == 1 and len(out[0][2]) > 0
     assert all(all(o[2]) for o in out)
     # every rank serves only its own GPU's pods; together they cover the node's work
+    assert all(o[1] > 0 for o in out)
+
+
+def test_bench_control_plane_lockstep_gloo_sliced_gpus():
+    """The bench's default layout (sliced GPUs) under two ranks: the same node simulation on both,
+    no flip at all (re-carving needs no commit), each rank serving its own GPU's slices."""
+    out = _run(2, layout="slices")
+    assert len({tuple(o[4]) for o in out}) == 1 and len({tuple(o[5]) for o in out}) == 1
+    assert all(o[6] == [] for o in out)          # no amd-smi set call on any rank
     assert all(o[1] > 0 for o in out)
 
 
