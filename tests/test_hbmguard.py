@@ -152,3 +152,36 @@ def test_register_on_the_manager():
 def test_native_proc_root_is_this_process(tmp_path):
     # the real /proc: this test process has no pod cgroup, and its env has no slice ids unless set
     assert slice_ids_of(os.getpid()) == tuple(i for i in os.environ.get("NOS_SLICE_IDS", "").split(",") if i)
+
+
+def test_guard_on_a_sliced_node_evicts_the_pod_over_budget_and_frees_its_slice(tmp_path):
+    """End to end on the simulated cluster: two 1/8 pods on a sliced GPU; one pod's process holds
+    more VRAM than its slice's 36 GB budget (the interposer bypassed). The guard, wired as the
+    partition agent wires it (slice store, kubelet PodResources, the node's pods, eviction through
+    the API), attributes the process by its pod cgroup, evicts that pod only, and the freed slice
+    serves the next pod."""
+    from walkai_nos_amd.controllers.hbmguard import node_pods_by_uid, pod_evictor
+    from walkai_nos_amd.kube import objects as ko
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=1, policy="pack", xcp_layout="slices", refresh_interval=5.0)
+    c.run(30)
+    sn = c.nodes["node-0"]
+    for n in ("good", "rogue"):
+        c.submit({"amd.com/cpx_nps1": 1}, name=n)
+    c.run(60)
+    assert {ko.name(p) for p in c.running_pods()} == {"good", "rogue"}
+    uid = {ko.name(p): p["metadata"]["uid"] for p in c.running_pods()}
+    _proc(tmp_path, 500, uid["good"], {})
+    _proc(tmp_path, 501, uid["rogue"], {})
+    sn.smi.set_process_memory(0, 500, 30 * GB)
+    sn.smi.set_process_memory(0, 501, 60 * GB)
+    g = HbmGuard(sn.smi, sn.xcp_slices.load, "node-0", pods_by_device=sn.kubelet.resource_client().get_used_devices_by_pod,
+                 pods_by_uid=node_pods_by_uid(c.api, "node-0"), evict=pod_evictor(c.api), action="evict",
+                 strikes=1, proc_root=str(tmp_path))
+    (v,) = g.check()
+    assert v.action == "evicted" and v.account.pod == ("default", "rogue") and v.account.budget == 36 * GB
+    sn.smi.set_process_memory(0, 501, 0)
+    c.submit({"amd.com/cpx_nps1": 1}, name="next")
+    c.run(60)
+    assert {ko.name(p) for p in c.running_pods()} == {"good", "next"}
+    assert g.check() == [] and [a.pod for a in g.last] == [("default", "good")]
