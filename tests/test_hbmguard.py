@@ -180,6 +180,8 @@ def test_guard_on_a_sliced_node_evicts_the_pod_over_budget_and_frees_its_slice(t
                  strikes=1, proc_root=str(tmp_path))
     (v,) = g.check()
     assert v.action == "evicted" and v.account.pod == ("default", "rogue") and v.account.budget == 36 * GB
+    (ev,) = [e for e in c.api.list("Event", namespace="default") if e.get("reason") == "HBMBudgetExceeded"]
+    assert ev["involvedObject"]["name"] == "rogue" and ev["type"] == "Warning" and "budget 36000000000" in ev["message"]
     sn.smi.set_process_memory(0, 501, 0)
     c.submit({"amd.com/cpx_nps1": 1}, name="next")
     c.run(60)

@@ -121,7 +121,7 @@ def main(argv=None) -> int:
     if slice_store is not None:
         from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_evictor
         HbmGuard(smi, slice_store.load, node, pods_by_device=resources.get_used_devices_by_pod,
-                 pods_by_uid=node_pods_by_uid(client, node), evict=pod_evictor(client), action=cfg.hbmGuard,
+                 pods_by_uid=node_pods_by_uid(client, node), evict=pod_evictor(client, node), action=cfg.hbmGuard,
                  slack_bytes=cfg.hbmGuardSlackBytes).register(mgr, cfg.hbmGuardIntervalSeconds)
     serve_endpoints(mgr, cfg)
     stop = None

@@ -249,8 +249,18 @@ def node_pods_by_uid(client: Any, node: str) -> Callable[[], Dict[str, PodKey]]:
     return f
 
 
-def pod_evictor(client: Any) -> Callable[[str, str, str], None]:
-    """Deletes the pod (its controller, if any, recreates it against a fresh slice)."""
+def pod_evictor(client: Any, node: str = "") -> Callable[[str, str, str], None]:
+    """Records a ``HBMBudgetExceeded`` Warning event on the pod, then deletes it (its controller,
+    if any, recreates it against a fresh slice)."""
     def f(namespace: str, name: str, reason: str) -> None:
+        try:
+            client.create({
+                "apiVersion": "v1", "kind": "Event",
+                "metadata": {"generateName": f"{name}.", "namespace": namespace},
+                "involvedObject": {"apiVersion": "v1", "kind": "Pod", "name": name, "namespace": namespace},
+                "reason": "HBMBudgetExceeded", "message": reason, "type": "Warning",
+                "source": {"component": "nos-hbm-guard", "host": node}})
+        except Exception as e:  # noqa: BLE001 - the eviction matters, the event is a courtesy
+            log.warning("event for %s/%s not recorded: %s", namespace, name, e)
         client.delete("Pod", name, namespace)
     return f
