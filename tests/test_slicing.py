@@ -205,3 +205,30 @@ def test_pack_policy_plans_cumask_nodes_oldest_first():
     c.submit({"amd.com/gpu-36gb": 1}, name="m0")
     c.run(120)
     assert {ko.name(p) for p in c.running_pods()} == {"s0", "m0"}
+
+
+def test_at_most_eight_slices_per_gpu_unless_the_node_allows_more():
+    """Each slice serves one pod process, and beyond 8 processes per GPU the hardware scheduler
+    time-slices them (profiles/procs_cap_r4.json): the planner carves at most 8 slices per GPU;
+    the node label nos.nebuly.com/max-slices-per-gpu raises (or lowers) it."""
+    g = SlicingGPU.full("MI355X", 0, 288)
+    assert g.create_slices("8gb", 8) and not g.create_slices("8gb", 1)
+    assert not g.can_create_more_slices() and g.spare_memory_gb() == 288 - 64
+    n = SlicingNode("n", [SlicingGPU.full("MI355X", 0, 288), SlicingGPU.full("MI355X", 1, 288)])
+    n.update_geometry_for({"16gb": 12})
+    assert n.gpus[0].geometry() == {"16gb": 8} and n.gpus[1].geometry() == {"16gb": 4}
+    wide = SlicingGPU.full("MI355X", 0, 288, max_slices=16)
+    assert wide.create_slices("8gb", 16) and not wide.create_slices("8gb", 1)
+    assert wide.clone().max_slices == 16
+
+
+@pytest.mark.parametrize("label,running", [(None, 8), ("10", 10), ("bogus", 8)])
+def test_cumask_node_serves_at_most_its_slice_cap(label, running):
+    c = SimCluster(n_nodes=1, gpus_per_node=1, kind="cumask")
+    if label is not None:
+        c.api.patch("Node", "node-0", {"metadata": {"labels": {"nos.nebuly.com/max-slices-per-gpu": label}}})
+    c.run(30)
+    for i in range(12):
+        c.submit({"amd.com/gpu-8gb": 1}, name=f"m{i}")
+    c.run(120)
+    assert len(c.running_pods()) == running and len(c.pending_pods()) == 12 - running

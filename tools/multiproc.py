@@ -10,7 +10,9 @@ Scenarios (each a fresh set of processes, all released at one instant for a comm
 * ``cumask_<N>``  N = 3/5/7 dedicated-CU slices that split the 8 row groups (256 CUs) between them;
 * ``cpx8``        8 x ``32cu.36gb`` — BASELINE config 2 (8 pods, 1/8 GPU each) on the SPX device;
 * ``config3``     4 x ``64cu.72gb`` — BASELINE config 3 (4 pods, own CU set + HBM limit), with the
-  HBM shim, and ``config3_noshim`` without it (the shim's cost).
+  HBM shim, and ``config3_noshim`` without it (the shim's cost);
+* ``dense_14`` / ``shared_14``  beyond eight pods per GPU: 6 dedicated 32-CU slices + 8 memory-only
+  slices on the other 64 CUs, and 14 memory-only slices (the bench density phase's mixes).
 
     python tools/multiproc.py [--seconds 10] [--only shared_1,config3] --out gpurun_out/multiproc.json
 """
@@ -43,6 +45,11 @@ def scenarios():
     out["cpx8"] = (["32cu.36gb"] * 8, True)
     out["config3"] = (["64cu.72gb"] * 4, True)
     out["config3_noshim"] = (["64cu.72gb"] * 4, False)
+    # beyond 8 pods (the bench density phase's mixes, at 14 pods: a box runs at most 16 GPU processes)
+    out["dense_14"] = (["32cu.24gb"] * 6 + ["8gb"] * 8, True)
+    out["shared_14"] = (["16gb"] * 14, True)
+    for n in (8, 9, 10, 12):   # where process time-slicing starts
+        out[f"shared_{n}"] = (["16gb"] * n, True)
     return out
 
 

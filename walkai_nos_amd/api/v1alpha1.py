@@ -25,6 +25,8 @@ LABEL_CAPACITY_INFO = "nos.nebuly.com/capacity"
 # the default), "slices" (every GPU in SPX carved into CU-mask slices of the partition sizes: mixed
 # geometries, re-carved without a drain), "auto" (the planner chooses per GPU); models/xcp/slices.py
 LABEL_XCP_LAYOUT = "nos.nebuly.com/xcp-layout"
+# cumask nodes: slices per GPU the planner may carve (default models/slicing/profile.MAX_SLICES_PER_GPU)
+LABEL_MAX_SLICES_PER_GPU = "nos.nebuly.com/max-slices-per-gpu"
 CAPACITY_IN_QUOTA = "in-quota"
 CAPACITY_OVER_QUOTA = "over-quota"
 

@@ -874,10 +874,14 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
             dt = time.perf_counter() - t0
             out[name]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
             out[name]["per_pod"] = _per_pod_spread(got, keys, dt)
-    # CU-mask slices beyond 8 per GPU
+    # CU-mask slices beyond 8 per GPU: the node is labelled to allow 16 (the default cap is 8
+    # because pods are processes and beyond 8 processes the hardware scheduler time-slices them,
+    # profiles/procs_cap_r4.json; the bench serves these pods as threads of one process)
     for variant, mix in CUMASK_DENSITY.items():
         c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
                         policy="fifo")
+        for n in c2.nodes:
+            c2.api.patch("Node", n, {"metadata": {"labels": {api.LABEL_MAX_SLICES_PER_GPU: "16"}}})
         c2.run(30)
         k = 0
         for _ in range(cfg.gpus):

@@ -18,7 +18,7 @@ from .. import annotation as ann
 from .. import gpu_util
 from .. import resource as res
 from ..geometry import Geometry
-from .profile import (CU_GRANULARITY, MIN_SHARED_CUS, MIN_SLICE_MEMORY_GB, as_resource_name,
+from .profile import (CU_GRANULARITY, MAX_SLICES_PER_GPU, MIN_SHARED_CUS, MIN_SLICE_MEMORY_GB, as_resource_name,
                       extract_profile_name, is_slice_resource, parse_profile)
 
 
@@ -30,13 +30,18 @@ class SlicingGPU:
     cu_count: int = 256
     used: Dict[str, int] = field(default_factory=dict)
     free: Dict[str, int] = field(default_factory=dict)
+    #: slices the planner may carve on this GPU (each serves one pod process; beyond 8 the hardware
+    #: scheduler time-slices processes, :data:`~.profile.MAX_SLICES_PER_GPU`)
+    max_slices: int = MAX_SLICES_PER_GPU
 
     @classmethod
-    def full(cls, model: str, index: int, memory_gb: int, cu_count: int = 256) -> "SlicingGPU":
-        return cls(model, index, memory_gb, cu_count)
+    def full(cls, model: str, index: int, memory_gb: int, cu_count: int = 256,
+             max_slices: int = MAX_SLICES_PER_GPU) -> "SlicingGPU":
+        return cls(model, index, memory_gb, cu_count, max_slices=max_slices)
 
     def clone(self) -> "SlicingGPU":
-        return SlicingGPU(self.model, self.index, self.memory_gb, self.cu_count, dict(self.used), dict(self.free))
+        return SlicingGPU(self.model, self.index, self.memory_gb, self.cu_count, dict(self.used), dict(self.free),
+                          self.max_slices)
 
     def validate(self) -> None:
         for d in (self.used, self.free):
@@ -77,12 +82,15 @@ class SlicingGPU:
     def spare_cus(self) -> int:
         return self._cu_budget() - self._tot_cus()
 
+    def slice_count(self) -> int:
+        return sum(self.geometry().values())
+
     def can_create_more_slices(self) -> bool:
-        return self.spare_memory_gb() >= MIN_SLICE_MEMORY_GB
+        return self.spare_memory_gb() >= MIN_SLICE_MEMORY_GB and self.slice_count() < self.max_slices
 
     def _can_create(self, profile: str, num: int = 1) -> bool:
         prof = parse_profile(profile)
-        if self.spare_memory_gb() < prof.memory_gb * num:
+        if self.spare_memory_gb() < prof.memory_gb * num or self.slice_count() + num > self.max_slices:
             return False
         budget = self._cu_budget(extra_shared=not prof.dedicated)
         return budget - self._tot_cus() >= prof.cus * num
@@ -207,17 +215,29 @@ def new_node(node: Dict[str, Any]) -> SlicingNode:
     count = gpu_util.get_count(node)
     mem = gpu_util.get_memory_gb(node)
     cus = gpu_util.get_cu_count(node)
+    cap = max_slices_per_gpu(node)
     status, _ = ann.parse_node_annotations(ko.annotations(node))
     gpus: Dict[int, SlicingGPU] = {}
     for idx, items in sorted(ann.group_by_gpu_index(status).items()):
         used = {a.profile: a.quantity for a in items if a.is_used()}
         free = {a.profile: a.quantity for a in items if a.is_free()}
-        g = SlicingGPU(model, idx, mem, cus, used, free)
+        g = SlicingGPU(model, idx, mem, cus, used, free, cap)
         g.validate()
         gpus[idx] = g
     for i in range(count):
-        gpus.setdefault(i, SlicingGPU.full(model, i, mem, cus))
+        gpus.setdefault(i, SlicingGPU.full(model, i, mem, cus, cap))
     return SlicingNode(ko.name(node), [gpus[i] for i in sorted(gpus)], res.from_k8s(ko.node_allocatable(node)))
+
+
+def max_slices_per_gpu(node: Dict[str, Any]) -> int:
+    """The node's ``nos.nebuly.com/max-slices-per-gpu`` label (a positive integer), else the default."""
+    from ...api.v1alpha1 import LABEL_MAX_SLICES_PER_GPU
+    v = ko.labels(node).get(LABEL_MAX_SLICES_PER_GPU)
+    try:
+        n = int(v) if v is not None else MAX_SLICES_PER_GPU
+    except ValueError:
+        return MAX_SLICES_PER_GPU
+    return n if n > 0 else MAX_SLICES_PER_GPU
 
 
 def get_requested_profiles(pod: Dict[str, Any]) -> Dict[str, int]:

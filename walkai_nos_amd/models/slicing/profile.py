@@ -31,6 +31,13 @@ MIN_SLICE_MEMORY_GB = 1
 CU_GRANULARITY = 32
 #: CUs always left to the shared pool when memory-only slices exist
 MIN_SHARED_CUS = 32
+#: slices (pods, one process each) per GPU before the hardware scheduler time-slices processes:
+#: measured with pods as processes (``profiles/procs_cap_r4.json``), 8 memory-only pods share an
+#: SPX MI355X evenly (383 inf/s, per-pod max/min 1.03); a 9th and 10th keep the aggregate but not
+#: the shares (1.25, 3.0: some processes are switched out for whole scheduling quanta), and at 12-14
+#: the aggregate falls to 292 / 271 (14 mixed dedicated + memory-only pods: 192,
+#: ``profiles/dense_r4.json``). The node label ``nos.nebuly.com/max-slices-per-gpu`` overrides it.
+MAX_SLICES_PER_GPU = 8
 REPLICA_SEPARATOR = "::"
 
 _PROFILE_RE = re.compile(r"^(?:(\d+)cu\.)?(\d+)gb$")
