@@ -187,3 +187,38 @@ def test_guard_on_a_sliced_node_evicts_the_pod_over_budget_and_frees_its_slice(t
     c.run(60)
     assert {ko.name(p) for p in c.running_pods()} == {"good", "next"}
     assert g.check() == [] and [a.pod for a in g.last] == [("default", "good")]
+
+
+def test_cpx_on_nps1_partitions_share_memory_and_get_an_eighth_each():
+    from walkai_nos_amd.controllers.hbmguard import shared_memory_partitions
+    smi = FakeAmdSmi(n_gpus=2)
+    smi.set_compute_partition(0, "CPX")          # 8 compute partitions, one NPS1 memory pool
+    parts = shared_memory_partitions(smi.device_map())
+    assert len(parts) == 8 and {g for g, _ in parts.values()} == {0}
+    assert {b for _, b in parts.values()} == {288 * GB // 8}
+    smi.set_compute_partition(1, "DPX")
+    assert len(shared_memory_partitions(smi.device_map())) == 10   # DPX on NPS1 shares memory too
+    smi2 = FakeAmdSmi(n_gpus=1)
+    smi2.set_memory_partition("NPS2")
+    smi2.set_compute_partition(0, "DPX")          # one memory partition per compute partition: hardware-isolated
+    assert shared_memory_partitions(smi2.device_map()) == {}
+
+
+def test_guard_holds_a_cpx_pod_to_its_eighth_of_the_shared_hbm(tmp_path):
+    from walkai_nos_amd.controllers.hbmguard import shared_memory_partitions
+    smi = FakeAmdSmi(n_gpus=1)
+    smi.set_compute_partition(0, "CPX")
+    devs = smi.device_map().partitions_of(0)
+    used = [("t", "cpx-a", Device("amd.com/cpx_nps1", devs[0].device_id, STATUS_USED)),
+            ("t", "cpx-b", Device("amd.com/cpx_nps1", devs[1].device_id, STATUS_USED))]
+    _proc(tmp_path, 10, UID_A, {"NOS_PARTITION_IDS": devs[0].device_id})
+    _proc(tmp_path, 11, None, {"NOS_PARTITION_IDS": devs[1].device_id})
+    smi.set_process_memory(0, 10, 30 * GB, partition=0)
+    smi.set_process_memory(0, 11, 50 * GB, partition=1)         # past 36 GB + slack
+    evicted = []
+    g = HbmGuard(smi, dict, "n", pods_by_device=lambda: used, pods_by_uid=lambda: {UID_A: ("t", "cpx-a")},
+                 evict=lambda ns, n, why: evicted.append(n), action="evict", strikes=1, proc_root=str(tmp_path),
+                 partitions=lambda: shared_memory_partitions(smi.device_map()))
+    (v,) = g.check()
+    assert v.account.pod == ("t", "cpx-b") and v.account.budget == 36 * GB and evicted == ["cpx-b"]
+    assert sorted(a.pod for a in g.last) == [("t", "cpx-a"), ("t", "cpx-b")]

@@ -118,11 +118,12 @@ def main(argv=None) -> int:
     log.info("start-up reconciliation: %s", actuator.startup())
     from ..exporters.gpu_metrics import GpuMetricsPoller
     GpuMetricsPoller(smi, node).register(mgr)
-    if slice_store is not None:
-        from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_evictor
-        HbmGuard(smi, slice_store.load, node, pods_by_device=resources.get_used_devices_by_pod,
-                 pods_by_uid=node_pods_by_uid(client, node), evict=pod_evictor(client, node), action=cfg.hbmGuard,
-                 slack_bytes=cfg.hbmGuardSlackBytes).register(mgr, cfg.hbmGuardIntervalSeconds)
+    from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_evictor, shared_memory_partitions
+    # sliced GPUs' slices, and hardware partitions sharing one memory pool (CPX on NPS1)
+    HbmGuard(smi, slice_store.load if slice_store is not None else dict, node,
+             pods_by_device=resources.get_used_devices_by_pod, pods_by_uid=node_pods_by_uid(client, node),
+             evict=pod_evictor(client, node), action=cfg.hbmGuard, slack_bytes=cfg.hbmGuardSlackBytes,
+             partitions=lambda: shared_memory_partitions(smi.device_map())).register(mgr, cfg.hbmGuardIntervalSeconds)
     serve_endpoints(mgr, cfg)
     stop = None
     if plugins is not None:

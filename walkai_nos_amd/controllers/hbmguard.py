@@ -19,7 +19,11 @@ loop from outside the container, the way kubelet enforces memory by eviction:
 4. a pod over budget for ``strikes`` consecutive checks is reported (metric, log) and, with
    ``action: evict``, deleted — its slice goes back to the pool and its neighbours' memory is safe.
 
-Processes on a sliced GPU that nothing attributes are reported as ``unattributed`` bytes (never
+The same holds for hardware compute partitions that share one memory partition (CPX on NPS1:
+eight partitions, one HBM pool): nothing in hardware keeps a 1/8 partition's pod to 1/8 of the HBM,
+so those partitions get that share as their budget (:func:`shared_memory_partitions`).
+
+Processes on a guarded GPU that nothing attributes are reported as ``unattributed`` bytes (never
 evicted: without a pod there is nothing to evict).
 """
 from __future__ import annotations
@@ -64,17 +68,37 @@ def pod_uid_of(pid: int, proc_root: str = "/proc") -> Optional[str]:
     return m.group(1).replace("_", "-") if m else None
 
 
+_ID_VARS = (b"NOS_SLICE_IDS=", b"NOS_PARTITION_IDS=")
+
+
 def slice_ids_of(pid: int, proc_root: str = "/proc") -> Tuple[str, ...]:
-    """``NOS_SLICE_IDS`` from the process's initial environment (what ``Allocate`` set), or ()."""
+    """The device ids ``Allocate`` put in the process's initial environment (``NOS_SLICE_IDS``,
+    ``NOS_PARTITION_IDS``), or ()."""
     try:
         with open(os.path.join(proc_root, str(pid), "environ"), "rb") as f:
             env = f.read().split(b"\0")
     except OSError:
         return ()
+    out: List[str] = []
     for kv in env:
-        if kv.startswith(b"NOS_SLICE_IDS="):
-            return tuple(i for i in kv[len(b"NOS_SLICE_IDS="):].decode(errors="replace").split(",") if i)
-    return ()
+        for var in _ID_VARS:
+            if kv.startswith(var):
+                out.extend(i for i in kv[len(var):].decode(errors="replace").split(",") if i and i not in out)
+    return tuple(out)
+
+
+def shared_memory_partitions(device_map: Any) -> Dict[str, Tuple[int, int]]:
+    """Hardware partitions sharing a memory partition with others (more compute partitions than
+    NPS memory partitions, e.g. CPX on NPS1): device id -> (GPU, budget = the GPU's HBM / its
+    compute partitions), the share the profile promises and that nothing in hardware enforces."""
+    from ..models.xcp.profile import COMPUTE_MODES, MEMORY_MODES
+    vram = {g.index: g.vram_bytes for g in device_map.gpus}
+    out: Dict[str, Tuple[int, int]] = {}
+    for d in device_map.devices:
+        n = COMPUTE_MODES.get(d.compute_mode.lower(), 1)
+        if n > MEMORY_MODES.get(d.memory_mode.lower(), 1) and vram.get(d.gpu_index):
+            out[d.device_id] = (d.gpu_index, vram[d.gpu_index] // n)
+    return out
 
 
 @dataclass
@@ -104,7 +128,8 @@ class HbmGuard:
     """Checks pods' VRAM against their slices' HBM budgets (see the module docstring).
 
     ``slices``: GPU index -> the node's slices (``SliceStore.load``: objects with ``id`` and
-    ``hbm_bytes``); ``pods_by_device``: [(namespace, pod, device)] of running containers
+    ``hbm_bytes``); ``partitions``: device id -> (GPU, budget) of hardware partitions that share
+    memory (:func:`shared_memory_partitions`); ``pods_by_device``: [(namespace, pod, device)] of running containers
     (``ResourceClient.get_used_devices_by_pod``); ``pods_by_uid``: pod UID -> (namespace, name) of
     the node's pods; ``evict``: deletes a pod (``action: evict``)."""
 
@@ -112,11 +137,13 @@ class HbmGuard:
                  pods_by_device: Optional[Callable[[], Iterable[Tuple[str, str, Any]]]] = None,
                  pods_by_uid: Optional[Callable[[], Mapping[str, PodKey]]] = None,
                  evict: Optional[Callable[[str, str, str], None]] = None, action: str = "report",
-                 slack_bytes: int = 1 << 30, strikes: int = 2, proc_root: str = "/proc"):
+                 slack_bytes: int = 1 << 30, strikes: int = 2, proc_root: str = "/proc",
+                 partitions: Optional[Callable[[], Mapping[str, Tuple[int, int]]]] = None):
         if action not in ACTIONS:
             raise ValueError(f"hbm guard action {action!r} not in {ACTIONS}")
         self.smi, self.slices, self.node = smi, slices, node
         self.pods_by_device, self.pods_by_uid, self.evict = pods_by_device, pods_by_uid, evict
+        self.partitions = partitions
         self.action, self.slack_bytes, self.strikes, self.proc_root = action, slack_bytes, strikes, proc_root
         self._strikes: Dict[Tuple[Any, ...], int] = {}
         self._evicted: Dict[PodKey, int] = {}      # pod -> checks since its deletion was requested
@@ -130,6 +157,11 @@ class HbmGuard:
         """Every pod's (or slice set's) VRAM on each sliced GPU, from one amd-smi sample."""
         slices = self.slices() or {}
         budget_of: Dict[str, Tuple[int, int]] = {s.id: (g, int(s.hbm_bytes)) for g, ss in slices.items() for s in ss}
+        if self.partitions is not None:
+            try:
+                budget_of.update(self.partitions())
+            except Exception as e:  # noqa: BLE001 - device map unreadable: guard the slices only
+                log.warning("partition budgets unavailable: %s", e)
         ids_of_pod: Dict[PodKey, List[str]] = {}
         if self.pods_by_device is not None:
             try:
@@ -148,9 +180,7 @@ class HbmGuard:
                 log.warning("node pods unavailable: %s", e)
         out: Dict[Tuple[Any, ...], Account] = {}
         self.unattributed = {}
-        for g in sorted(slices):
-            if not slices[g]:
-                continue
+        for g in sorted({g for g, _ in budget_of.values()}):
             try:
                 procs = self.smi.process_memory(g)
             except Exception as e:  # noqa: BLE001 - a GPU mid-flip or off the bus: skip it this pass
