@@ -222,3 +222,21 @@ def test_guard_holds_a_cpx_pod_to_its_eighth_of_the_shared_hbm(tmp_path):
     (v,) = g.check()
     assert v.account.pod == ("t", "cpx-b") and v.account.budget == 36 * GB and evicted == ["cpx-b"]
     assert sorted(a.pod for a in g.last) == [("t", "cpx-a"), ("t", "cpx-b")]
+
+
+def test_node_pods_are_listed_only_for_an_unknown_pod_uid(node):
+    calls = []
+    known = {UID_A: ("team-a", "pod-a")}
+    node.guard.pods_by_uid = lambda: calls.append(1) or dict(known)
+    node.guard.check()
+    assert calls == []                                   # no GPU process: no API call
+    _proc(node.root, 100, UID_A, {})
+    node.smi.set_process_memory(0, 100, 10 * GB)
+    node.guard.check()
+    node.guard.check()
+    assert len(calls) == 1 and node.guard.last[0].pod == ("team-a", "pod-a")   # cached after the first miss
+    known[UID_B] = ("team-b", "pod-b")                  # a pod created since the last list
+    _proc(node.root, 101, UID_B, {})
+    node.smi.set_process_memory(0, 101, 10 * GB)
+    node.guard.check()
+    assert len(calls) == 2 and len(node.guard.last) == 2

@@ -149,6 +149,8 @@ class HbmGuard:
         self._evicted: Dict[PodKey, int] = {}      # pod -> checks since its deletion was requested
         self._series: set = set()
         self.checks = 0
+        self._uid_map: Dict[str, PodKey] = {}
+        self.uid_lists = 0                          # API server lists of the node's pods
         self.last: List[Account] = []
         self.unattributed: Dict[int, int] = {}
 
@@ -172,12 +174,19 @@ class HbmGuard:
             except Exception as e:  # noqa: BLE001 - kubelet down: attribute by environment only
                 log.warning("pod resources unavailable: %s", e)
         pod_of_id = {i: p for p, ids in ids_of_pod.items() for i in ids}
-        uid_map: Mapping[str, PodKey] = {}
-        if self.pods_by_uid is not None:
-            try:
-                uid_map = self.pods_by_uid()
-            except Exception as e:  # noqa: BLE001
-                log.warning("node pods unavailable: %s", e)
+        refreshed = [False]
+
+        def pod_of_uid(uid: str) -> Optional[PodKey]:
+            # the node's pods are listed from the API server only when a process names a pod UID
+            # the cached map does not know (once per pass): an idle node costs no API call
+            if uid not in self._uid_map and not refreshed[0] and self.pods_by_uid is not None:
+                refreshed[0] = True
+                try:
+                    self._uid_map = dict(self.pods_by_uid())
+                    self.uid_lists += 1
+                except Exception as e:  # noqa: BLE001
+                    log.warning("node pods unavailable: %s", e)
+            return self._uid_map.get(uid)
         out: Dict[Tuple[Any, ...], Account] = {}
         self.unattributed = {}
         for g in sorted({g for g, _ in budget_of.values()}):
@@ -190,7 +199,7 @@ class HbmGuard:
                 pod: Optional[PodKey] = None
                 uid = pod_uid_of(pid, self.proc_root)
                 if uid is not None:
-                    pod = uid_map.get(uid)
+                    pod = pod_of_uid(uid)
                 ids: Tuple[str, ...] = tuple(sorted(ids_of_pod.get(pod, ()))) if pod is not None else ()
                 if not ids:
                     ids = tuple(i for i in slice_ids_of(pid, self.proc_root) if budget_of.get(i, (None,))[0] == g)
