@@ -240,3 +240,23 @@ def test_node_pods_are_listed_only_for_an_unknown_pod_uid(node):
     node.smi.set_process_memory(0, 101, 10 * GB)
     node.guard.check()
     assert len(calls) == 2 and len(node.guard.last) == 2
+
+
+def test_slack_is_per_process():
+    # a pod running four GPU processes pays the HIP runtime's overhead four times: 37.6 GB on a
+    # 36 GB slice is inside 36 + 4 x 0.75 GiB, while one process holding the same 37.6 GB is not
+    smi = FakeAmdSmi(n_gpus=1)
+    slices = {0: [SimpleNamespace(id="s0", hbm_bytes=36 * GB)]}
+    import tempfile
+    from pathlib import Path
+    with tempfile.TemporaryDirectory() as d:
+        root = Path(d)
+        for pid in range(10, 14):
+            _proc(root, pid, None, {"NOS_SLICE_IDS": "s0"})
+            smi.set_process_memory(0, pid, 9_400_000_000)
+        g = HbmGuard(smi, lambda: slices, strikes=1, proc_root=str(root))
+        assert g.check() == [] and g.last[0].used == 37_600_000_000
+        for pid in range(11, 14):
+            smi.set_process_memory(0, pid, 0)
+        smi.set_process_memory(0, 10, 37_600_000_000)
+        assert len(g.check()) == 1

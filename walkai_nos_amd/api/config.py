@@ -128,8 +128,9 @@ class AgentConfig(ManagerConfig):
     #: off | report (metric + log) | evict (delete the pod)
     hbmGuard: str = "report"
     hbmGuardIntervalSeconds: float = 10.0
-    #: VRAM a process maps beyond what the budget interposer counts (HIP runtime, code objects)
-    hbmGuardSlackBytes: int = 1 << 30
+    #: VRAM each process may map beyond what the budget interposer counts (HIP runtime, code
+    #: objects: 490 MiB measured for a PyTorch process)
+    hbmGuardSlackBytes: int = 768 << 20
 
     def validate(self) -> None:
         super().validate()

@@ -14,8 +14,8 @@ loop from outside the container, the way kubelet enforces memory by eviction:
    kubelet's PodResources gives the pod's slice ids) or, outside Kubernetes, by the
    ``NOS_SLICE_IDS`` that ``Allocate`` put in its environment;
 3. a pod's VRAM summed over its processes is held against the sum of its slices' budgets plus a
-   slack for what the HIP runtime maps beyond the interposer's count (code objects, queues,
-   scratch);
+   slack per process for what the HIP runtime maps beyond the interposer's count (code objects,
+   queues, scratch: 490 MiB for a PyTorch process, ``profiles/pytest_hbmguard_r4.log``);
 4. a pod over budget for ``strikes`` consecutive checks is reported (metric, log) and, with
    ``action: evict``, deleted — its slice goes back to the pool and its neighbours' memory is safe.
 
@@ -137,7 +137,7 @@ class HbmGuard:
                  pods_by_device: Optional[Callable[[], Iterable[Tuple[str, str, Any]]]] = None,
                  pods_by_uid: Optional[Callable[[], Mapping[str, PodKey]]] = None,
                  evict: Optional[Callable[[str, str, str], None]] = None, action: str = "report",
-                 slack_bytes: int = 1 << 30, strikes: int = 2, proc_root: str = "/proc",
+                 slack_bytes: int = 768 << 20, strikes: int = 2, proc_root: str = "/proc",
                  partitions: Optional[Callable[[], Mapping[str, Tuple[int, int]]]] = None):
         if action not in ACTIONS:
             raise ValueError(f"hbm guard action {action!r} not in {ACTIONS}")
@@ -223,7 +223,7 @@ class HbmGuard:
         found: List[Violation] = []
         for a in accts:
             seen.add(a.key)
-            limit = a.budget + self.slack_bytes
+            limit = a.budget + self.slack_bytes * max(1, len(a.pids))   # runtime overhead per process
             if a.used <= limit:
                 self._strikes.pop(a.key, None)
                 continue
@@ -235,7 +235,7 @@ class HbmGuard:
             who = f"{a.pod[0]}/{a.pod[1]}" if a.pod else f"slices {','.join(a.slice_ids)}"
             if act == "evict" and a.pod is not None and self.evict is not None and a.pod not in self._evicted:
                 reason = (f"HBM budget exceeded: {a.used} B held on GPU {a.gpu}, budget {a.budget} B "
-                          f"(+{self.slack_bytes} B slack) for slices {','.join(a.slice_ids)}")
+                          f"(+{self.slack_bytes} B slack per process) for slices {','.join(a.slice_ids)}")
                 try:
                     self.evict(a.pod[0], a.pod[1], reason)
                     self._evicted[a.pod] = 0
