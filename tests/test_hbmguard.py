@@ -260,3 +260,24 @@ def test_slack_is_per_process():
             smi.set_process_memory(0, pid, 0)
         smi.set_process_memory(0, 10, 37_600_000_000)
         assert len(g.check()) == 1
+
+
+def test_a_pod_process_cannot_charge_another_pods_slice(node):
+    # pod-a's child process names pod-b's slice in a forged environment: the cgroup says pod-a,
+    # so the VRAM is pod-a's, and pod-b (within its own budget) is never blamed
+    _proc(node.root, 100, UID_A, {"NOS_SLICE_IDS": "gpu0::s1"})
+    node.smi.set_process_memory(0, 100, 50 * GB)
+    node.guard.check()
+    (v,) = node.guard.check()
+    assert v.account.pod == ("team-a", "pod-a") and v.account.slice_ids == ("gpu0::s0",)
+    assert [n for _, n, _ in node.evicted] == ["pod-a"]
+
+
+def test_a_pod_without_a_device_on_the_gpu_is_reported_not_evicted(node):
+    # e.g. the agent's own probe helper: a pod process on a guarded GPU where its pod holds no device
+    uid_agent = "2d7e4c9a-3333-4b2c-9e3c-0f4a5b6c7d8e"
+    node.guard.pods_by_uid = lambda: {UID_A: ("team-a", "pod-a"), uid_agent: ("nos-system", "agent")}
+    _proc(node.root, 100, uid_agent, {})
+    node.smi.set_process_memory(0, 100, 100 * GB)
+    node.guard.check()
+    assert node.guard.check() == [] and node.guard.unattributed == {0: 100 * GB} and node.evicted == []

@@ -11,8 +11,9 @@ loop from outside the container, the way kubelet enforces memory by eviction:
 1. amd-smi's per-process VRAM on every GPU (``AmdSmi.process_memory``: the KFD's own accounting,
    which no container can change);
 2. each process is attributed to a pod by its cgroup (``/proc/<pid>/cgroup`` names the pod UID;
-   kubelet's PodResources gives the pod's slice ids) or, outside Kubernetes, by the
-   ``NOS_SLICE_IDS`` that ``Allocate`` put in its environment;
+   kubelet's PodResources gives the pod's slice ids) — authoritative, so a child process cannot
+   charge another pod's slice by forging its environment — or, for a process in no pod's cgroup,
+   by the ``NOS_SLICE_IDS`` / ``NOS_PARTITION_IDS`` that ``Allocate`` put in its environment;
 3. a pod's VRAM summed over its processes is held against the sum of its slices' budgets plus a
    slack per process for what the HIP runtime maps beyond the interposer's count (code objects,
    queues, scratch: 490 MiB for a PyTorch process, ``profiles/pytest_hbmguard_r4.log``);
@@ -199,12 +200,15 @@ class HbmGuard:
                 pod: Optional[PodKey] = None
                 uid = pod_uid_of(pid, self.proc_root)
                 if uid is not None:
+                    # a pod's process: its cgroup is authoritative (an environment can be forged by
+                    # a child process to charge another pod's slice); a pod holding no device of
+                    # this GPU (the agent's own probe helpers, say) is reported, never evicted
                     pod = pod_of_uid(uid)
-                ids: Tuple[str, ...] = tuple(sorted(ids_of_pod.get(pod, ()))) if pod is not None else ()
-                if not ids:
+                    ids: Tuple[str, ...] = tuple(sorted(i for i in ids_of_pod.get(pod, ()) if budget_of[i][0] == g)) \
+                        if pod is not None else ()
+                else:
                     ids = tuple(i for i in slice_ids_of(pid, self.proc_root) if budget_of.get(i, (None,))[0] == g)
-                    if ids and pod is None:
-                        pod = pod_of_id.get(ids[0])
+                    pod = pod_of_id.get(ids[0]) if ids else None
                 if not ids:
                     self.unattributed[g] = self.unattributed.get(g, 0) + nbytes
                     continue
