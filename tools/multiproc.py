@@ -48,7 +48,7 @@ def scenarios():
     # beyond 8 pods (the bench density phase's mixes, at 14 pods: a box runs at most 16 GPU processes)
     out["dense_14"] = (["32cu.24gb"] * 6 + ["8gb"] * 8, True)
     out["shared_14"] = (["16gb"] * 14, True)
-    for n in (8, 9, 10, 12):   # where process time-slicing starts
+    for n in (6, 8, 9, 10, 12):   # 6: the sharing table's missing count; 9+: where process time-slicing starts
         out[f"shared_{n}"] = (["16gb"] * n, True)
     return out
 
