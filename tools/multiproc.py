@@ -61,6 +61,7 @@ def main() -> int:
     ap.add_argument("--env", default="{}", help="extra env for every pod, JSON (e.g. {\"NOS_POD_STREAMS\": \"4\"})")
     ap.add_argument("--tag", default="", help="suffix of the scenario names in the output")
     ap.add_argument("--stagger", type=float, default=0.0, help="seconds between pod starts")
+    ap.add_argument("--queues", default="", help="GPU_MAX_HW_QUEUES per pod in start order, e.g. 1,2,1,2,1")
     args = ap.parse_args()
     extra = json.loads(args.env)
     todo = scenarios()
@@ -74,12 +75,14 @@ def main() -> int:
     for name, (profiles, shim) in todo.items():
         t0 = time.time()
         dedicated = all("cu." in p for p in profiles)
+        per = [{"GPU_MAX_HW_QUEUES": q} for q in args.queues.split(",")] if args.queues else None
         r = run_pods(profiles, seconds=args.seconds, shim=shim, census=dedicated, extra_env=extra,
-                     stagger_s=args.stagger)
+                     stagger_s=args.stagger, per_pod_env=per)
         r["profiles"] = profiles
         r["shim"] = shim
         r["env"] = extra
         r["stagger_s"] = args.stagger
+        r["queues"] = args.queues
         r["wall_s"] = round(time.time() - t0, 1)
         rates = [p["inf_per_s"] for p in r["per_pod"]]
         r["per_pod_max_over_min"] = round(max(rates) / max(1e-9, min(rates)), 3) if rates else None

@@ -71,9 +71,11 @@ def allocate_envs(profiles: Sequence[str], cu_count: int = 256, shim: bool = Tru
 
 def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, census: bool = False,
              graphs: bool = True, ready_timeout: float = 600.0, extra_env: Optional[Dict[str, str]] = None,
-             cu_count: int = 256, stagger_s: float = 0.0) -> Dict[str, Any]:
+             cu_count: int = 256, stagger_s: float = 0.0,
+             per_pod_env: Optional[Sequence[Dict[str, str]]] = None) -> Dict[str, Any]:
     """Start one process per profile, release them together, collect their JSON lines.
-    ``stagger_s``: wait this long between pod starts (pods of a node start at different times)."""
+    ``stagger_s``: wait this long between pod starts (pods of a node start at different times);
+    ``per_pod_env``: env overrides of pod i (after ``extra_env``)."""
     envs = allocate_envs(profiles, cu_count, shim)
     pods: List[PodProc] = []
     base = dict(os.environ)
@@ -88,7 +90,8 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
     logs = []
     try:
         for i, (prof, env) in enumerate(zip(profiles, envs)):
-            e = {**base, **env, "NOS_POD_SEED": str(i), **(extra_env or {})}  # extra_env overrides Allocate's
+            e = {**base, **env, "NOS_POD_SEED": str(i), **(extra_env or {}),  # extra_env overrides Allocate's
+                 **(per_pod_env[i] if per_pod_env and i < len(per_pod_env) else {})}
             log = tempfile.TemporaryFile(mode="w+")  # a full stderr pipe would stall the pod
             logs.append(log)
             p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
