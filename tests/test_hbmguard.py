@@ -281,3 +281,36 @@ def test_a_pod_without_a_device_on_the_gpu_is_reported_not_evicted(node):
     node.smi.set_process_memory(0, 100, 100 * GB)
     node.guard.check()
     assert node.guard.check() == [] and node.guard.unattributed == {0: 100 * GB} and node.evicted == []
+
+
+def test_native_process_memory_binding_grows_its_buffer():
+    """NativeAmdSmi._process_memory over the C ABI: a list longer than the buffer is re-read with
+    a bigger one; a negative count is an error (the library itself is exercised on the GPU box)."""
+    import threading
+
+    from walkai_nos_amd.device.amdsmi import NativeAmdSmi
+    from walkai_nos_amd.models.errors import GpuError
+
+    class Lib:
+        def __init__(self, procs):
+            self.procs, self.calls = procs, []
+
+        def nos_smi_process_memory(self, ordinal, pids, vram, cap):
+            self.calls.append(cap)
+            if self.procs is None:
+                return -1
+            for i, (p, b) in enumerate(self.procs[:cap]):
+                pids[i], vram[i] = p, b
+            return len(self.procs)
+
+        def nos_smi_last_error(self):
+            return b"amdsmi_get_gpu_process_list failed"
+
+    smi = object.__new__(NativeAmdSmi)
+    smi._lock = threading.Lock()
+    smi._lib = Lib([(1000 + i, i * GB) for i in range(70)])
+    got = smi._process_memory(SimpleNamespace(ordinal=0))
+    assert len(got) == 70 and got[1069] == 69 * GB and smi._lib.calls == [64, 86]
+    smi._lib = Lib(None)
+    with pytest.raises(GpuError):
+        smi._process_memory(SimpleNamespace(ordinal=0))
