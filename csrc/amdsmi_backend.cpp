@@ -261,6 +261,39 @@ int nos_smi_process_memory(uint32_t idx, uint32_t* pids, uint64_t* vram, uint32_
   return int(got);
 }
 
+// Per-process VRAM, CU occupancy and queue-eviction time on this processor (the slice guards'
+// input): cu_occupancy is the KFD's CU-equivalents of the process's waves in flight (waves /
+// waves-per-CU, sampled when read), evicted_ms the time its queues spent evicted (time-sliced
+// out by the hardware scheduler). Fills up to cap entries; returns the process count, or -1.
+int nos_smi_process_info(uint32_t idx, uint32_t* pids, uint64_t* vram, uint32_t* cu_occupancy,
+                         uint32_t* evicted_ms, uint32_t cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  amdsmi_processor_handle h;
+  if (handle(idx, &h)) return -1;
+  uint32_t n = 0;
+  amdsmi_status_t st = amdsmi_get_gpu_process_list(h, &n, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) {
+    map_status(st, "amdsmi_get_gpu_process_list");
+    return -1;
+  }
+  if (n == 0 || cap == 0) return int(n);
+  std::vector<amdsmi_proc_info_t> list(n);
+  uint32_t got = n;
+  st = amdsmi_get_gpu_process_list(h, &got, list.data());
+  if (st != AMDSMI_STATUS_SUCCESS && st != AMDSMI_STATUS_OUT_OF_RESOURCES) {
+    map_status(st, "amdsmi_get_gpu_process_list");
+    return -1;
+  }
+  uint32_t k = got < n ? got : n;
+  for (uint32_t i = 0; i < k && i < cap; ++i) {
+    pids[i] = uint32_t(list[i].pid);
+    vram[i] = list[i].memory_usage.vram_mem ? list[i].memory_usage.vram_mem : list[i].mem;
+    cu_occupancy[i] = list[i].cu_occupancy;
+    evicted_ms[i] = list[i].evicted_time;
+  }
+  return int(got);
+}
+
 int nos_smi_activity(uint32_t idx, uint32_t* gfx, uint32_t* umc, uint32_t* mm) {
   std::lock_guard<std::mutex> lk(g_mu);
   amdsmi_processor_handle h;

@@ -275,3 +275,42 @@ def test_slices_node_turns_an_idle_hardware_gpu_into_a_sliced_one():
     assert {ko.name(p) for p in c.running_pods()} == {"d0", "c0"}
     assert [(k, g, m) for k, g, m in sn.smi.set_calls] == [("compute", 0, "SPX")]
     assert ko.annotations(c.api.get("Node", "node-0"))[api.ANNOTATION_SLICED_GPUS_STATUS] == "0"
+
+
+class _BusyGpuClient:
+    """A partition client whose GPUs 0 (CPX, processes on it) and 1 (already SPX) are planned sliced."""
+
+    def __init__(self):
+        self.modes = {0: "cpx_nps1", 1: "spx_nps1"}
+        self.set_calls = []
+
+    def current_profiles(self):
+        return dict(self.modes)
+
+    def gpu_busy(self, gpu):
+        return gpu == 0
+
+    def set_profile(self, gpu, profile):
+        self.set_calls.append((gpu, profile))
+        self.modes[gpu] = profile
+
+
+def test_actuator_keeps_no_slice_layout_for_a_gpu_whose_spx_flip_was_skipped_as_busy():
+    """a skipped (busy) flip to SPX must not save the GPU's new slice layout — the reporter
+    would publish a CPX GPU as sliced and the plugin would stop withholding it."""
+    from walkai_nos_amd.controllers.agent.actuator import Actuator
+    from walkai_nos_amd.controllers.agent.plan import ModeChange, XcpConfigPlan
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    from walkai_nos_amd.device.slicing_client import MemorySliceStore
+    from walkai_nos_amd.kube.memory import InMemoryAPIServer
+    store = MemorySliceStore()
+    pc = _BusyGpuClient()
+    act = Actuator(InMemoryAPIServer(), pc, SharedState(), "node-a", journal=False, slice_store=store)
+    act._votes = lambda applied: [True]
+    plan = XcpConfigPlan(changes=[ModeChange(0, "cpx_nps1", "spx_nps1")],
+                         slices={0: [_slice("g0::x0", "dpx_nps1", [0, 1, 2, 3])],
+                                 1: [_slice("g1::x0", "cpx_nps1", [0])]})
+    err = act.apply(plan, "p1")
+    assert err is not None and pc.set_calls == []                    # busy: not flipped, retried later
+    assert set(store.load()) == {1}                                  # GPU 1 (SPX) re-carved; GPU 0 untouched
+    assert [s.id for s in store.load()[1]] == ["g1::x0"]

@@ -232,3 +232,57 @@ def test_cumask_node_serves_at_most_its_slice_cap(label, running):
         c.submit({"amd.com/gpu-8gb": 1}, name=f"m{i}")
     c.run(120)
     assert len(c.running_pods()) == running and len(c.pending_pods()) == 12 - running
+
+
+@pytest.mark.parametrize("failure", ["factory", "vote", "veto"])
+def test_slice_agent_commit_failure_restores_the_layout_and_finishes_the_apply(failure):
+    """a barrier that cannot be built, raises or vetoes leaves the old layout in
+    the store, the plugin re-read and the apply recorded (ref ``actuator.go:181-184`` rollback)."""
+    from walkai_nos_amd.controllers.agent.shared import SharedState
+    from walkai_nos_amd.controllers.sliceagent.agent import SliceActuator
+    from walkai_nos_amd.device.amdsmi import FakeAmdSmi
+    from walkai_nos_amd.device.podresources import StaticResourceClient
+    from walkai_nos_amd.device.slicing_client import MemorySliceStore, SlicingClient
+    from walkai_nos_amd.kube.memory import InMemoryAPIServer
+    from walkai_nos_amd.kube.runtime import Request
+
+    class Barrier:
+        def vote_all(self, votes):
+            if failure == "vote":
+                raise RuntimeError("helper died")
+            return failure != "veto"
+
+        def close(self):
+            pass
+
+    def factory(n):
+        if failure == "factory":
+            raise FileNotFoundError("nos-gpuhelper not built")
+        return Barrier()
+
+    class Plugin:
+        restarts = 0
+
+        def restart(self, node, timeout=60.0):
+            Plugin.restarts += 1
+
+    smi = FakeAmdSmi(n_gpus=1)
+    bdf = smi.list_gpus()[0].bdf
+    store = MemorySliceStore()
+    old = {0: [Slice(f"{bdf}::s0", "256cu.288gb", list(range(32)))]}
+    store.save(old)
+    api_ = InMemoryAPIServer()
+    node = ko.new_node("n0", {})
+    node["metadata"]["annotations"] = {"nos.nebuly.com/spec-gpu-0-32cu.36gb": "2",
+                                       "nos.nebuly.com/status-gpu-0-256cu.288gb-free": "1",
+                                       "nos.nebuly.com/spec-partitioning-plan": "7"}
+    api_.create(node)
+    shared = SharedState()
+    shared.on_report_done()
+    sc = SlicingClient(StaticResourceClient(lambda: [], lambda: []), smi)
+    act = SliceActuator(api_, sc, store, shared, "n0", device_plugin=Plugin(), barrier_factory=factory)
+    with pytest.raises(GpuError):
+        act.reconcile(Request("n0"))
+    assert store.load() == old                                 # the old layout is back
+    assert Plugin.restarts == 1                                # the plugin re-read it
+    assert shared.last_commit and not shared.at_least_one_report_since_last_apply()   # apply recorded

@@ -19,6 +19,12 @@
 #   pmc_op             PMC passes over one op (NOS_OP, NOS_SLICE), counters in their own runs
 #   pmc_modes          L2 counters of a partition mode with all partitions busy (NOS_MODE, NOS_PARTS)
 #   kbench             tools/kbench.py per-op / per-mode microbenchmarks (NOS_KBENCH_ARGS)
+#   bench_runs         bench.py once per NOS_BENCH_RUNS entry ("<tag>:<arg>,<arg> ..."), e.g. layouts / seeds
+#   bench_long         bench.py over NOS_STEPS quanta (default 100) for a longer window
+#   fair               tools/gpu_fair.sh: memory-only fairness as processes (NOS_FAIR_ONLY, NOS_FAIR_VARIANTS)
+#   replay             tools/model_replay.py + replay_stats kernel traces per slice (NOS_SLICES, default "dpx cpx")
+#   procs_cap          tools/multiproc.py at 8-12 memory-only pods + the KFD queue properties
+#   cu_guard           the CU-mask bypass guard test on real amd-smi (gpurun_out/cu_guard_samples.json)
 #   attn_proj          tools/attn_proj_probe.py: fused merge+projection+LayerNorm vs the unfused launches
 #   pmc_attn_proj      PMC passes over the fused kernel (NOS_ABLATE = its timing-only ablation mask)
 set -u
@@ -102,6 +108,30 @@ for s in "$@"; do
       pmc "$D" p4 "${P[@]}" -- TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE
       rc=$?; echo "pmc_attn_proj rc=$rc" | tee -a "$OUT/gpu_sh.log"; [ $rc -eq 0 ] || exit $rc ;;
     kbench) step kbench 600 python tools/kbench.py ${NOS_KBENCH_ARGS:-} --out "$OUT/kbench.json" ;;
+    bench_runs)
+      for spec in ${NOS_BENCH_RUNS:-slices_1234:--layout=slices partitions_1234:--layout=partitions}; do
+        tag=${spec%%:*}; args=${spec#*:}
+        step "bench_$tag" 400 python -u bench.py ${args//,/ } --out "$OUT/bench_$tag.json"
+      done ;;
+    bench_long) step "bench_${NOS_STEPS:-100}q" 900 python -u bench.py --steps "${NOS_STEPS:-100}" --warmup 5 \
+                  --out "$OUT/bench_${NOS_STEPS:-100}q.json" ;;
+    fair) step fair 1100 bash tools/gpu_fair.sh ;;
+    replay)
+      mkdir -p "$OUT/replay"
+      for sl in ${NOS_SLICES:-dpx cpx}; do
+        step "replay_$sl" 300 bash -c "cd /tmp && rocprofv3 --kernel-trace --output-format csv -d '$OUT/replay' -o $sl \
+          -- python3 '$ROOT/tools/model_replay.py' --slice $sl --replays 20"
+        f=$(find "$OUT/replay" -name "${sl}_kernel_trace.csv" | sort | tail -1)
+        step "replay_stats_$sl" 120 python tools/replay_stats.py "$f" --replays 20
+      done ;;
+    procs_cap)
+      step procs_cap 700 python -u tools/multiproc.py --seconds 8 --only shared_8,shared_9,shared_10,shared_12 \
+        --out "$OUT/procs_cap.json"
+      for f in /sys/class/kfd/kfd/topology/nodes/*/properties; do
+        grep -H -E "simd_count|max_waves|num_cp_queues|num_xcc|cp_queue|vmid" "$f" || true
+      done > "$OUT/kfd_props.txt" 2>&1 ;;
+    cu_guard) step cu_guard 300 python -u -m pytest tests/test_gpu_native.py -x -v -rs -s --timeout 240 \
+                --timeout-method thread -k cu_guard ;;
     *) echo "unknown step $s" | tee -a "$OUT/gpu_sh.log"; exit 2 ;;
   esac
 done

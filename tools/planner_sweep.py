@@ -28,7 +28,8 @@ def run(job):
     pp = r["per_profile"]
     return {"gpus": gpus, "load": load, "seed": seed, "util_pct": r["util_pct"], "flips": r["flips"],
             "time_in_flip_pct": r["time_in_flip_pct"], "pending_mean": r["pending_mean"],
-            "inf_per_s_model": r["inf_per_s_model"],
+            "inf_per_s_model": r["inf_per_s_model"], "offered_pct": r["idle"]["offered_pct"],
+            "idle_pct": r["idle"]["by_cause_pct"],
             "tts_p99_lifetimes": {p: v.get("tts_lifetimes_p99") for p, v in pp.items()},
             "pods_bound": {p: v["pods_bound"] for p, v in pp.items()}}
 
@@ -41,8 +42,8 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--pack", default="{}", help="PackParams overrides as JSON")
     ap.add_argument("--workers", type=int, default=6)
-    ap.add_argument("--layout", default="partitions", help="xcp-layout of the node: partitions | slices | auto")
-    ap.add_argument("--out", default="profiles/planner_sweep_r3.json")
+    ap.add_argument("--layout", default="slices", help="xcp-layout of the node: partitions | slices | auto")
+    ap.add_argument("--out", default="profiles/planner_sweep_r5_slices.json")
     a = ap.parse_args()
     pack = json.loads(a.pack)
     jobs = list(itertools.product([int(g) for g in a.gpus.split(",")], [float(x) for x in a.loads.split(",")],
@@ -60,6 +61,8 @@ def main() -> int:
             "flips_mean": round(sum(r["flips"] for r in grp) / len(grp), 1),
             "time_in_flip_pct_mean": round(sum(r["time_in_flip_pct"] for r in grp) / len(grp), 2),
             "pending_mean": round(sum(r["pending_mean"] for r in grp) / len(grp), 2),
+            "offered_pct_mean": round(sum(r["offered_pct"] for r in grp) / len(grp), 2),
+            "idle_pct_mean": {k: round(sum(r["idle_pct"][k] for r in grp) / len(grp), 2) for k in grp[0]["idle_pct"]},
             "tts_p99_lifetimes_worst_seed": tts}
         print(f"{g}gpu/load{l}", json.dumps(cells[f"{g}gpu/load{l}"]), flush=True)
     out = {"steps": a.steps, "seeds": a.seeds, "pack_overrides": pack, "layout": a.layout, "cells": cells, "rows": rows}

@@ -131,11 +131,19 @@ class AgentConfig(ManagerConfig):
     #: VRAM each process may map beyond what the budget interposer counts (HIP runtime, code
     #: objects: 490 MiB measured for a PyTorch process)
     hbmGuardSlackBytes: int = 768 << 20
+    #: pods running on more CUs than their slices have (HSA_CU_MASK bypassed; amd-smi per-process
+    #: CU occupancy, controllers/hbmguard.py): off | report (metric + Warning event) | evict
+    cuGuard: str = "report"
+    cuGuardStrikes: int = 3
 
     def validate(self) -> None:
         super().validate()
         if self.hbmGuard not in ("off", "report", "evict"):
             raise ValueError("hbmGuard must be 'off', 'report' or 'evict'")
+        if self.cuGuard not in ("off", "report", "evict"):
+            raise ValueError("cuGuard must be 'off', 'report' or 'evict'")
+        if self.cuGuardStrikes < 1:
+            raise ValueError("cuGuardStrikes must be >= 1")
         if self.hbmGuardIntervalSeconds <= 0:
             raise ValueError("hbmGuardIntervalSeconds must be greater than 0")
         if self.hbmGuardSlackBytes < 0:

@@ -80,6 +80,8 @@ CUMASK_DENSITY = {"cumask": (("32cu.24gb", 6), ("8gb", 10)), "cumask_shared": ((
 #: spread, while one partition alone runs 16.1 vs 14.8 ms per inference
 #: (profiles/partition_emulation_r2.json). ``NOS_PARTITION_EMULATION`` overrides.
 EMULATION = os.environ.get("NOS_PARTITION_EMULATION", "spread")
+#: why a GPU's capacity went unallocated in a quantum (``NodeBench._account_idle``)
+IDLE_CAUSES = ("flip_outage", "drain", "fragmentation", "placement_lag", "no_demand")
 XCDS = 8
 #: emulations whose partitions run on their own XCDs (kernels pinned with ``csrc/pin.h``). "landing":
 #: pinned, and the CU mask gives a partition its own XCDs minus one CU per XCD plus that reserved
@@ -658,6 +660,8 @@ class NodeBench:
         self.profile_pods: Dict[str, set] = collections.defaultdict(set)        # pods that served in the window
         self.tts: Dict[str, List[float]] = collections.defaultdict(list)        # bound in the window: wait (s)
         self.dark_wall_s = 0.0
+        self.idle_acct: Dict[str, float] = collections.defaultdict(float)  # cause -> GPU-quanta
+        self.offered_gpu_quanta = 0.0    # GPU-quanta of work that arrived (expected lifetime x size)
 
     def dark(self, gpu: int, node: Optional[str] = None) -> float:
         """Fraction of this quantum ``gpu`` of ``node`` (default: this rank's node) is dark (flip outage)."""
@@ -692,6 +696,7 @@ class NodeBench:
             name = f"p{self.churn.seq}"
             c.submit({f"amd.com/{prof}": 1}, name=name)
             self.profile_of[name] = prof
+            self.offered_gpu_quanta += self.cfg.mean_lifetime_quanta / COMPUTE_MODES[prof.split("_")[0]]
             self.created[name] = now
             self.churn.seq += 1
         c.run(self.cfg.cluster_s)
@@ -713,6 +718,7 @@ class NodeBench:
             if n not in self.live:
                 self.live[n] = float(self.churn.lifetime())
         frac = c.gpu_allocated_fraction()
+        self._account_idle(frac)
         self.raw_util_samples.append(100.0 * sum(frac.values()) / max(1, len(frac)))
         self.util_samples.append(100.0 * sum(v * (1.0 - self.dark(g, n)) for (n, g), v in frac.items())
                                  / max(1, len(frac)))
@@ -721,6 +727,55 @@ class NodeBench:
         self.gpu_quanta += self.cfg.gpus * self.cfg.nodes
         self.outage_gpu_quanta += sum(self.dark(g, n) for (n, g) in frac)
         self.host_s["control"] += time.perf_counter() - t0
+
+    def _account_idle(self, frac: Dict[Tuple[str, int], float]) -> None:
+        """Charge every GPU's unallocated share of this quantum to one cause (:data:`IDLE_CAUSES`),
+        in GPU-quanta: ``flip_outage`` (dark), ``drain`` (the GPU's spec asks for what it cannot
+        host yet: no new pod is placed on it until enough leave), ``fragmentation`` (pods wait, but
+        every one of them is bigger than the GPU's unused room — on a hardware-partitioned GPU: no
+        waiting pod asks for its free partitions' profile), ``placement_lag`` (a waiting pod would
+        fit: the control plane has not placed it yet) and ``no_demand`` (nothing waits)."""
+        from .models.xcp import node as xnode
+        waiting = [self.profile_of.get(ko.name(p), "") for p in self.cluster.pending_pods()]
+        waiting = [p for p in waiting if p]
+        for nname, sn in self.cluster.nodes.items():
+            try:
+                model = xnode.new_node(self.cluster.api.get("Node", nname))
+            except (ValueError, KeyError, NotImplementedError):
+                model = None
+            gpus = {g.index: g for g in model.gpus} if model is not None else {}
+            for idx in range(self.cfg.gpus):
+                v = frac.get((nname, idx))
+                if v is None:
+                    continue
+                dark = self.dark(idx, nname)
+                self.idle_acct["flip_outage"] += dark
+                idle = max(0.0, 1.0 - v) * (1.0 - dark)
+                if idle <= 1e-9:
+                    continue
+                g = gpus.get(idx)
+                if g is not None and g.target is not None:
+                    cause = "drain"
+                elif not waiting:
+                    cause = "no_demand"
+                elif g is not None and getattr(g, "sliced", False):
+                    need = min(1.0 / COMPUTE_MODES[p.split("_")[0]] for p in waiting)
+                    cause = "placement_lag" if need <= idle + 1e-9 else "fragmentation"
+                elif g is not None:
+                    cause = "placement_lag" if any(g.free.get(p, 0) > 0 for p in waiting) else "fragmentation"
+                else:
+                    cause = "fragmentation"
+                self.idle_acct[cause] += idle
+
+    def idle_report(self) -> Dict[str, Any]:
+        """Unallocated GPU-quanta of the window by cause, and each cause's share of GPU time (%);
+        ``offered_pct``: the work that arrived in the window, in % of the window's GPU time (below 100
+        allocation is bounded by it, plus what the queue held when the window began)."""
+        total = max(1, self.gpu_quanta)
+        return {"gpu_quanta": self.gpu_quanta,
+                "offered_pct": round(100.0 * self.offered_gpu_quanta / total, 2),
+                "by_cause_gpu_quanta": {k: round(self.idle_acct.get(k, 0.0), 3) for k in IDLE_CAUSES},
+                "by_cause_pct": {k: round(100.0 * self.idle_acct.get(k, 0.0) / total, 2) for k in IDLE_CAUSES}}
 
     def end_step(self) -> None:
         """Age every running pod by the part of the quantum its GPU was lit, then let outages run."""
@@ -1236,7 +1291,8 @@ def control_only(cfg: BenchConfig, steps: int, skip: int = 0) -> Dict[str, Any]:
             "pods_per_gpu": round(_mean(nb.pods_samples) / cfg.gpus, 2),
             "inf_per_s_model": round(served / (n * cfg.quantum_s), 1),
             "admission_failures": nb.cluster.admission_failures,
-            "per_profile": nb.profile_report(n * cfg.quantum_s)}
+            "per_profile": nb.profile_report(n * cfg.quantum_s),
+            "idle": nb.idle_report()}
 
 
 def smoke_step() -> None:

@@ -58,7 +58,8 @@ def nos_partition_plugin(client, node: str, smi, resources, cfg, slice_store=Non
                            slices=slice_store.load if slice_store is not None else None, degraded=degraded)
     plugins = partition_plugin_manager(state, socket_dir=cfg.devicePluginDir,
                                        kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
-                                       shim_path=cfg.hbmLimitShimPath)
+                                       shim_path=cfg.hbmLimitShimPath,
+                                       shim_present=lambda: os.path.exists(cfg.hbmLimitShimPath))
     publisher = AllocatablePublisher(client, node) if cfg.publishAllocatable else None
     return PartitionPluginHook(plugins, state, publisher), plugins
 
@@ -118,12 +119,15 @@ def main(argv=None) -> int:
     log.info("start-up reconciliation: %s", actuator.startup())
     from ..exporters.gpu_metrics import GpuMetricsPoller
     GpuMetricsPoller(smi, node).register(mgr)
-    from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_evictor, shared_memory_partitions
-    # sliced GPUs' slices, and hardware partitions sharing one memory pool (CPX on NPS1)
+    from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_event, pod_evictor, shared_memory_partitions
+    # sliced GPUs' slices (HBM budget and CU mask), and hardware partitions sharing one memory pool
+    # (CPX on NPS1: HBM only, their CUs are hardware-isolated)
     HbmGuard(smi, slice_store.load if slice_store is not None else dict, node,
              pods_by_device=resources.get_used_devices_by_pod, pods_by_uid=node_pods_by_uid(client, node),
              evict=pod_evictor(client, node), action=cfg.hbmGuard, slack_bytes=cfg.hbmGuardSlackBytes,
-             partitions=lambda: shared_memory_partitions(smi.device_map())).register(mgr, cfg.hbmGuardIntervalSeconds)
+             partitions=lambda: shared_memory_partitions(smi.device_map()), cu_action=cfg.cuGuard,
+             cu_strikes=cfg.cuGuardStrikes, cu_count=smi.device_map().gpus[0].cu_count or 256,
+             event=pod_event(client, node)).register(mgr, cfg.hbmGuardIntervalSeconds)
     serve_endpoints(mgr, cfg)
     stop = None
     if plugins is not None:

@@ -67,10 +67,11 @@ def main(argv=None) -> int:
     threading.Thread(target=run_forever, args=(plugins, 2.0, stop), daemon=True).start()
     from ..exporters.gpu_metrics import GpuMetricsPoller
     GpuMetricsPoller(smi, node).register(mgr)
-    from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_evictor
+    from ..controllers.hbmguard import HbmGuard, node_pods_by_uid, pod_event, pod_evictor
     HbmGuard(smi, store.load, node, pods_by_device=sc.resources.get_used_devices_by_pod,
              pods_by_uid=node_pods_by_uid(client, node), evict=pod_evictor(client, node), action=cfg.hbmGuard,
-             slack_bytes=cfg.hbmGuardSlackBytes).register(mgr, cfg.hbmGuardIntervalSeconds)
+             slack_bytes=cfg.hbmGuardSlackBytes, cu_action=cfg.cuGuard, cu_strikes=cfg.cuGuardStrikes,
+             cu_count=cu_count, event=pod_event(client, node)).register(mgr, cfg.hbmGuardIntervalSeconds)
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr, stop)
 

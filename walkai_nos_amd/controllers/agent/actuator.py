@@ -49,7 +49,7 @@ from ...kube.runtime import Request, Result
 from ...models import annotation as ann
 from ...models.errors import GpuError, is_not_found
 from ...models.xcp.profile import parse_profile
-from ...models.xcp.slices import parse_gpu_set
+from ...models.xcp.slices import SLICED_MODE, parse_gpu_set
 from ...parallel.barrier import CommitBarrier
 from ...utils.metrics import REGISTRY
 from .plan import XcpConfigPlan, XcpState, new_xcp_config_plan
@@ -209,8 +209,13 @@ class Actuator:
         if ok and plan.slices and self.slice_store is not None:
             # a re-carve is a configuration change only (no device operation, nothing to vote on):
             # the plugin serves the new layout after its next sync
+            # only for GPUs in SPX now: a GPU whose flip to SPX was skipped (busy) keeps its hardware
+            # partitions, and a saved layout would make the reporter publish it as sliced
+            modes = self.pc.current_profiles()
+            ready = {g: ss for g, ss in plan.slices.items()
+                     if g not in busy and (not ss or str(modes.get(g, "")).startswith(SLICED_MODE))}
             cur = self.slice_store.load()
-            cur.update({g: ss for g, ss in plan.slices.items()})
+            cur.update(ready)
             self.slice_store.save({g: ss for g, ss in cur.items() if ss})
             changed = True
         if not ok and flipped:

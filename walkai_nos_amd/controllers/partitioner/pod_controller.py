@@ -35,6 +35,7 @@ from ...models.xcp import node as xcp_node
 from ...partitioning.planner import Partitioner, build_node_partitioning, new_plan_id
 from ...utils import pod as podutil
 from ...utils.metrics import REGISTRY
+from .lifetimes import LifetimeTracker
 
 log = logging.getLogger("nos.partitioner")
 
@@ -181,8 +182,16 @@ class PackParams:
                                     # single GPU cycle through the modes its pods ask for
     slice_reserve_after: float = 900.0  # seconds: sliced GPUs (xcp-layout slices/auto) — the oldest pod that
                                     # fits on no sliced GPU this long drains one for itself (0 = never)
+    slice_reserve_lifetimes: float = 3.75  # ... once the planner has seen pods finish (lifetimes.py): this
+                                    # many median pod run times instead (0 = keep the constant)
     slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
-    slice_reserve_stretch: float = 2.0  # ... at most this many times
+    slice_reserve_stretch: float = 1.5  # ... at most this many times
+    slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed
+    slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
+    slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
+    slice_whole_overtake: float = 960.0  # seconds: a whole-GPU slice left free goes to the next whole-GPU pod
+                                    # unless the oldest waiting pod is this much older (0 = strict FIFO)
+    slice_whole_overtake_lifetimes: float = 4.0  # ... this many median pod run times once learned (0 = constant)
     slice_fill: bool = True         # carve a sliced GPU's leftover groups into cpx slices
 
 
@@ -283,7 +292,9 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
                       incoming: Optional[Mapping[str, int]] = None, params: Optional[PackParams] = None,
                       spx_demand: float = 0.0,
                       mode_age: Optional[Callable[[str, int], float]] = None,
-                      last_served: Optional[Mapping[str, float]] = None) -> Dict[str, NodeModel]:
+                      last_served: Optional[Mapping[str, float]] = None,
+                      pods_of: Optional[Callable[[str, int], List[Tuple[int, float]]]] = None,
+                      life: Any = None) -> Dict[str, NodeModel]:
     """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
     reference's "first node that can change wins").
 
@@ -344,16 +355,21 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
                         out[prof] = q
         return out
     free_of = {n: best_free(current[n]) for n in names}
+    placed_on: Dict[Tuple[str, int], float] = {}   # (node, GPU) -> oldest pod given a free partition there
     for req, age in pending:
         placed = False
         for name in names:
             bf = free_of[name]
             if any(bf.get(prof, 0) < q for prof, q in req.items()):
                 continue
+            before = [dict(g.used) for g in current[name].gpus]
             try:
                 current[name].add_pod(req)
                 free_of[name] = best_free(current[name])
                 placed = True
+                for g, b in zip(current[name].gpus, before):
+                    if g.used != b:
+                        placed_on[(name, g.index)] = max(age, placed_on.get((name, g.index), 0.0))
                 break
             except ValueError:
                 continue
@@ -367,7 +383,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         return changed
     if any(getattr(m, "layout", "partitions") != "partitions" for m in current.values()):
         from .sliced import plan_sliced
-        plan_sliced(current, models, changed, unserved, params, mode_age)
+        plan_sliced(current, models, changed, unserved, params, mode_age, pods_of, life, placed_on)
         if not unserved:
             return changed
     # the homogeneous rules below only touch GPUs of nodes laid out as hardware partitions
@@ -567,6 +583,7 @@ class PodController:
         self._mode_since: Dict[Tuple[str, int], Tuple[Optional[str], float]] = {}  # (node, gpu) -> (mode, since)
         self._last_served: Dict[str, float] = {}  # profile -> last time a GPU was in its mode
         self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
+        self.lifetimes = LifetimeTracker()        # run times of finished pods (sliced-GPU drains)
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -688,6 +705,34 @@ class PodController:
                     self._mode_since[(name, g.index)] = (mode, now)
         return lambda name, idx: now - self._mode_since.get((name, idx), (None, float("-inf")))[1]
 
+    def _gpu_pods(self, nodes: List[Dict[str, Any]], now: float) -> Callable[[str, int], List[Tuple[int, float]]]:
+        """(groups, seconds run) of the pods on each GPU: the agents' ``status-pods`` annotation
+        names them, their ``startTime`` dates them; feeds the lifetime model as pods finish."""
+        import json
+
+        from ...models.xcp.slices import groups_of
+        names = {ko.name(n) for n in nodes}
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Running", copy=False)
+                if ko.pod_node_name(p) in names]
+        groups: Dict[str, int] = {}
+        mine = []
+        for p in pods:
+            r = requested_profiles(self.kind, p)
+            if r:
+                mine.append(p)
+                groups["/".join(ko.key(p))] = sum(groups_of(k) * q for k, q in r.items())
+        ages = self.lifetimes.update(mine, now)
+        by: Dict[Tuple[str, int], List[Tuple[int, float]]] = {}
+        for n in nodes:
+            try:
+                doc = json.loads(ko.annotations(n).get(api.ANNOTATION_GPU_PODS_STATUS) or "{}")
+            except ValueError:
+                continue
+            for g, keys in doc.items():
+                if str(g).isdigit():
+                    by[(ko.name(n), int(g))] = [(groups[k], ages[k]) for k in keys if k in ages and k in groups]
+        return lambda name, idx: by.get((name, idx), [])
+
     def _update_spx_demand(self, nodes: List[Dict[str, Any]], pending: List[Tuple[Dict[str, int], float]]) -> None:
         """EMA of whole-GPU demand: SPX partitions in use plus SPX pods waiting."""
         used = 0
@@ -793,8 +838,11 @@ class PodController:
                     incoming[p] = incoming.get(p, 0) + q
             pend = self.pending_with_age()
             self._update_spx_demand(nodes, pend)
+            pods_of = self._gpu_pods(nodes, now) \
+                if any(getattr(m, "layout", "partitions") != "partitions" for m in models.values()) else None
             changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand,
-                                        self._mode_ages(models, now), self._served(models, now))
+                                        self._mode_ages(models, now), self._served(models, now),
+                                        pods_of, self.lifetimes.model)
             need = requested
         elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}

@@ -53,10 +53,13 @@ def _hardware_gpu(g: Any, profile: str) -> Any:
 
 
 def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: Dict[str, Any], unserved: Pending,
-                params: Any, mode_age: Optional[Callable[[str, int], float]] = None) -> None:
+                params: Any, mode_age: Optional[Callable[[str, int], float]] = None,
+                pods_of: Optional[Callable[[str, int], List[Tuple[int, float]]]] = None, life: Any = None,
+                placed_on: Optional[Mapping[Tuple[str, int], float]] = None) -> None:
     """Layout choice, backfill, reservation and fill for the sliced GPUs of ``current`` (module
     docstring); places the pods it can (removing them from ``unserved``) and records the nodes
-    whose spec changed in ``changed``."""
+    whose spec changed in ``changed``. ``placed_on``: (node, GPU) -> age of the oldest pending pod
+    the caller already gave a free slice there in this pass."""
     before = {n: [_spec(g) for g in m.gpus] for n, m in original.items()}
 
     def past_stint(name: str, idx: int) -> bool:
@@ -91,16 +94,86 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     for _, g in sliced:
         if g.target is not None and g.target_sliced:
             g.target = None
-    # 2./3. backfill and reservation, oldest first. Under overload the threshold stretches with the
-    # backlog (GPUs of waiting work per sliced GPU): every drain idles groups, and when the queue is
-    # long anyway, batching whole-GPU pods less often serves more and shortens the waits behind them
+    # thresholds: seconds until the planner has seen pods finish, then multiples of their median
+    # run time (a cluster whose pods run for hours is not judged by a bench's minutes)
+    learned = life is not None and life.ready()
+    median = life.median() if learned else None
+    reserve_after = params.slice_reserve_after
+    overtake = params.slice_whole_overtake
+    if learned and params.slice_reserve_lifetimes > 0:
+        reserve_after = params.slice_reserve_lifetimes * median
+    if learned and params.slice_whole_overtake_lifetimes > 0:
+        overtake = params.slice_whole_overtake_lifetimes * median
+    # under overload the reservation threshold stretches with the backlog (GPUs of waiting work per
+    # sliced GPU): every drain idles groups, and when the queue is long anyway, draining for
+    # whole-GPU pods less often serves more and shortens the waits behind them
     backlog = sum(groups_of(s[0]) * s[1] / 8.0 for s in (_single(r) for r, _ in unserved)
                   if s is not None and is_slice_profile(s[0])) / max(1, len(sliced))
-    reserve_after = params.slice_reserve_after
     if params.slice_reserve_backlog > 0:
         reserve_after *= min(params.slice_reserve_stretch, max(1.0, backlog / params.slice_reserve_backlog))
+    aged = learned and pods_of is not None
+
+    def drain_key(name: str, g: Any, need: int) -> float:
+        """How much a drain of ``g`` for ``need`` groups idles: the expected idle group-seconds
+        until its running pods free the room (their ages against the observed run times,
+        ``lifetimes.drain_cost``), else the groups in use."""
+        if not aged:
+            return float(g.used_groups())
+        from .lifetimes import drain_cost
+        return drain_cost(pods_of(name, g.index), g.capacity, need, life)[0]
+
+    # reservations in force: a sliced GPU whose spec asks for its slices in use plus one that does
+    # not fit yet is draining for the biggest such slice, and keeps draining for a pod of that
+    # profile until one is placed (re-deciding every pass against a threshold that moves with the
+    # backlog let reservations lapse, and small pods refilled the GPU in between: the drain never
+    # ended, and the groups its pods freed idled all along)
+    held: Dict[Tuple[str, int], str] = {}
+    if params.slice_reserve_hold:
+        for name, m in original.items():
+            for og in m.gpus:
+                if getattr(og, "sliced", False) and og.target is not None and og.target_sliced:
+                    extra = [x for x, n in og.target.items() if n > og.used.get(x, 0) and is_slice_profile(x)]
+                    if extra:
+                        held[(name, og.index)] = max(extra, key=lambda x: (groups_of(x), x))
+    by_key = {(name, g.index): g for name, g in sliced}
+    name_of = {id(g): name for name, g in sliced}
+
+    def reserve(name: str, g: Any, p: str, q: int) -> None:
+        """Drain ``g`` for ``q`` slices of ``p``: its spec becomes the slices in use plus those."""
+        want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
+        want[p] = want.get(p, 0) + q
+        g.used = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
+        g.free = {}
+        g.target, g.target_sliced = want, True
+
+    def place(g: Any, p: str, q: int, age: Optional[float] = None) -> None:
+        for _ in range(q):
+            g.claim(p)
+        key = (name_of[id(g)], g.index)
+        claimed[key] = max(claimed.get(key, 0.0), float("inf") if age is None else age)
+
+    # GPUs that took a pod in this pass -> the oldest such pod's wait: a free slice the caller gave
+    # a pending pod, or a backfill below. A drain withholds the GPU and strands those pods, so only
+    # an overdue reservation of a pod older than all of them may take such a GPU
+    claimed: Dict[Tuple[str, int], float] = dict(placed_on or {})
+    # 2a. whole-GPU runs: a sliced GPU a whole-GPU pod just left (its one free slice is the whole
+    # GPU) goes to the next waiting whole-GPU pod unless the oldest waiting pod is more than
+    # ``overtake`` older. Handing it to smaller pods instead means draining it again for the next
+    # whole-GPU pod, and every such drain idles most of the GPU for a good part of a pod lifetime
+    if overtake > 0 and unserved:
+        oldest = max(age for _, age in unserved)
+        for name, g in sliced:
+            free = [(p, n) for p, n in g.free.items() if n > 0]
+            if g.target is not None or not g.is_idle() or len(free) != 1 or free[0][1] != 1 \
+                    or groups_of(free[0][0]) != g.capacity:
+                continue
+            nxt = next(((req, age) for req, age in unserved if _single(req) == (free[0][0], 1)), None)
+            if nxt is not None and nxt[1] >= oldest - overtake:
+                place(g, free[0][0], 1, nxt[1])
+                unserved.remove(nxt)
+    # 2b./3. backfill and reservation, oldest first
     reserved = False
-    claimed = set()   # GPUs that took a pod in this pass: never drained for a younger one
+    waiting: Pending = []   # pods that fit nowhere and reserved nothing, oldest first
     for req, age in list(unserved):
         s = _single(req)
         if s is None or not is_slice_profile(s[0]):
@@ -112,18 +185,21 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         cands = [(bool(g.degraded), g.room(), name, g.index, g) for name, g in sliced
                  if g.target is None and g.room() >= need]
         if cands:
-            *_, g = min(cands, key=lambda c: c[:4])
-            name = next(n for n, x in sliced if x is g)
-            for _ in range(q):
-                g.claim(p)
-            claimed.add((name, g.index))
+            place(min(cands, key=lambda c: c[:4])[-1], p, q, age)
             unserved.remove((req, age))
             continue
-        if reserved or params.slice_reserve_after <= 0 or age < reserve_after:
+        hk = next((k for k in sorted(held) if held[k] == p and claimed.get(k, -1.0) < age and by_key.get(k) is not None
+                   and by_key[k].target is None), None)
+        if hk is not None:
+            reserve(hk[0], by_key[hk], p, q)
             continue
-        victims = [(bool(g.degraded), g.used_groups(), name, g.index, g) for name, g in sliced
-                   if g.target is None and (name, g.index) not in claimed]
+        if reserved or params.slice_reserve_after <= 0 or age < reserve_after:
+            waiting.append((req, age))
+            continue
+        victims = [(bool(g.degraded), drain_key(name, g, need), name, g.index, g) for name, g in sliced
+                   if g.target is None and claimed.get((name, g.index), -1.0) < age]
         if not victims and any(g.target is None for _, g in sliced):
+            waiting.append((req, age))
             continue  # every sliced GPU just took an older pod: reconsider on the next pass
         if not victims:
             # an auto node's busy hardware GPU in another mode drains towards slices for the pod
@@ -137,13 +213,29 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
                 reserved = True
             continue
         *_, g = min(victims, key=lambda c: c[:4])
-        name = next(n for n, x in sliced if x is g)
-        want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
-        want[p] = want.get(p, 0) + q
-        g.used = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
-        g.free = {}
-        g.target, g.target_sliced = want, True
+        reserve(name_of[id(g)], g, p, q)
         reserved = True
+    # 3b. a free drain: after the backfill every pod that still waits is bigger than the unused room
+    # of every GPU not draining, so that room idles whatever the planner does; the oldest waiting
+    # pod reserves the GPU with the most of it (recomputed every pass, so it lapses as soon as a
+    # smaller pod arrives that the room fits)
+    if params.slice_free_drain:
+        draining = {max((x for x, n in g.target.items() if n > g.used.get(x, 0)), key=groups_of, default=None)
+                    for _, g in sliced if g.target is not None}
+        # with more GPUs one empties on its own sooner: the wait before a free drain scales with them
+        free_after = params.slice_free_drain_after * (median if learned else 240.0) * max(0, len(sliced) - 1)
+        for req, age in waiting:
+            p, q = _single(req)
+            if p in draining or age < free_after:
+                continue          # one GPU at a time drains for a profile: the others keep serving
+            need = q * groups_of(p)
+            idle = [(-g.room(), g.used_groups(), name, g.index, g) for name, g in sliced
+                    if g.target is None and (name, g.index) not in claimed and 0 < g.room() < need]
+            if not idle:
+                break
+            g = min(idle, key=lambda c: c[:4])[-1]
+            reserve(name_of[id(g)], g, p, q)
+            draining.add(p)
     # 4. fill
     if params.slice_fill:
         for _, g in sliced:

@@ -132,26 +132,42 @@ class SliceActuator:
             if plan.is_empty():
                 return Result()
             t0 = time.perf_counter()
-            self.store.save(plan.new)
-            ok = self._commit(len(plan.new))
-            if not ok:
-                self.store.save(current)
-            if self.device_plugin is not None:
-                self.device_plugin.restart(self.node_name)
-            REGISTRY.phase_seconds.labels(phase="agent_apply_total").observe(time.perf_counter() - t0)
-            self.shared.record_commit(ok)
-            self.shared.on_apply_done()
+            ok = False
+            try:
+                self.store.save(plan.new)
+                ok = self._commit(len(plan.new))
+            finally:
+                # whatever happened after the save (a veto, a barrier that could not be built or
+                # raised), the store, the plugin and the shared state come out consistent: the old
+                # layout back unless committed, the plugin re-read, the apply recorded
+                if not ok:
+                    self.store.save(current)
+                if self.device_plugin is not None:
+                    self.device_plugin.restart(self.node_name)
+                REGISTRY.phase_seconds.labels(phase="agent_apply_total").observe(time.perf_counter() - t0)
+                self.shared.record_commit(ok)
+                self.shared.on_apply_done()
             if not ok:
                 raise GpuError("commit barrier vetoed the slice plan")
             return Result()
 
     def _commit(self, n: int) -> bool:
+        """The node-atomic vote over the new layout (ref ``actuator.go:181-184`` rolls back a failed
+        apply): a barrier that cannot be built or fails is a veto."""
         if self.barrier_factory is None:
             return True
-        b = self.barrier_factory(max(1, n))
+        try:
+            b = self.barrier_factory(max(1, n))
+        except Exception as e:  # noqa: BLE001
+            log.error("commit barrier unavailable (%s): vetoing the slice plan", e)
+            REGISTRY.apply_errors.labels(node=self.node_name, op="barrier_unavailable").inc()
+            return False
         try:
             vote_all = getattr(b, "vote_all", None)
             return bool(vote_all([True] * n)) if vote_all is not None else bool(b.vote(True))
+        except Exception as e:  # noqa: BLE001
+            log.error("commit barrier failed (%s): vetoing the slice plan", e)
+            return False
         finally:
             b.close()
 

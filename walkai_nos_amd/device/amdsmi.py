@@ -30,14 +30,14 @@ import os
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Set
+from typing import Dict, List, Optional, Set, Tuple
 
 from ..models.errors import GpuError
 from ..models.xcp.known_configs import get_model_spec
 from ..models.xcp.profile import COMPUTE_MODES, MEMORY_MODES
 from .topology import NO_PARTITION, DeviceMap, GpuInfo, LogicalDevice, ProcInfo, build_device_map
 
-__all__ = ["AmdSmi", "FakeAmdSmi", "NativeAmdSmi", "GpuInfo", "LogicalDevice", "DeviceMap", "new_backend",
+__all__ = ["AmdSmi", "FakeAmdSmi", "NativeAmdSmi", "ProcessStats", "GpuInfo", "LogicalDevice", "DeviceMap", "new_backend",
            "COMPUTE_MODE_NAMES", "MEMORY_MODE_NAMES"]
 
 COMPUTE_MODE_NAMES = ("SPX", "DPX", "QPX", "CPX")
@@ -46,6 +46,22 @@ MEMORY_MODE_NAMES = ("NPS1", "NPS2", "NPS4", "NPS8")
 
 def _nps(mode: str) -> int:
     return MEMORY_MODES.get(mode.lower(), 1)
+
+
+@dataclass
+class ProcessStats:
+    """One process on one GPU as amd-smi reports it (``amdsmi_proc_info_t``): VRAM bytes; CU
+    occupancy — the KFD's CU-equivalents of the process's waves in flight when sampled (waves over
+    waves-per-CU), so a process confined to n CUs never reads more than n; None when the backend
+    has no such field — and the milliseconds its queues spent evicted (time-sliced out)."""
+    vram: int = 0
+    cu_occupancy: Optional[int] = None
+    evicted_ms: int = 0
+
+    def merge(self, o: "ProcessStats") -> "ProcessStats":
+        cu = None if self.cu_occupancy is None and o.cu_occupancy is None else \
+            (self.cu_occupancy or 0) + (o.cu_occupancy or 0)
+        return ProcessStats(self.vram + o.vram, cu, self.evicted_ms + o.evicted_ms)
 
 
 class AmdSmi:
@@ -85,6 +101,10 @@ class AmdSmi:
 
     def _process_memory(self, proc: ProcInfo) -> Dict[int, int]:
         raise NotImplementedError
+
+    def _process_info(self, proc: ProcInfo) -> Dict[int, ProcessStats]:
+        """pid -> stats; backends without CU occupancy report VRAM only (``cu_occupancy`` None)."""
+        return {pid: ProcessStats(b) for pid, b in self._process_memory(proc).items()}
 
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         raise NotImplementedError
@@ -197,6 +217,16 @@ class AmdSmi:
                 out[pid] = out.get(pid, 0) + b
         return out
 
+    def process_info(self, index: int) -> Dict[int, ProcessStats]:
+        """pid -> :class:`ProcessStats` (VRAM bytes, CU occupancy, queue-eviction ms) of every process
+        holding a context on physical GPU ``index``, summed over its logical devices (the input of
+        the slice guards, ``controllers/hbmguard.py``)."""
+        out: Dict[int, ProcessStats] = {}
+        for p in self._members(index):
+            for pid, st in self._process_info(p).items():
+                out[pid] = out[pid].merge(st) if pid in out else st
+        return out
+
     def activity(self, index: int) -> Dict[str, float]:
         acts = [self._activity(p) for p in self._members(index)]
         return {k: sum(a[k] for a in acts) / len(acts) for k in ("gfx", "umc", "mm")}
@@ -224,6 +254,7 @@ class _FakeGpu:
     memory: str = "NPS1"
     processes: Dict[int, int] = field(default_factory=dict)  # partition -> process count
     vram: Dict[int, Dict[int, int]] = field(default_factory=dict)  # partition -> {pid: VRAM bytes}
+    cu: Dict[int, Tuple[int, int]] = field(default_factory=dict)     # pid -> (CU occupancy, evicted ms)
 
 
 class FakeAmdSmi(AmdSmi):
@@ -346,6 +377,14 @@ class FakeAmdSmi(AmdSmi):
         g = self._gpu_of(proc)
         return dict(g.vram.get(proc.partition_id if proc.partition_id != NO_PARTITION else 0, {}))
 
+    def _process_info(self, proc: ProcInfo) -> Dict[int, ProcessStats]:
+        g = self._gpu_of(proc)
+        out = {}
+        for pid, b in self._process_memory(proc).items():
+            cu, ev = g.cu.get(pid, (0, 0))
+            out[pid] = ProcessStats(b, cu, ev)
+        return out
+
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:
         return {"gfx": 100.0 if self._process_count(proc) else 0.0, "umc": 0.0, "mm": 0.0}
 
@@ -376,6 +415,12 @@ class FakeAmdSmi(AmdSmi):
                 per[pid] = nbytes
             else:
                 per.pop(pid, None)
+
+    def set_process_cus(self, index: int, pid: int, cu_occupancy: int, evicted_ms: int = 0) -> None:
+        """Pretend process ``pid`` on GPU ``index`` has ``cu_occupancy`` CUs' worth of waves in
+        flight and ``evicted_ms`` of queue eviction (it must hold VRAM to be listed)."""
+        with self._lock:
+            self._gpu(index).cu[pid] = (cu_occupancy, evicted_ms)
 
     def attach(self, device_id: str, n: int = 1) -> None:
         """Pretend ``n`` more processes opened the partition behind ``device_id``."""
@@ -428,6 +473,11 @@ class NativeAmdSmi(AmdSmi):
         L.nos_smi_process_count.argtypes = [ctypes.c_uint32]
         L.nos_smi_process_memory.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                              ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]
+        self._has_info = hasattr(L, "nos_smi_process_info")
+        if self._has_info:
+            L.nos_smi_process_info.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32),
+                                               ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
         L.nos_smi_activity.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 3
         L.nos_smi_vram.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.nos_smi_power_clock.argtypes = [ctypes.c_uint32] + [ctypes.POINTER(ctypes.c_uint32)] * 4
@@ -497,6 +547,21 @@ class NativeAmdSmi(AmdSmi):
                 raise GpuError(f"process list: {self._err()}")
             if n <= cap:
                 return {int(pids[i]): int(vram[i]) for i in range(n)}
+            cap = n + 16
+
+    def _process_info(self, proc: ProcInfo) -> Dict[int, ProcessStats]:
+        if not self._has_info:
+            return super()._process_info(proc)
+        cap = 64
+        while True:
+            pids, vram = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+            cu, ev = (ctypes.c_uint32 * cap)(), (ctypes.c_uint32 * cap)()
+            with self._lock:
+                n = self._lib.nos_smi_process_info(proc.ordinal, pids, vram, cu, ev, cap)
+            if n < 0:
+                raise GpuError(f"process list: {self._err()}")
+            if n <= cap:
+                return {int(pids[i]): ProcessStats(int(vram[i]), int(cu[i]), int(ev[i])) for i in range(n)}
             cap = n + 16
 
     def _activity(self, proc: ProcInfo) -> Dict[str, float]:

@@ -254,10 +254,14 @@ class PartitionDevicePlugin(PluginServer):
     """One ``amd.com/<mode>_<nps>`` resource of the node's compute partitions."""
 
     def __init__(self, resource_name: str, state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
-                 poll_interval: float = 1.0, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so", cu_count: int = 256):
+                 poll_interval: float = 1.0, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so", cu_count: int = 256,
+                 shim_present: Optional[Callable[[], bool]] = None):
         super().__init__(resource_name, socket_dir, poll_interval, prefix="nos-xcp-")
         self.state = state
         self.shim_path = shim_path
+        #: whether the shim exists on the host (None: assume it does); the agent mounts the host's
+        #: shim directory at the same path, so it checks its own view
+        self.shim_present = shim_present
         self.cu_count = cu_count
 
     def _devices(self) -> List[PartitionDevice]:
@@ -313,9 +317,15 @@ class PartitionDevicePlugin(PluginServer):
                 car.envs[constant.ENV_HSA_CU_MASK] = hsa_cu_mask(cus, 0)
             if cus:
                 car.envs[constant.ENV_HBM_LIMIT] = str(hbm)
-                car.envs["LD_PRELOAD"] = self.shim_path
                 car.envs["NOS_SLICE_IDS"] = ",".join(cr.devicesIDs)
-                car.mounts.add(container_path=self.shim_path, host_path=self.shim_path, read_only=True)
+                if self.shim_present is None or self.shim_present():
+                    car.envs["LD_PRELOAD"] = self.shim_path
+                    car.mounts.add(container_path=self.shim_path, host_path=self.shim_path, read_only=True)
+                else:
+                    # a bind mount of a missing host file fails the container's creation: start the
+                    # pod without the in-process limiter (the HBM guard still polices its budget)
+                    log.warning("HBM-limit shim %s is missing on this node: slices %s start without it",
+                                self.shim_path, list(cr.devicesIDs))
             car.devices.add(container_path="/dev/kfd", host_path="/dev/kfd", permissions="rw")
             for n in sorted(set(nodes)):
                 car.devices.add(container_path=n, host_path=n, permissions="rw")
@@ -324,12 +334,13 @@ class PartitionDevicePlugin(PluginServer):
 
 def partition_plugin_manager(state: PartitionState, socket_dir: str = DEVICE_PLUGIN_DIR,
                              kubelet_socket: str = KUBELET_SOCKET, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so",
-                             **kw: Any) -> PluginManager:
+                             shim_present: Optional[Callable[[], bool]] = None, **kw: Any) -> PluginManager:
     """A :class:`PluginManager` over the partition view: one plugin per resource name present (a
     flip to a mode never served before registers its resource on the next sync)."""
     return PluginManager(None, socket_dir=socket_dir, kubelet_socket=kubelet_socket,
                          resources=lambda: sorted(state.view()),
-                         factory=lambda r: PartitionDevicePlugin(r, state, socket_dir, shim_path=shim_path), **kw)
+                         factory=lambda r: PartitionDevicePlugin(r, state, socket_dir, shim_path=shim_path,
+                                                                 shim_present=shim_present), **kw)
 
 
 class AllocatablePublisher:

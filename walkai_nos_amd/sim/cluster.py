@@ -448,7 +448,9 @@ class SimCluster:
             self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Failed", "reason": "UnexpectedAdmissionError",
                                                             "message": str(e)}}, ko.namespace(pod))
             return
-        self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Running"}}, ko.namespace(pod))
+        self.api.patch("Pod", ko.name(pod), {"status": {"phase": "Running",
+                                                        "startTime": ko.now_rfc3339(self.clock())}},
+                       ko.namespace(pod))
         self.binds.append((self.clock(), ko.key(pod)[1], node))
 
     # -- workload -----------------------------------------------------------------------
