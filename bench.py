@@ -37,6 +37,9 @@ def main() -> int:
     ap.add_argument("--flip-cost", type=float, default=-1.0,
                     help="cluster seconds a GPU serves nothing per compute-partition flip "
                          "(default: the measured components, bench_core.FLIP_COST_COMPONENTS)")
+    ap.add_argument("--pod-start", type=float, default=-1.0,
+                    help="cluster seconds a newly bound pod holds its slice before its first inference "
+                         "(default: measured on this box before the window, bench_core.measure_pod_start)")
     ap.add_argument("--device-plugin", default="nos", choices=("nos", "amd"),
                     help="nos: drains enforced by the partition plugin's device health; amd: no enforcement")
     ap.add_argument("--policy", default="pack", choices=("pack", "fifo", "batch", "simulate"))
@@ -56,6 +59,9 @@ def main() -> int:
     ap.add_argument("--erq", action="store_true",
                     help="Elastic Resource Quota mode (BASELINE config 5): two quota'd namespaces borrow and "
                          "reclaim on the real data plane; prints its own JSON line (walkai_nos_amd/bench_erq.py)")
+    ap.add_argument("--no-data-plane", action="store_true",
+                    help="REHEARSAL of the launch path without a GPU (gloo, control plane only; inferences "
+                         "priced with the measured mode rates, marked in the output — never a measurement)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -64,7 +70,8 @@ def main() -> int:
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        if not args.no_data_plane:
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
         # RCCL between the GPU ranks; NOS_BENCH_DIST_BACKEND=gloo rehearses the multi-rank path with
         # several ranks sharing fewer GPUs (RCCL refuses two ranks on one device)
         dist.init_process_group(os.environ.get("NOS_BENCH_DIST_BACKEND", "nccl"),
@@ -82,7 +89,8 @@ def main() -> int:
                       preroll=args.preroll, quantum_s=args.quantum, cluster_s=args.cluster_s,
                       flip_cost_s=args.flip_cost, policy=args.policy, depth=args.depth,
                       density=not args.no_density, pod_streams=args.pod_streams, lane_cus=args.lane_cus,
-                      device_plugin=args.device_plugin, layout=args.layout)
+                      device_plugin=args.device_plugin, layout=args.layout, pod_start_s=args.pod_start,
+                      data_plane=not args.no_data_plane)
     if args.emulation:
         cfg.emulation = args.emulation
     if args.erq:

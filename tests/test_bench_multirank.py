@@ -104,3 +104,36 @@ def test_density_per_pod_spread():
     assert r == {"min": 5.0, "max": 10.0, "max_over_min": 2.0}
     assert _per_pod_spread({}, ["a"], 1.0)["max_over_min"] is None   # a pod that served nothing
     assert _per_pod_spread({}, [], 1.0) == {}
+
+
+def test_bench_py_eight_rank_rehearsal_prints_one_json_line():
+    """``bench.py --gpus 8`` launched the way the driver launches it
+    (torch.distributed.run, 8 ranks, 127.0.0.1) on gloo without a GPU: the ranks stay in lock-step
+    through the window and the post-window model, rank 0 prints exactly one JSON line, within the
+    time an 8-GPU driver run allows. Inferences are priced (the output says REHEARSAL)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, NOS_BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("LD_PRELOAD", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+                        "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py", "--gpus", "8",
+                        "--steps", "20", "--warmup", "5", "--no-data-plane", "--no-density"],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=900)
+    wall = time.time() - t0
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8 and out["steps"] == 20 and out["warmup"] == 5
+    assert out["data"].startswith("REHEARSAL") and out["value"] > 0
+    assert out["gpu_utilization_pct"] > 50 and out["config"]["parallelism"].endswith("8 GPU node")
+    assert wall < 600, wall

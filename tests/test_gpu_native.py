@@ -469,19 +469,33 @@ def test_cu_guard_flags_only_the_process_outside_its_cu_mask(gpu):
     base = {k: v for k, v in os.environ.items() if k not in ("HSA_CU_MASK", "LD_PRELOAD")}
     envs = [dict(base, HSA_CU_MASK=hsa_cu_mask(slices[0].cus), NOS_SLICE_IDS="gpu0::s0"),
             dict(base, NOS_SLICE_IDS="gpu0::s1")]                   # s1's pod dropped its mask
-    procs = [subprocess.Popen([sys.executable, "-u", "-c", CU_HOG_CHILD % {"root": ROOT, "seconds": 8.0}],
-                              env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for e in envs]
-    samples, found = [], []
+    smi = NativeAmdSmi()
+    # amd-smi reports the KFD's (host) pids; this box runs the test in its own PID namespace (the
+    # agents run with hostPID), so each child's host pid is learned as the one that appears when it
+    # starts, children started one at a time
+    host_to_local = {}
+    procs, samples, found = [], [], []
     try:
-        for p in procs:
+        for e in envs:
+            before = set(smi.process_info(0))
+            p = subprocess.Popen([sys.executable, "-u", "-c", CU_HOG_CHILD % {"root": ROOT, "seconds": 20.0}],
+                                 env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+            procs.append(p)
             assert p.stdout.readline().strip() == "READY", p.stderr.read()[-2000:]
-        smi = NativeAmdSmi()
+            new, t_seen = set(), time.time()
+            while not new and time.time() - t_seen < 8.0:   # the KFD's list can lag a process's start
+                new = set(smi.process_info(0)) - before - set(host_to_local)
+                time.sleep(0.1)
+            assert len(new) == 1, new
+            host_to_local[new.pop()] = p.pid
         g = HbmGuard(smi, lambda: {0: slices}, "box", action="off", cu_action="report", cu_strikes=3,
-                     cu_probe_checks=8)
+                     cu_probe_checks=8, pid_map=lambda pid: host_to_local.get(pid, pid))
         t0 = time.time()
         while time.time() - t0 < 5.0:
             found += g.check()
-            samples.append({"t": round(time.time() - t0, 2), "state": g.cu_state.get(0),
+            raw = {pid: [st.cu_occupancy, st.evicted_ms, st.vram] for pid, st in smi.process_info(0).items()}
+            samples.append({"t": round(time.time() - t0, 2), "state": g.cu_state.get(0), "raw": raw,
+                            "children": [p.pid for p in procs],
                             "accounts": {",".join(a.slice_ids): {"cu_used": a.cu_used, "cu_budget": a.cu_budget,
                                                                  "evicted_ms": a.evicted_ms, "pids": a.pids}
                                          for a in g.last}})

@@ -116,6 +116,14 @@ def working_cus(cus: Optional[List[int]], pin: int, total_cus: int = 256) -> int
 FLIP_COST_COMPONENTS = {"commit_barrier_s": 0.33, "probe_s": 0.39, "plugin_push_s": 0.05, "amdsmi_switch_s": 10.0}
 FLIP_COST_MEASURED = ("commit_barrier_s", "probe_s", "plugin_push_s")
 
+#: A new pod's start-up: from its process starting (kubelet has admitted it and holds its slice) to
+#: its first inference — interpreter + torch import, model load, warm-up and HIP-graph capture of the
+#: reference demo's client (``dataplane/client.py``), spawned with ``Allocate``'s environment. The
+#: slice is allocated but serves nothing meanwhile, so every pod bound in the window is charged this
+#: much cluster time at its start (``bench.py`` measures it on the box before the window,
+#: :func:`measure_pod_start`; this is the fallback).
+POD_START_S = 8.0
+
 
 def default_flip_cost(commit_barrier_s: Optional[float] = None) -> float:
     """The flip outage from its components, with this run's measured commit barrier if given."""
@@ -154,13 +162,25 @@ class BenchConfig:
     pack: Optional[Dict[str, float]] = None  # PackParams overrides (field name -> value)
     arrivals: str = "steady"             # steady (constant rate, seeded phase) | poisson
     layout: str = "partitions"           # node label nos.nebuly.com/xcp-layout: partitions | slices | auto
+    data_plane: bool = True              # False: a rehearsal of the launch path without a GPU (inferences
+                                         # priced with MODE_RATES, never a measurement)
     commit_barrier_s: float = -1.0       # this run's measured node commit barrier (<0: the component constant)
+    pod_start_s: float = -1.0            # cluster seconds a newly bound pod holds its slice before it serves
+                                         # (<0: POD_START_S; bench.py measures it on the box before the window)
 
     def __post_init__(self) -> None:
         #: the flip cost is the components' sum (so a measured commit barrier replaces its constant)
         self.flip_cost_default = self.flip_cost_s < 0
         if self.flip_cost_s < 0:
             self.flip_cost_s = default_flip_cost(self.commit_barrier_s)
+        self.pod_start_default = self.pod_start_s < 0
+        if self.pod_start_s < 0:
+            self.pod_start_s = POD_START_S
+
+    @property
+    def pod_start_quanta(self) -> float:
+        """A new pod's start-up (process start to first inference) in quanta."""
+        return self.pod_start_s / self.cluster_s
 
     @property
     def flip_quanta(self) -> float:
@@ -443,8 +463,9 @@ class DataPlane:
         for s in self.slots.values():
             s.drain()
 
-    def serve(self, keys: List[Any], deadline: float) -> Dict[Any, int]:
+    def serve(self, keys: List[Any], deadline: float, start_at: Optional[Dict[Any, float]] = None) -> Dict[Any, int]:
         """Keep every listed slot busy until ``deadline``; returns the inferences enqueued per slot.
+        ``start_at``: key -> wall time its pod starts serving (a pod still starting up).
 
         A different set of compute modes than in the last quantum means the GPU was re-partitioned:
         every queued inference of the old layout finishes first (the agent only flips an idle GPU),
@@ -460,7 +481,7 @@ class DataPlane:
             self._layout = layout
         active = [(k, self.slots[remap[k][0]] if k in remap else self.slots[k]) for k in keys]
         if self.cfg.depth <= 1 and active:
-            return self._serve_loops(active, deadline, {k: v[1] for k, v in remap.items()})
+            return self._serve_loops(active, deadline, {k: v[1] for k, v in remap.items()}, start_at)
         n: Dict[Any, int] = {k: 0 for k in keys}
         while True:
             now = time.perf_counter()
@@ -507,7 +528,8 @@ class DataPlane:
         return out
 
     def _serve_loops(self, active: List[Tuple[Any, "Slot"]], deadline: float,
-                     streams: Optional[Dict[Any, Any]] = None) -> Dict[Any, int]:
+                     streams: Optional[Dict[Any, Any]] = None,
+                     start_at: Optional[Dict[Any, float]] = None) -> Dict[Any, int]:
         """The reference demo's loop (``client/main.py:23-25``), one per pod lane, each on its own
         thread: start one inference, wait for it (a blocking event wait, the GIL released), record
         its GPU time, start the next — until ``deadline``. A polling loop over every pod would leave
@@ -523,6 +545,9 @@ class DataPlane:
             K.set_slice_pin(slot.pin)
             done = 0
             stream = (streams or {}).get(key) or lane.stream
+            wait = (start_at or {}).get(key, 0.0) - time.perf_counter()
+            if wait > 0:
+                time.sleep(min(wait, max(0.0, deadline - time.perf_counter())))
             with torch.no_grad(), torch.cuda.stream(stream):
                 while time.perf_counter() < deadline:
                     st = torch.cuda.Event(enable_timing=True)
@@ -640,6 +665,7 @@ class NodeBench:
         self.created: Dict[str, float] = {}           # pod -> cluster time it was created
         self.bound_at: Dict[str, float] = {}          # pod -> cluster time it was bound
         self.outage: Dict[Tuple[str, int], float] = {}  # (node, GPU) -> quanta of outage left
+        self.starting: Dict[str, float] = {}          # pod -> quanta of start-up left (serves nothing)
         self._flips_seen = {n: len(sn.smi.set_calls) for n, sn in self.cluster.nodes.items()}
         self._binds_seen = 0
         self.reset_stats()
@@ -660,6 +686,7 @@ class NodeBench:
         self.profile_pods: Dict[str, set] = collections.defaultdict(set)        # pods that served in the window
         self.tts: Dict[str, List[float]] = collections.defaultdict(list)        # bound in the window: wait (s)
         self.dark_wall_s = 0.0
+        self.start_gpu_quanta = 0.0      # allocated GPU-quanta spent in pods' start-up
         self.idle_acct: Dict[str, float] = collections.defaultdict(float)  # cause -> GPU-quanta
         self.offered_gpu_quanta = 0.0    # GPU-quanta of work that arrived (expected lifetime x size)
 
@@ -710,6 +737,8 @@ class NodeBench:
             self._flips_seen[nname] = len(calls)
         for t, name, _ in c.binds[self._binds_seen:]:
             self.bound_at[name] = t
+            if self.cfg.pod_start_quanta > 0:
+                self.starting[name] = self.cfg.pod_start_quanta
             if name in self.created:
                 self.tts[self.profile_of.get(name, "?")].append(t - self.created[name])
         self._binds_seen = len(c.binds)
@@ -777,14 +806,28 @@ class NodeBench:
                 "by_cause_gpu_quanta": {k: round(self.idle_acct.get(k, 0.0), 3) for k in IDLE_CAUSES},
                 "by_cause_pct": {k: round(100.0 * self.idle_acct.get(k, 0.0) / total, 2) for k in IDLE_CAUSES}}
 
+    def start_dark(self, name: str) -> float:
+        """Fraction of this quantum pod ``name`` spends starting up (allocated, not serving)."""
+        return min(1.0, max(0.0, self.starting.get(name, 0.0)))
+
     def end_step(self) -> None:
-        """Age every running pod by the part of the quantum its GPU was lit, then let outages run."""
+        """Age every running pod by the part of the quantum it served (its GPU lit and its start-up
+        over), then let outages and start-ups run."""
         gpus_of = self.pod_gpus()
         for name in list(self.live):
             lit = min((1.0 - self.dark(g, n) for (n, g) in gpus_of.get(name, ())), default=1.0)
+            sd = self.start_dark(name)
+            if sd > 0 and lit > 0:
+                prof = self.profile_of.get(name, "")
+                self.start_gpu_quanta += min(sd, lit) / COMPUTE_MODES.get(prof.split("_")[0], 1)
+            lit = max(0.0, lit - sd)
             if lit > 0:
                 self.profile_pods[self.profile_of.get(name, "?")].add(name)
             self.live[name] -= lit
+        for name in list(self.starting):
+            self.starting[name] -= 1.0
+            if self.starting[name] <= 1e-9 or name not in self.live:
+                del self.starting[name]
         for g in list(self.outage):
             self.outage[g] -= 1.0
             if self.outage[g] <= 1e-9:
@@ -800,7 +843,8 @@ class NodeBench:
         t0 = time.perf_counter()
         deadline = deadline if deadline is not None else t0 + self.cfg.quantum_s
         self.control_step()
-        keys = self.my_pods()
+        by_pod = pod_keys(self.sn, self.cfg.rank)
+        keys = list(by_pod.values())
         dark = self.dark(self.cfg.rank)
         if not keys:
             self.empty_steps += 1
@@ -814,7 +858,19 @@ class NodeBench:
                 if wait > 0:
                     time.sleep(wait)
                     self.dark_wall_s += wait
-            n = self.data.serve(keys if dark < 1.0 else [], deadline)
+            # a pod still starting up holds its slice and serves from the end of its start-up on
+            start_at = {key: lit_from + self.start_dark(name) * self.cfg.quantum_s
+                        for (_, name), key in by_pod.items() if self.start_dark(name) > 0}
+            n = self.data.serve(keys if dark < 1.0 else [], deadline, start_at)
+        elif self.cfg.world > 1 or not self.cfg.data_plane:
+            # a rehearsal without a GPU: this rank's pods priced with the measured mode rates
+            for (_, name), key in by_pod.items():
+                lit = max(0.0, 1.0 - dark - self.start_dark(name))
+                m = str(key[1] if key[0] == "slice" else key[0]).split("_")[0]
+                n[key] = int(MODE_RATES[m] / COMPUTE_MODES[m] * self.cfg.quantum_s * lit)
+            wait = deadline - time.perf_counter()
+            if wait > 0:
+                time.sleep(wait)
         self.host_s["serve"] += time.perf_counter() - t1
         total = sum(n.values())
         self.inferences += total
@@ -1021,7 +1077,20 @@ def flip_sensitivity(cfg: BenchConfig, costs=(2.0, 5.0, 10.0, 30.0), steps: Opti
     return out
 
 
-def seed_model(cfg: BenchConfig, seeds=(1, 2, 3, 4, 5)) -> Dict[str, Any]:
+def pod_start_sensitivity(cfg: BenchConfig, factors=(0.0, 1.0, 2.0, 4.0)) -> Dict[str, Any]:
+    """The control plane alone over the same seeded window with pods' start-up at these multiples
+    of the charged one (what start-up costs in allocation and modelled inferences; replaces the
+    flip-cost sensitivity on layouts that never flip)."""
+    import dataclasses
+    out: Dict[str, Any] = {}
+    for f in factors:
+        c = dataclasses.replace(cfg, pod_start_s=f * cfg.pod_start_s, rank=0, world=1)
+        r = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
+        out[f"{round(f * cfg.pod_start_s, 1):g}s"] = {k: r[k] for k in ("util_pct", "inf_per_s_model")}
+    return out
+
+
+def seed_model(cfg: BenchConfig, seeds=tuple(range(1, 11))) -> Dict[str, Any]:
     """The control plane alone over the same window for other churn seeds (no GPU): how much the
     default seed's window is representative. ``inf_per_s_model`` prices served partition-time with
     :data:`MODE_RATES`; ``cpx_served_windows``: windows in which some 1/8-GPU pod was served."""
@@ -1034,10 +1103,13 @@ def seed_model(cfg: BenchConfig, seeds=(1, 2, 3, 4, 5)) -> Dict[str, Any]:
                          "pending_mean": r["pending_mean"],
                          "served": {p: v["inferences"] > 0 for p, v in r["per_profile"].items()}}
     v = [x["inf_per_s_model"] for x in rows.values()]
+    u = sorted(x["util_pct"] for x in rows.values())
     c = dataclasses.replace(cfg, rank=0, world=1)
-    own = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)["inf_per_s_model"]
+    own = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
     return {"seeds": list(seeds), "mean": round(sum(v) / len(v), 1), "min": min(v), "max": max(v),
-            "this_seed_model": own, "cpx_served_windows": sum(1 for x in rows.values() if x["served"]["cpx_nps1"]),
+            "util_pct_mean": round(sum(u) / len(u), 2), "util_pct_min": u[0],
+            "this_seed_model": own["inf_per_s_model"], "this_seed_util_pct": own["util_pct"],
+            "cpx_served_windows": sum(1 for x in rows.values() if x["served"]["cpx_nps1"]),
             "per_seed": rows}
 
 
@@ -1068,7 +1140,8 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     from .parallel.barrier import LocalBarrier, RankCommitBarrier
 
     distributed = cfg.world > 1
-    if cfg.flip_cost_default:
+    gpu = cfg.data_plane
+    if cfg.flip_cost_default and gpu:
         # charge flips this run's own commit barrier (the node's devices, spawned as the agent does)
         measured = measure_commit_barrier() if cfg.rank == 0 else None
         if distributed:
@@ -1079,43 +1152,59 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         if measured is not None:
             cfg.commit_barrier_s = measured
             cfg.flip_cost_s = default_flip_cost(measured)
+    pod_start = None
+    if cfg.pod_start_default and gpu:
+        # charge pods this box's own start-up (one pod process spawned as kubelet would, rank 0)
+        pod_start = measure_pod_start() if cfg.rank == 0 else None
+        ps = pod_start["pod_start_s"] if pod_start else -1.0
+        if distributed:
+            t = torch.tensor([ps], dtype=torch.float64,
+                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, 0)
+            ps = float(t.item())
+        if ps > 0:
+            cfg.pod_start_s = ps
     if distributed:
         # the agent's commit path (Actuator._commit -> barrier.vote_all(per-device votes)); each
         # rank contributes the votes of its own GPU's partitions, all-reduced over RCCL
         bf = lambda n: RankCommitBarrier(rank=cfg.rank, world=cfg.world)  # noqa: E731
     else:
         bf = lambda n: LocalBarrier(n)  # noqa: E731
-    nb = NodeBench(cfg, barrier_factory=bf)
+    nb = NodeBench(cfg, barrier_factory=bf, gpu_data_plane=gpu)
+
+    def sync() -> None:
+        if nb.data is not None:
+            nb.data.drain_all()
+            torch.cuda.synchronize()
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
     for _ in range(cfg.warmup):
         nb.step()
-    nb.data.drain_all()
-    torch.cuda.synchronize()
+    sync()
     if distributed:
         dist.barrier()
     nb.reset_stats()
-    for s in nb.data.slots.values():
+    for s in (nb.data.slots.values() if nb.data is not None else ()):
         s.latency_ms.clear()
-    busy = HwBusySampler(nb.data.device)
-    busy.start()
+    busy = HwBusySampler(nb.data.device) if nb.data is not None else None
+    if busy is not None:
+        busy.start()
     t0 = time.perf_counter()
     deadline = t0
     for _ in range(cfg.steps):
         deadline += cfg.quantum_s
         nb.step(deadline)
-    nb.data.drain_all()
-    torch.cuda.synchronize()
+    sync()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    hw_busy = busy.stop()
-    on_gpu = dist.get_backend() == "nccl" if distributed else True
+    hw_busy = busy.stop() if busy is not None else None
+    on_gpu = (dist.get_backend() == "nccl" if distributed else True) and gpu
     profs = [p for p, _ in MIX]
     stats = torch.tensor([elapsed, float(nb.inferences), hw_busy if hw_busy is not None else -1.0]
                          + [float(nb.profile_inferences.get(p, 0)) for p in profs],
-                         dtype=torch.float64, device=f"cuda:{nb.data.device}" if on_gpu else "cpu")
+                         dtype=torch.float64, device=f"cuda:{nb.data.device}" if on_gpu and nb.data else "cpu")
     if distributed:
         t = stats[:1].clone()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -1129,7 +1218,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         total_inf = float(nb.inferences)
     latency = inference_latency(nb.data)
     per_profile = nb.profile_report(elapsed)
-    barrier_8dev = node_barrier_probe(cfg) if cfg.rank == 0 else None
+    barrier_8dev = node_barrier_probe(cfg) if cfg.rank == 0 and gpu else None
     density = density_phase(cfg, nb.data) if cfg.density else {}
     nb.close()
     value = total_inf / elapsed
@@ -1139,8 +1228,13 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     from .models.workload.yolos import YolosSmall
     from .ops import kernels as K
     flops = YolosSmall().flops_per_inference(cfg.hw)
-    sens = flip_sensitivity(cfg) if cfg.rank == 0 else {}
-    seeds = seed_model(cfg) if cfg.rank == 0 else {}
+    # a layout that flips is priced by its flips; sliced GPUs never flip, so their sensitivity is to
+    # the pods' start-up instead
+    sens = (flip_sensitivity(cfg) if cfg.layout == "partitions" else pod_start_sensitivity(cfg)) \
+        if cfg.rank == 0 else {}
+    # the window is one draw of the churn: its spread over other seeds (fewer on big nodes, whose
+    # control plane takes longer per quantum)
+    seeds = seed_model(cfg, tuple(range(1, 11 if cfg.gpus <= 2 else 6))) if cfg.rank == 0 else {}
     sustainable = sustainable_load_row(cfg) if cfg.rank == 0 else {}
     life_s = cfg.mean_lifetime_quanta * cfg.cluster_s
     return {
@@ -1158,13 +1252,14 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "numerics": ("fp32-accurate: every fp32 product as 6 bf16 MFMAs over an exact 3-term bf16 split "
                      "of both operands (dropped terms 2^-24 relative; tests/test_gpu_kernels.py checks the "
                      "error vs fp64 against the f32-input MFMA path)") if cfg.backend == "hip" else "fp32",
-        "data": "synthetic (seeded pod churn; random-init YOLOS-small weights; synthetic 800x1066 images)",
+        "data": "synthetic (seeded pod churn; random-init YOLOS-small weights; synthetic 800x1066 images)" if gpu
+        else "REHEARSAL without a GPU: control plane only, inferences priced with MODE_RATES (not a measurement)",
         "gpu_utilization_pct": round(util, 2),
         "allocation_pct_incl_outage": round(raw, 2),
         "hw_busy_pct": hw_busy,
         "hw_busy_source": "amd-smi gfx_activity, sampled every 100 ms in the timed window" if hw_busy is not None
-        else f"unavailable: {busy.error}",
-        "hw_power_clock": busy.power_summary(),
+        else f"unavailable: {busy.error if busy is not None else 'no GPU (rehearsal)'}",
+        "hw_power_clock": busy.power_summary() if busy is not None else {},
         "pods_per_node": round(pods, 2),
         "pods_per_gpu": round(pods / cfg.gpus, 2),
         "per_profile": per_profile,
@@ -1180,7 +1275,15 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "flips": nb.flips,
         "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
         "dark_wall_s": round(nb.dark_wall_s, 3),
-        "flip_cost_sensitivity": sens,
+        "flip_cost_sensitivity" if cfg.layout == "partitions" else "pod_start_sensitivity": sens,
+        "pod_start": {"s": round(cfg.pod_start_s, 2),
+                      "source": ("measured in this run before the window (one pod process with Allocate's "
+                                 "environment, spawn to first inference)") if pod_start else
+                      ("POD_START_S constant" if cfg.pod_start_default else "--pod-start"),
+                      "measurement": pod_start,
+                      "pct_of_gpu_time": round(100.0 * nb.start_gpu_quanta / max(1, nb.gpu_quanta), 2)},
+        "serving_pct": round(util - 100.0 * nb.start_gpu_quanta / max(1, nb.gpu_quanta), 2),
+        "idle": nb.idle_report(),
         "seed_model": seeds,
         "load_0.85": sustainable,
         "commit_barrier_node": barrier_8dev,
@@ -1220,6 +1323,42 @@ def measure_commit_barrier() -> Optional[float]:
             return None
         return round(float(b.last["wall_ms"]) / 1000.0, 3)
     except Exception:  # noqa: BLE001 - the component constant is charged instead
+        return None
+
+
+def measure_pod_start(timeout: float = 180.0) -> Optional[Dict[str, Any]]:
+    """Seconds from a pod's process starting to its first inference, on this box: the reference
+    demo's client (``dataplane/client.py``: torch import, YOLOS-small load, warm-up, HIP-graph
+    capture) spawned with the environment ``Allocate`` gives a 1/8-GPU slice (CU mask, HBM budget,
+    shim), timed from ``Popen`` to its first inference. None when it cannot run."""
+    import subprocess
+    import sys
+    try:
+        from .dataplane.procs import ROOT, allocate_envs
+        env = dict(os.environ)
+        env.update(allocate_envs(["32cu.36gb"])[0])
+        env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        t0 = time.perf_counter()
+        p = subprocess.Popen([sys.executable, "-u", "-m", "walkai_nos_amd.dataplane.client", "--seconds", "0.3"],
+                             cwd=ROOT, env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                             stderr=subprocess.DEVNULL, text=True)
+        try:
+            ln = p.stdout.readline()
+            ready = time.perf_counter() - t0
+            if ln.strip() != "READY":
+                return None
+            p.stdin.write(f"GO {time.time():.6f}\n")
+            p.stdin.flush()
+            out, _ = p.communicate(timeout=timeout)
+        finally:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        res = json.loads(next(x for x in reversed(out.splitlines()) if x.startswith("{")))
+        first = (res.get("latency_ms") or {}).get("max", 0.0) / 1000.0
+        return {"pod_start_s": round(ready + first, 2), "to_ready_s": round(ready, 2),
+                "in_process_boot_s": res.get("boot_s"), "slice": "32cu.36gb (1/8 GPU)"}
+    except Exception:  # noqa: BLE001 - the constant is charged instead
         return None
 
 
@@ -1272,8 +1411,8 @@ def control_only(cfg: BenchConfig, steps: int, skip: int = 0) -> Dict[str, Any]:
             served = 0.0
         nb.control_step()
         for g in range(cfg.gpus):
-            lit = 1.0 - nb.dark(g)
-            for devs in nb.sn.kubelet.allocations.values():
+            for (_, pod), devs in nb.sn.kubelet.allocations.items():
+                lit = max(0.0, 1.0 - nb.dark(g) - nb.start_dark(pod))
                 for r, d in devs:
                     p = extract_profile_name(r)
                     if p is not None and nb.sn.smi.resolve(d).gpu_index == g:
