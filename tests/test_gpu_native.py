@@ -317,16 +317,28 @@ def test_two_concurrent_slice_processes_have_disjoint_census(gpu):
     assert all(p["hbm"]["loaded"] and p["hbm"]["peak_bytes"] <= p["hbm"]["limit_bytes"] for p in r["per_pod"]), r
 
 
-@pytest.mark.parametrize("pods", [3, 4])
+@pytest.mark.parametrize("pods", [3, 4, 5, 6, 7, 8])
 def test_memory_only_slice_processes_share_compute_evenly(gpu, pods):
-    """VERDICT r3 #2 (ref getting-started-mps.md:22, "computing resources are equally shared"):
-    memory-only pods as concurrent processes, each with the env Allocate() gives a memory-only
-    slice (GPU_MAX_HW_QUEUES by the auto rule among it): no pod serves more than 1.3x another."""
+    """VERDICT r3 #2 / r4 #5 (ref getting-started-mps.md:22, "computing resources are equally
+    shared"): memory-only pods as concurrent processes started one after another, each with the env
+    Allocate() gives a memory-only slice (GPU_MAX_HW_QUEUES by the auto rule). Every count the
+    planner leaves on a GPU shares within 1.25x. The counts it skips (SKIP_SHARED_COUNTS: 5, 7) are
+    measured too and must show the cause the skip is built on: two rate classes by start parity
+    (pods 0, 2, 4, ... on one pipe, 1, 3, ... on another), each class even within itself."""
     from walkai_nos_amd.dataplane.procs import run_pods
-    r = run_pods(["16gb"] * pods, seconds=6.0, ready_timeout=240)
+    from walkai_nos_amd.models.slicing.gpu import SlicingGPU
+    from walkai_nos_amd.models.slicing.profile import SKIP_SHARED_COUNTS
+    r = run_pods(["16gb"] * pods, seconds=6.0, ready_timeout=240, sequential=True)
     rates = [p["inf_per_s"] for p in r["per_pod"]]
     assert min(rates) > 0, r
-    assert max(rates) / min(rates) <= 1.3, rates
+    if pods not in SKIP_SHARED_COUNTS:
+        assert max(rates) / min(rates) <= 1.25, rates
+        return
+    g = SlicingGPU("MI355X", 0, 288, 256, {"16gb": pods - 1}, {})
+    assert not g.update_geometry_for({"16gb": 1}), "the planner must not carve this count"
+    even, odd = rates[0::2], rates[1::2]
+    assert max(even) / min(even) <= 1.08 and max(odd) / min(odd) <= 1.08, rates
+    assert min(odd) / max(even) >= 1.1, rates       # the smaller class (odd positions) is faster
 
 
 def test_eight_pod_processes_share_one_gpu_evenly(gpu):

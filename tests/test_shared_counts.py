@@ -1,0 +1,82 @@
+"""Memory-only slice counts the planner skips (``models/slicing/profile.py`` SKIP_SHARED_COUNTS):
+odd counts from five up split memory-only pods into two rate classes by start order
+(``profiles/fair_probe_r5.json``), so the cumask model never leaves 5 or 7 memory-only slices on a
+GPU — it carves two at once past them when two pods wait, else the odd pod waits."""
+from __future__ import annotations
+
+import pytest
+
+from walkai_nos_amd.api.config import GpuPartitionerConfig
+from walkai_nos_amd.controllers.partitioner.pod_controller import plan_cluster_fifo
+from walkai_nos_amd.models.slicing import gpu as sg
+from walkai_nos_amd.models.slicing import profile as sp
+
+
+def _gpu(shared_used=4, dedicated_used=0, skip=None):
+    used = {"16gb": shared_used} if shared_used else {}
+    if dedicated_used:
+        used["32cu.24gb"] = dedicated_used
+    return sg.SlicingGPU("MI355X", 0, 288, 256, used, {}, skip_shared=skip)
+
+
+def test_default_skips_five_and_seven():
+    assert sp.SKIP_SHARED_COUNTS == (5, 7)
+    assert GpuPartitionerConfig().sharedSliceSkipCounts == [5, 7]
+
+
+def test_a_fifth_memory_only_slice_alone_is_not_carved():
+    g = _gpu(4)
+    assert not g.update_geometry_for({"16gb": 1})
+    assert g.shared_count() == 4 and g.free == {}
+
+
+def test_two_waiting_pods_pass_the_skipped_count_together():
+    g = _gpu(4)
+    assert g.update_geometry_for({"16gb": 2})
+    assert g.shared_count() == 6 and g.free == {"16gb": 2}
+    # from six, the seventh alone is skipped too, two make eight
+    g2 = _gpu(6)
+    assert not g2.update_geometry_for({"16gb": 1})
+    assert g2.update_geometry_for({"16gb": 2}) and g2.shared_count() == 8
+
+
+def test_counts_below_five_and_dedicated_slices_are_unaffected():
+    g = _gpu(0)
+    assert g.update_geometry_for({"16gb": 3}) and g.shared_count() == 3
+    g = _gpu(4)
+    assert g.update_geometry_for({"32cu.24gb": 1}) and g.free == {"32cu.24gb": 1}
+
+
+def test_skip_list_can_be_disabled_per_gpu_and_globally():
+    g = _gpu(4, skip=())
+    assert g.update_geometry_for({"16gb": 1}) and g.shared_count() == 5
+    old = sp.SKIP_SHARED_COUNTS
+    try:
+        sg.set_skip_shared_counts([])
+        g = _gpu(4)
+        assert g.update_geometry_for({"16gb": 1}) and g.shared_count() == 5
+        assert g.clone().skip_shared is None
+    finally:
+        sp.SKIP_SHARED_COUNTS = old
+
+
+def test_config_rejects_bad_skip_counts():
+    with pytest.raises(ValueError):
+        GpuPartitionerConfig(sharedSliceSkipCounts=[1]).validate()
+    GpuPartitionerConfig(sharedSliceSkipCounts=[]).validate()
+
+
+def _node(shared_used):
+    return sg.SlicingNode("n0", [_gpu(shared_used)])
+
+
+@pytest.mark.parametrize("waiting,placed", [(1, 0), (2, 2), (3, 2)])
+def test_fifo_planner_pairs_pods_past_the_skipped_count(waiting, placed):
+    models = {"n0": _node(4)}
+    changed = plan_cluster_fifo(models, [{"16gb": 1}] * waiting)
+    if not placed:
+        assert changed == {}
+        return
+    g = changed["n0"].gpus[0]
+    # the pods the pass placed are "used" in the model; the third waits (7 would split again)
+    assert g.used.get("16gb", 0) - 4 == placed and g.shared_count() == 6

@@ -314,3 +314,33 @@ def test_actuator_keeps_no_slice_layout_for_a_gpu_whose_spx_flip_was_skipped_as_
     assert err is not None and pc.set_calls == []                    # busy: not flipped, retried later
     assert set(store.load()) == {1}                                  # GPU 1 (SPX) re-carved; GPU 0 untouched
     assert [s.id for s in store.load()[1]] == ["g1::x0"]
+
+
+def test_default_layout_of_unlabelled_nodes_comes_from_the_partitioner_config():
+    """VERDICT r4 next-round #7: the chart default is the layout the bench measures (slices)."""
+    from walkai_nos_amd.api.config import GpuPartitionerConfig
+    cfg = GpuPartitionerConfig()
+    assert cfg.defaultXcpLayout == "slices"
+    cfg.defaultXcpLayout = "mig"
+    with pytest.raises(ValueError):
+        cfg.validate()
+    n = ko.new_node("n", {api.LABEL_GPU_PARTITIONING: "xcp", "amd.com/gpu.product-name": "AMD_Instinct_MI355X",
+                          "amd.com/gpu.count": "1"})
+    assert xcp_node.get_layout(n) == "partitions"          # library default: unchanged
+    try:
+        xcp_node.set_default_layout("slices")
+        assert xcp_node.get_layout(n) == "slices"
+        n["metadata"]["labels"][api.LABEL_XCP_LAYOUT] = "partitions"
+        assert xcp_node.get_layout(n) == "partitions"      # the label wins
+    finally:
+        xcp_node.set_default_layout("partitions")
+    import os
+
+    import yaml
+    vals = yaml.safe_load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                            "helm-charts", "nos", "values.yaml")))
+    import bench as _bench  # noqa: F401  (bench.py's --layout default, read from its parser)
+    import inspect
+    src = inspect.getsource(_bench.main)
+    assert 'ap.add_argument("--layout", default="slices"' in src
+    assert vals["gpuPartitioner"]["defaultXcpLayout"] == "slices"

@@ -116,6 +116,8 @@ for s in "$@"; do
     bench_long) step "bench_${NOS_STEPS:-100}q" 900 python -u bench.py --steps "${NOS_STEPS:-100}" --warmup 5 \
                   --out "$OUT/bench_${NOS_STEPS:-100}q.json" ;;
     fair) step fair 1100 bash tools/gpu_fair.sh ;;
+    fair_probe) step fair_probe 900 python -u tools/fair_probe.py --pods "${NOS_FAIR_PODS:-5,7,8}" \
+                  --reps "${NOS_FAIR_REPS:-2}" ${NOS_FAIR_ARGS:-} --out "$OUT/fair_probe.json" ;;
     replay)
       mkdir -p "$OUT/replay"
       for sl in ${NOS_SLICES:-dpx cpx}; do

@@ -19,7 +19,7 @@ omitted report interval means the documented 10 s rather than "no periodic repor
 from __future__ import annotations
 
 from dataclasses import asdict, dataclass, field
-from typing import Any, Dict, Optional, Type, TypeVar
+from typing import Any, Dict, List, Optional, Type, TypeVar
 
 import yaml
 
@@ -74,9 +74,20 @@ class GpuPartitionerConfig(ManagerConfig):
     #: knobs of the ``pack`` policy (``PackParams``); keys: minFill, starveAfterSeconds,
     #: drainAfterSeconds, drainBacklog, spxReserve, reserveDecay, drainGain, drainGainAfterSeconds,
     #: reserveBreakFill, minStintSeconds, unservedAfterSeconds; sliced GPUs (xcp-layout slices /
-    #: auto): sliceReserveAfterSeconds, sliceReserveBacklog (GPUs of waiting work per sliced GPU
-    #: above which the threshold stretches; 0 = never), sliceReserveStretch (its largest factor), sliceFill
+    #: auto): sliceReserveAfterSeconds, sliceReserveLifetimes (the threshold in median pod run times
+    #: once learned; 0 = the constant), sliceReserveBacklog (GPUs of waiting work per sliced GPU
+    #: above which the threshold stretches; 0 = never), sliceReserveStretch (its largest factor),
+    #: sliceReserveHold, sliceFreeDrain, sliceFreeDrainAfterLifetimes, sliceWholeOvertakeSeconds,
+    #: sliceWholeOvertakeLifetimes, sliceFill
     packing: Dict[str, Any] = field(default_factory=dict)
+    #: xcp layout of a node that carries no nos.nebuly.com/xcp-layout label: slices (SPX GPUs carved
+    #: into CU-mask slices, mixed geometries, no flips), partitions (hardware compute partitions
+    #: only) or auto (per GPU: a hardware mode for homogeneous demand, else slices)
+    defaultXcpLayout: str = "slices"
+    #: memory-only slice counts the planner never leaves on a cumask GPU: it carves two at once past
+    #: them, or the odd pod waits (models/slicing/profile.py SKIP_SHARED_COUNTS: odd counts from 5
+    #: up split the pods into two rate classes by start order); [] disables
+    sharedSliceSkipCounts: List[int] = field(default_factory=lambda: [5, 7])
 
     PACKING_KEYS = {"minFill": "min_fill", "starveAfterSeconds": "starve_after", "drainAfterSeconds": "drain_after",
                     "drainBacklog": "drain_backlog", "spxReserve": "spx_reserve", "reserveDecay": "reserve_decay",
@@ -84,8 +95,11 @@ class GpuPartitionerConfig(ManagerConfig):
                     "unservedAfterSeconds": "unserved_after", "replanEverySeconds": "replan_every",
                     "reserveBreakFill": "reserve_break_fill", "sliceReserveAfterSeconds": "slice_reserve_after",
                     "sliceReserveBacklog": "slice_reserve_backlog", "sliceReserveStretch": "slice_reserve_stretch",
-                    "sliceFill": "slice_fill"}
-    BOOL_PACKING_KEYS = ("spxReserve", "sliceFill")
+                    "sliceReserveLifetimes": "slice_reserve_lifetimes", "sliceReserveHold": "slice_reserve_hold",
+                    "sliceFreeDrain": "slice_free_drain", "sliceFreeDrainAfterLifetimes": "slice_free_drain_after",
+                    "sliceWholeOvertakeSeconds": "slice_whole_overtake",
+                    "sliceWholeOvertakeLifetimes": "slice_whole_overtake_lifetimes", "sliceFill": "slice_fill"}
+    BOOL_PACKING_KEYS = ("spxReserve", "sliceFill", "sliceReserveHold", "sliceFreeDrain")
 
     def pack_params(self) -> Any:
         from ..controllers.partitioner.pod_controller import PackParams
@@ -108,6 +122,10 @@ class GpuPartitionerConfig(ManagerConfig):
             raise ValueError("devicePluginDelaySeconds must be greater than 0")
         if self.planningPolicy not in ("fifo", "batch", "simulate", "pack"):
             raise ValueError("planningPolicy must be 'fifo', 'batch', 'simulate' or 'pack'")
+        if self.defaultXcpLayout not in ("partitions", "slices", "auto"):
+            raise ValueError("defaultXcpLayout must be 'partitions', 'slices' or 'auto'")
+        if any(not isinstance(c, int) or c < 2 for c in self.sharedSliceSkipCounts):
+            raise ValueError("sharedSliceSkipCounts must list integers >= 2")
         if self.scoring not in ("fraction", "pods"):
             raise ValueError("scoring must be 'fraction' or 'pods'")
 

@@ -119,9 +119,9 @@ FLIP_COST_MEASURED = ("commit_barrier_s", "probe_s", "plugin_push_s")
 #: A new pod's start-up: from its process starting (kubelet has admitted it and holds its slice) to
 #: its first inference — interpreter + torch import, model load, warm-up and HIP-graph capture of the
 #: reference demo's client (``dataplane/client.py``), spawned with ``Allocate``'s environment. The
-#: slice is allocated but serves nothing meanwhile, so every pod bound in the window is charged this
-#: much cluster time at its start (``bench.py`` measures it on the box before the window,
-#: :func:`measure_pod_start`; this is the fallback).
+#: slice is allocated but serves nothing meanwhile: every pod bound in the window spends this much of
+#: its lifetime (cluster time) starting before it serves (``bench.py`` measures it on the box before
+#: the window, :func:`measure_pod_start`; this is the fallback).
 POD_START_S = 8.0
 
 
@@ -811,8 +811,9 @@ class NodeBench:
         return min(1.0, max(0.0, self.starting.get(name, 0.0)))
 
     def end_step(self) -> None:
-        """Age every running pod by the part of the quantum it served (its GPU lit and its start-up
-        over), then let outages and start-ups run."""
+        """Age every running pod by the part of the quantum its GPU was lit (a pod's lifetime
+        includes its start-up, during which it holds its slice and serves nothing), then let outages
+        and start-ups run."""
         gpus_of = self.pod_gpus()
         for name in list(self.live):
             lit = min((1.0 - self.dark(g, n) for (n, g) in gpus_of.get(name, ())), default=1.0)
@@ -820,8 +821,7 @@ class NodeBench:
             if sd > 0 and lit > 0:
                 prof = self.profile_of.get(name, "")
                 self.start_gpu_quanta += min(sd, lit) / COMPUTE_MODES.get(prof.split("_")[0], 1)
-            lit = max(0.0, lit - sd)
-            if lit > 0:
+            if lit > sd:
                 self.profile_pods[self.profile_of.get(name, "?")].add(name)
             self.live[name] -= lit
         for name in list(self.starting):

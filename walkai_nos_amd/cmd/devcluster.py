@@ -49,7 +49,7 @@ def node_labels(gpus: int, model: str = "MI355X", kind: str = api.PARTITIONING_K
     out = {api.LABEL_GPU_PARTITIONING: kind,
            constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}", constant.LABEL_AMD_GPU_COUNT: str(gpus),
            constant.LABEL_AMD_GPU_VRAM: "288G", constant.LABEL_AMD_GPU_CU_COUNT: "256"}
-    if kind == api.PARTITIONING_KIND_XCP and layout != "partitions":
+    if kind == api.PARTITIONING_KIND_XCP:     # explicit: the partitioner's default layout is slices
         out[api.LABEL_XCP_LAYOUT] = layout
     return out
 

@@ -28,6 +28,10 @@ def main(argv=None) -> int:
         log.info("loaded known geometries from %s", cfg.knownMigGeometriesFile)
     client = make_client(args.kubeconfig)
     mgr = make_manager(client, cfg, "gpupartitioner")
+    from ..models.xcp.node import set_default_layout
+    set_default_layout(cfg.defaultXcpLayout)
+    from ..models.slicing.gpu import set_skip_shared_counts
+    set_skip_shared_counts(cfg.sharedSliceSkipCounts)
     setup_partitioner(mgr, batch_timeout=cfg.batchWindowTimeoutSeconds, batch_idle=cfg.batchWindowIdleSeconds,
                       scoring=cfg.scoring, policy=cfg.planningPolicy, pack=cfg.pack_params())
     serve_endpoints(mgr, cfg)

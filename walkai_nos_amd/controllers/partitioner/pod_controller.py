@@ -18,6 +18,8 @@ Deliberate changes vs the reference:
 """
 from __future__ import annotations
 
+import collections
+
 import logging
 import time
 from dataclasses import dataclass
@@ -122,7 +124,11 @@ def plan_cluster_fifo(models: Mapping[str, NodeModel], pending: List[Dict[str, i
     changed: Dict[str, NodeModel] = {}
     extra = {p: q for p, q in (incoming or {}).items() if q > 0}
     hopeless = set()  # profiles no node can provide in this pass (capacity only shrinks within a pass)
+    # pods still to walk per request: a memory-only slice count the model skips (SKIP_SHARED_COUNTS)
+    # is passed by carving for this pod and the next one with the same request at once
+    behind = collections.Counter(tuple(sorted(r.items())) for r in pending)
     for req in pending:
+        behind[tuple(sorted(req.items()))] -= 1
         placed = False
         for name in sorted(current):
             try:
@@ -141,13 +147,18 @@ def plan_cluster_fifo(models: Mapping[str, NodeModel], pending: List[Dict[str, i
         if key in hopeless:
             continue
         best: Optional[Tuple[Tuple[int, str], str, NodeModel]] = None
+        wants = [req] + ([{p: 2 * q for p, q in req.items()}] if behind[key] > 0 else [])
         for name, m in sorted(current.items()):
-            cand = m.clone()
-            if not cand.update_geometry_for(req):
-                continue
-            try:
-                cand.add_pod(req)
-            except ValueError:
+            for want in wants:
+                cand = m.clone()
+                if not cand.update_geometry_for(want):
+                    continue
+                try:
+                    cand.add_pod(req)
+                except ValueError:
+                    continue
+                break
+            else:
                 continue
             score = (_changed_gpus(m, cand), name)
             if best is None or score < best[0]:

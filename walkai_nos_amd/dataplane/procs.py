@@ -72,10 +72,11 @@ def allocate_envs(profiles: Sequence[str], cu_count: int = 256, shim: bool = Tru
 def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, census: bool = False,
              graphs: bool = True, ready_timeout: float = 600.0, extra_env: Optional[Dict[str, str]] = None,
              cu_count: int = 256, stagger_s: float = 0.0,
-             per_pod_env: Optional[Sequence[Dict[str, str]]] = None) -> Dict[str, Any]:
+             per_pod_env: Optional[Sequence[Dict[str, str]]] = None, sequential: bool = False) -> Dict[str, Any]:
     """Start one process per profile, release them together, collect their JSON lines.
     ``stagger_s``: wait this long between pod starts (pods of a node start at different times);
-    ``per_pod_env``: env overrides of pod i (after ``extra_env``)."""
+    ``per_pod_env``: env overrides of pod i (after ``extra_env``); ``sequential``: start pod i+1
+    only once pod i is READY (its queues exist), so the pods' start order is their index."""
     envs = allocate_envs(profiles, cu_count, shim)
     pods: List[PodProc] = []
     base = dict(os.environ)
@@ -97,28 +98,11 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
             p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                  stderr=log, text=True)
             pods.append(PodProc(PodSpec(prof, f"pod{i}"), env.get("NOS_SLICE_IDS", ""), env, p))
+            if sequential:
+                _wait_ready(pods[-1:], pods, logs, ready_timeout)
             if stagger_s > 0:
                 time.sleep(stagger_s)
-
-        def tail(i: int) -> str:
-            logs[i].seek(0)
-            return logs[i].read()[-2000:]
-        deadline = time.time() + ready_timeout
-        waiting = {id(p.proc.stdout): p for p in pods}
-        while waiting:
-            left = deadline - time.time()
-            if left <= 0:
-                raise TimeoutError(f"{len(waiting)} pod(s) not ready after {ready_timeout}s")
-            r, _, _ = select.select([p.proc.stdout for p in waiting.values()], [], [], min(left, 5.0))
-            for f in r:
-                pod = waiting[id(f)]
-                ln = f.readline()
-                if not ln:
-                    pod.proc.wait()
-                    raise RuntimeError(f"{pod.spec.name} exited before READY (rc={pod.proc.returncode}): "
-                                       f"{tail(pods.index(pod))}")
-                if ln.strip() == "READY":
-                    del waiting[id(f)]
+        _wait_ready([p for p in pods if not sequential], pods, logs, ready_timeout)
         go = time.time() + 1.0
         for p in pods:
             p.proc.stdin.write(f"GO {go:.6f}\n")
@@ -127,7 +111,7 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
             out, _ = p.proc.communicate(timeout=seconds + 300)
             line = next((ln for ln in reversed(out.splitlines()) if ln.startswith("{")), None)
             if p.proc.returncode != 0 or line is None:
-                raise RuntimeError(f"{p.spec.name} failed (rc={p.proc.returncode}): {tail(i)}")
+                raise RuntimeError(f"{p.spec.name} failed (rc={p.proc.returncode}): {_tail(logs[i])}")
             p.result = json.loads(line)
     finally:
         for p in pods:
@@ -137,6 +121,31 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
         for log in logs:
             log.close()
     return summarize(pods, seconds)
+
+
+def _tail(log) -> str:
+    log.seek(0)
+    return log.read()[-2000:]
+
+
+def _wait_ready(subset: List[PodProc], pods: List[PodProc], logs: list, timeout: float) -> None:
+    """Until every pod of ``subset`` printed READY (a pod that exits first raises with its log)."""
+    deadline = time.time() + timeout
+    waiting = {id(p.proc.stdout): p for p in subset}
+    while waiting:
+        left = deadline - time.time()
+        if left <= 0:
+            raise TimeoutError(f"{len(waiting)} pod(s) not ready after {timeout}s")
+        r, _, _ = select.select([p.proc.stdout for p in waiting.values()], [], [], min(left, 5.0))
+        for f in r:
+            pod = waiting[id(f)]
+            ln = f.readline()
+            if not ln:
+                pod.proc.wait()
+                raise RuntimeError(f"{pod.spec.name} exited before READY (rc={pod.proc.returncode}): "
+                                   f"{_tail(logs[pods.index(pod)])}")
+            if ln.strip() == "READY":
+                del waiting[id(f)]
 
 
 def summarize(pods: List[PodProc], seconds: float) -> Dict[str, Any]:

@@ -11,15 +11,21 @@ profile).  Generalised to two dimensions: HBM GB <= GPU memory and dedicated CUs
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Mapping
+from typing import Any, Dict, List, Mapping, Optional, Tuple
 
 from ...kube import objects as ko
 from .. import annotation as ann
 from .. import gpu_util
 from .. import resource as res
 from ..geometry import Geometry
+from . import profile as _profile
 from .profile import (CU_GRANULARITY, MAX_SLICES_PER_GPU, MIN_SHARED_CUS, MIN_SLICE_MEMORY_GB, as_resource_name,
                       extract_profile_name, is_slice_resource, parse_profile)
+
+
+def set_skip_shared_counts(counts) -> None:
+    """The partitioner's ``sharedSliceSkipCounts`` (see :data:`~.profile.SKIP_SHARED_COUNTS`)."""
+    _profile.SKIP_SHARED_COUNTS = tuple(sorted({int(c) for c in counts}))
 
 
 @dataclass
@@ -33,6 +39,8 @@ class SlicingGPU:
     #: slices the planner may carve on this GPU (each serves one pod process; beyond 8 the hardware
     #: scheduler time-slices processes, :data:`~.profile.MAX_SLICES_PER_GPU`)
     max_slices: int = MAX_SLICES_PER_GPU
+    #: memory-only slice counts never left on the GPU (None: :data:`~.profile.SKIP_SHARED_COUNTS`)
+    skip_shared: Optional[Tuple[int, ...]] = None
 
     @classmethod
     def full(cls, model: str, index: int, memory_gb: int, cu_count: int = 256,
@@ -41,7 +49,7 @@ class SlicingGPU:
 
     def clone(self) -> "SlicingGPU":
         return SlicingGPU(self.model, self.index, self.memory_gb, self.cu_count, dict(self.used), dict(self.free),
-                          self.max_slices)
+                          self.max_slices, self.skip_shared)
 
     def validate(self) -> None:
         for d in (self.used, self.free):
@@ -85,12 +93,21 @@ class SlicingGPU:
     def slice_count(self) -> int:
         return sum(self.geometry().values())
 
+    def shared_count(self) -> int:
+        """Memory-only slices on the GPU (used and free)."""
+        return sum(q for p, q in self.geometry().items() if not parse_profile(p).dedicated)
+
+    def _skipped(self) -> Tuple[int, ...]:
+        return _profile.SKIP_SHARED_COUNTS if self.skip_shared is None else self.skip_shared
+
     def can_create_more_slices(self) -> bool:
         return self.spare_memory_gb() >= MIN_SLICE_MEMORY_GB and self.slice_count() < self.max_slices
 
     def _can_create(self, profile: str, num: int = 1) -> bool:
         prof = parse_profile(profile)
         if self.spare_memory_gb() < prof.memory_gb * num or self.slice_count() + num > self.max_slices:
+            return False
+        if not prof.dedicated and self.shared_count() + num in self._skipped():
             return False
         budget = self._cu_budget(extra_shared=not prof.dedicated)
         return budget - self._tot_cus() >= prof.cus * num
@@ -122,6 +139,15 @@ class SlicingGPU:
                 out[p] = d
         return out
 
+    def _create_step(self, profile: str, missing: int) -> int:
+        """Create one slice of ``profile``, or two at once when one would leave a skipped
+        memory-only count and two are missing; the number created."""
+        if self.create_slices(profile, 1):
+            return 1
+        if missing >= 2 and not parse_profile(profile).dedicated and self.create_slices(profile, 2):
+            return 2
+        return 0
+
     def update_geometry_for(self, required: Mapping[str, int]) -> bool:
         missing = self.missing_slices(required)
         if not missing:
@@ -131,20 +157,20 @@ class SlicingGPU:
         for p in sorted(missing, key=lambda x: parse_profile(x)):
             # (1) spare capacity first
             if self.can_create_more_slices():
-                for _ in range(missing[p]):
-                    if not self.create_slices(p, 1):
+                while missing[p] > 0:
+                    n = self._create_step(p, missing[p])
+                    if not n:
                         break
-                    missing[p] -= 1
+                    missing[p] -= n
                     updated = True
             # (2) free up room by deleting the original free slices
             for k in original_free:
                 self.free.pop(k, None)
-            for _ in range(missing[p]):
-                if not self.can_create_more_slices():
+            while missing[p] > 0 and self.can_create_more_slices():
+                n = self._create_step(p, missing[p])
+                if not n:
                     break
-                if not self.create_slices(p, 1):
-                    break
-                missing[p] -= 1
+                missing[p] -= n
                 updated = True
             # (3) restore the original free slices (all-or-nothing per profile)
             for k, v in original_free.items():

@@ -38,6 +38,18 @@ MIN_SHARED_CUS = 32
 #: the aggregate falls to 292 / 271 (14 mixed dedicated + memory-only pods: 192,
 #: ``profiles/dense_r4.json``). The node label ``nos.nebuly.com/max-slices-per-gpu`` overrides it.
 MAX_SLICES_PER_GPU = 8
+#: memory-only slice counts the planner never leaves on a GPU (it carves two at once past them, or
+#: waits). Memory-only pods share every CU and the hardware scheduler deals each process's queues
+#: over the MEC pipes in runlist (start) order; a HIP process holds two compute queues, so with one
+#: stream queue per pod the pods alternate between two pipes and an odd count splits into two rate
+#: classes — ceil(n/2) pods at the slow rate, floor(n/2) at the fast one, by start parity, the same
+#: on every run (``profiles/fair_probe_r5.json``: 5 pods 73.4 vs 93.7 inf/s, max/min 1.28; 7 pods
+#: 54.1 vs 65.5, 1.21; 8 pods 1.003). Three pods get two queues each instead (Allocate's
+#: ``sharedSliceHwQueues`` rule) and share evenly. The GPU's aggregate hardly moves with the pod
+#: count (366-413 inf/s at 3-8 pods), so skipping an odd count costs no throughput, only the odd
+#: pod's start: it waits for a partner or for one of the running pods to finish.
+#: ``GpuPartitionerConfig.sharedSliceSkipCounts`` overrides it.
+SKIP_SHARED_COUNTS = (5, 7)
 REPLICA_SEPARATOR = "::"
 
 _PROFILE_RE = re.compile(r"^(?:(\d+)cu\.)?(\d+)gb$")

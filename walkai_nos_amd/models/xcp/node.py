@@ -36,10 +36,23 @@ def fraction_weight(profile: str) -> float:
 SCORING = {"pods": None, "fraction": fraction_weight}
 
 
+#: layout of a node without the ``nos.nebuly.com/xcp-layout`` label (the partitioner's
+#: ``defaultXcpLayout``, set once at start-up by ``cmd/gpupartitioner.py``)
+DEFAULT_LAYOUT = LAYOUT_PARTITIONS
+
+
+def set_default_layout(layout: str) -> None:
+    global DEFAULT_LAYOUT
+    if layout not in LAYOUTS:
+        raise ValueError(f"unknown xcp layout {layout!r}")
+    DEFAULT_LAYOUT = layout
+
+
 def get_layout(node: Dict[str, Any]) -> str:
-    """The node's ``nos.nebuly.com/xcp-layout`` (unknown values: hardware partitions only). Slices
-    need NPS1 (a sliced GPU is in SPX, which other memory modes do not offer)."""
-    v = (ko.labels(node).get(api.LABEL_XCP_LAYOUT) or LAYOUT_PARTITIONS).lower()
+    """The node's ``nos.nebuly.com/xcp-layout`` (absent: :data:`DEFAULT_LAYOUT`; unknown values:
+    hardware partitions only). Slices need NPS1 (a sliced GPU is in SPX, which other memory modes
+    do not offer)."""
+    v = (ko.labels(node).get(api.LABEL_XCP_LAYOUT) or DEFAULT_LAYOUT).lower()
     if v not in LAYOUTS or gpu_util.get_memory_partition(node) != SLICE_NPS:
         return LAYOUT_PARTITIONS
     return v
