@@ -31,9 +31,11 @@ def main() -> int:
     ap.add_argument("--backend", choices=("hip", "torch"), default="hip")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--preroll", type=int, default=60,
-                    help="control-plane-only steps before warmup, so timing starts in steady state")
-    ap.add_argument("--quantum", type=float, default=0.5, help="wall seconds of serving per step")
-    ap.add_argument("--cluster-s", type=float, default=60.0, help="cluster seconds one step stands for")
+                    help="control-plane-only quanta before warmup, so timing starts in steady state")
+    ap.add_argument("--quantum", type=float, default=0.5, help="wall seconds of serving per quantum")
+    ap.add_argument("--cluster-s", type=float, default=60.0, help="cluster seconds one quantum stands for")
+    ap.add_argument("--quanta-per-step", type=int, default=2,
+                    help="quanta per driver step: the timed window is steps x this many quanta")
     ap.add_argument("--flip-cost", type=float, default=-1.0,
                     help="cluster seconds a GPU serves nothing per compute-partition flip "
                          "(default: the measured components, bench_core.FLIP_COST_COMPONENTS)")
@@ -87,6 +89,7 @@ def main() -> int:
     cfg = BenchConfig(gpus=gpus, steps=args.steps, warmup=args.warmup, seed=args.seed, offered_load=args.load,
                       backend=args.backend, graphs=not args.no_graphs, rank=rank, world=world,
                       preroll=args.preroll, quantum_s=args.quantum, cluster_s=args.cluster_s,
+                      quanta_per_step=args.quanta_per_step,
                       flip_cost_s=args.flip_cost, policy=args.policy, depth=args.depth,
                       density=not args.no_density, pod_streams=args.pod_streams, lane_cus=args.lane_cus,
                       device_plugin=args.device_plugin, layout=args.layout, pod_start_s=args.pod_start,

@@ -22,6 +22,7 @@
 #   bench_runs         bench.py once per NOS_BENCH_RUNS entry ("<tag>:<arg>,<arg> ..."), e.g. layouts / seeds
 #   bench_long         bench.py over NOS_STEPS quanta (default 100) for a longer window
 #   fair               tools/gpu_fair.sh: memory-only fairness as processes (NOS_FAIR_ONLY, NOS_FAIR_VARIANTS)
+#   fair_probe         tools/fair_probe.py: per-pod rates, amd-smi CU occupancy, KFD queues (NOS_FAIR_PODS)
 #   replay             tools/model_replay.py + replay_stats kernel traces per slice (NOS_SLICES, default "dpx cpx")
 #   procs_cap          tools/multiproc.py at 8-12 memory-only pods + the KFD queue properties
 #   cu_guard           the CU-mask bypass guard test on real amd-smi (gpurun_out/cu_guard_samples.json)

@@ -5,10 +5,12 @@ mixed fractional-GPU load*, on the workload the reference publishes numbers for 
 batch-1 inference pods, ``demos/gpu-sharing-comparison``).  ``value`` is the aggregate inference
 rate the node sustains; allocation %, pods/node and per-profile service are reported next to it.
 
-**Time model: a compressed replay of cluster time.**  One step = one *quantum* of
-``cluster_s`` (60) seconds of cluster time, replayed in ``quantum_s`` (0.5) wall seconds of GPU
-serving.  Every cluster-time duration is compressed by the same factor — pod lifetimes (2-6
-quanta, so the driver's 20 timed steps span 5 mean lifetimes), the planner's thresholds and every
+**Time model: a compressed replay of cluster time.**  One *quantum* = ``cluster_s`` (60) seconds
+of cluster time, replayed in ``quantum_s`` (0.5) wall seconds of GPU serving; one driver step =
+``quanta_per_step`` (2) quanta, so the driver's 20 timed steps span 40 quanta = 10 mean pod
+lifetimes (a 20-quantum window's allocation varies with the churn seed by sd 5.9 points, a
+40-quantum one by 3.2: ``profiles/window_length_r5.json``).  Every cluster-time duration is
+compressed by the same factor — pod lifetimes (2-6 quanta), the planner's thresholds and every
 compute-partition flip's outage — while the GPU serves at its real rate, so inferences per wall
 second of the replay equal inferences per second of the cluster.  Per quantum:
 
@@ -140,10 +142,11 @@ class BenchConfig:
     warmup: int = 5
     seed: int = 1234
     offered_load: float = 1.0            # offered GPU-equivalents per GPU (= capacity)
-    quantum_s: float = 0.5               # wall seconds of serving per step
-    cluster_s: float = 60.0              # cluster seconds one step stands for (the replay's compression)
+    quantum_s: float = 0.5               # wall seconds of serving per quantum
+    cluster_s: float = 60.0              # cluster seconds one quantum stands for (the replay's compression)
+    quanta_per_step: int = 2             # quanta per driver step (window = steps x this many quanta)
     flip_cost_s: float = -1.0            # cluster seconds a GPU is dark per flip (<0: FLIP_COST_COMPONENTS)
-    lifetime: Tuple[int, int] = (2, 6)   # served quanta per pod (uniform, stratified): mean 4 = 5 in 20 steps
+    lifetime: Tuple[int, int] = (2, 6)   # served quanta per pod (uniform, stratified): mean 4 = 10 in 20 steps
     hw: Tuple[int, int] = (800, 1066)
     backend: str = "hip"
     graphs: bool = True
@@ -186,6 +189,14 @@ class BenchConfig:
     def flip_quanta(self) -> float:
         """A flip's outage in quanta (fractional)."""
         return self.flip_cost_s / self.cluster_s
+
+    @property
+    def warmup_quanta(self) -> int:
+        return self.warmup * self.quanta_per_step
+
+    @property
+    def window_quanta(self) -> int:
+        return self.steps * self.quanta_per_step
 
     @property
     def mean_lifetime_quanta(self) -> float:
@@ -1072,7 +1083,8 @@ def flip_sensitivity(cfg: BenchConfig, costs=(2.0, 5.0, 10.0, 30.0), steps: Opti
     out: Dict[str, Any] = {}
     for fc in costs:
         c = dataclasses.replace(cfg, flip_cost_s=fc, rank=0, world=1)
-        r = control_only(c, steps if steps is not None else cfg.warmup + cfg.steps, skip=cfg.warmup)
+        r = control_only(c, steps if steps is not None else cfg.warmup_quanta + cfg.window_quanta,
+                         skip=cfg.warmup_quanta)
         out[f"{fc:g}s"] = {k: r[k] for k in ("util_pct", "flips", "time_in_flip_pct", "inf_per_s_model")}
     return out
 
@@ -1085,7 +1097,7 @@ def pod_start_sensitivity(cfg: BenchConfig, factors=(0.0, 1.0, 2.0, 4.0)) -> Dic
     out: Dict[str, Any] = {}
     for f in factors:
         c = dataclasses.replace(cfg, pod_start_s=f * cfg.pod_start_s, rank=0, world=1)
-        r = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
+        r = control_only(c, cfg.warmup_quanta + cfg.window_quanta, skip=cfg.warmup_quanta)
         out[f"{round(f * cfg.pod_start_s, 1):g}s"] = {k: r[k] for k in ("util_pct", "inf_per_s_model")}
     return out
 
@@ -1098,14 +1110,14 @@ def seed_model(cfg: BenchConfig, seeds=tuple(range(1, 11))) -> Dict[str, Any]:
     rows = {}
     for sd in seeds:
         c = dataclasses.replace(cfg, seed=sd, rank=0, world=1)
-        r = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
+        r = control_only(c, cfg.warmup_quanta + cfg.window_quanta, skip=cfg.warmup_quanta)
         rows[str(sd)] = {"inf_per_s_model": r["inf_per_s_model"], "util_pct": r["util_pct"],
                          "pending_mean": r["pending_mean"],
                          "served": {p: v["inferences"] > 0 for p, v in r["per_profile"].items()}}
     v = [x["inf_per_s_model"] for x in rows.values()]
     u = sorted(x["util_pct"] for x in rows.values())
     c = dataclasses.replace(cfg, rank=0, world=1)
-    own = control_only(c, cfg.warmup + cfg.steps, skip=cfg.warmup)
+    own = control_only(c, cfg.warmup_quanta + cfg.window_quanta, skip=cfg.warmup_quanta)
     return {"seeds": list(seeds), "mean": round(sum(v) / len(v), 1), "min": min(v), "max": max(v),
             "util_pct_mean": round(sum(u) / len(u), 2), "util_pct_min": u[0],
             "this_seed_model": own["inf_per_s_model"], "this_seed_util_pct": own["util_pct"],
@@ -1179,7 +1191,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     for _ in range(cfg.preroll):
         nb.control_step()
         nb.end_step()
-    for _ in range(cfg.warmup):
+    for _ in range(cfg.warmup_quanta):
         nb.step()
     sync()
     if distributed:
@@ -1192,7 +1204,7 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         busy.start()
     t0 = time.perf_counter()
     deadline = t0
-    for _ in range(cfg.steps):
+    for _ in range(cfg.window_quanta):
         deadline += cfg.quantum_s
         nb.step(deadline)
     sync()
@@ -1266,10 +1278,11 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "inference_latency_ms": latency,
         "pending_pods_mean": round(_mean(nb.pending_samples), 2),
         "pending_pods_max": max(nb.pending_samples) if nb.pending_samples else 0,
-        "window": {"quanta": cfg.steps, "cluster_s_per_quantum": cfg.cluster_s, "wall_s_per_quantum": cfg.quantum_s,
+        "window": {"quanta": cfg.window_quanta, "quanta_per_step": cfg.quanta_per_step,
+                   "cluster_s_per_quantum": cfg.cluster_s, "wall_s_per_quantum": cfg.quantum_s,
                    "compression": round(cfg.cluster_s / cfg.quantum_s, 1),
                    "mean_pod_lifetime_quanta": cfg.mean_lifetime_quanta,
-                   "pod_lifetimes_in_window": round(cfg.steps / cfg.mean_lifetime_quanta, 2),
+                   "pod_lifetimes_in_window": round(cfg.window_quanta / cfg.mean_lifetime_quanta, 2),
                    "mean_pod_lifetime_cluster_s": life_s},
         "flip_cost": flip_cost_report(cfg),
         "flips": nb.flips,
