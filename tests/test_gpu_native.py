@@ -330,6 +330,7 @@ def test_memory_only_slice_processes_share_compute_evenly(gpu, pods):
     from walkai_nos_amd.models.slicing.profile import SKIP_SHARED_COUNTS
     r = run_pods(["16gb"] * pods, seconds=6.0, ready_timeout=240, sequential=True)
     rates = [p["inf_per_s"] for p in r["per_pod"]]
+    print(f"memory-only pods={pods} inf/s by start order {rates} max/min {max(rates) / max(1e-9, min(rates)):.3f}")
     assert min(rates) > 0, r
     if pods not in SKIP_SHARED_COUNTS:
         assert max(rates) / min(rates) <= 1.25, rates

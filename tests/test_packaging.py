@@ -248,6 +248,7 @@ def test_helm_chart_renders_to_valid_objects():
     cms = {o["metadata"]["name"]: o for o in objs if o["kind"] == "ConfigMap"}
     cfg = load_config(cms["nos-gpu-partitioner-config"]["data"]["gpu_partitioner_config.yaml"])
     assert cfg.planningPolicy == "pack" and cfg.metricsBindAddress == "127.0.0.1:8080"
+    assert cfg.defaultXcpLayout == "slices" and cfg.sharedSliceSkipCounts == [5, 7]
     assert "known_geometries.yaml" in cms["nos-gpu-partitioner-config"]["data"]
 
 

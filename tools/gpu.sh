@@ -61,7 +61,7 @@ pmc() {  # pmc <dir> <tag> <program...> -- <counters>: one counter pass, kernel 
 for s in "$@"; do
   case $s in
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 --timeout-method thread ;;
-    test_k) step "test_${NOS_TEST_K:-x}" 600 python -u -m pytest tests -m gpu -x -v -rf --timeout 300 \
+    test_k) step "test_${NOS_TEST_K:-x}" 600 python -u -m pytest tests -m gpu -x -v -rfP --timeout 300 \
               --timeout-method thread -k "${NOS_TEST_K:-x}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 --out "$OUT/bench.json" ;;

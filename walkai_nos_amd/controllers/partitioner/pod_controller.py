@@ -196,7 +196,7 @@ class PackParams:
     slice_reserve_lifetimes: float = 3.75  # ... once the planner has seen pods finish (lifetimes.py): this
                                     # many median pod run times instead (0 = keep the constant)
     slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
-    slice_reserve_stretch: float = 1.5  # ... at most this many times
+    slice_reserve_stretch: float = 2.0  # ... at most this many times
     slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed
     slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
     slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
