@@ -9,6 +9,7 @@
 #   test_k             pytest -m gpu -k "$NOS_TEST_K"
 #   smoke              __graft_entry__.smoke()
 #   bench              bench.py as the driver runs it (--gpus 1 --steps 20 --warmup 5)
+#   bench_ranks        the driver's N > 1 launch rehearsed on the one GPU: NOS_RANKS ranks (default 2) over gloo
 #   bench_torch        bench.py on the PyTorch (hipBLASLt) backend, for comparison
 #   seeds              the bench window over churn seeds 1-5 and 1234 (NOS_SEEDS overrides)
 #   operator           tools/operator_gpu_report.py: device map, commit barrier, probes
@@ -65,6 +66,9 @@ for s in "$@"; do
               --timeout-method thread -k "${NOS_TEST_K:-x}" ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5 --out "$OUT/bench.json" ;;
+    bench_ranks) step "bench_${NOS_RANKS:-2}rank" 900 env NOS_BENCH_DIST_BACKEND=gloo python -m torch.distributed.run \
+                   --nnodes=1 --nproc-per-node "${NOS_RANKS:-2}" --master-addr 127.0.0.1 --master-port 29517 bench.py \
+                   --gpus "${NOS_RANKS:-2}" --steps 20 --warmup 5 --no-density ;;
     bench_torch) step bench_torch 600 python bench.py --steps 20 --warmup 5 --backend torch --out "$OUT/bench_torch.json" ;;
     seeds)
       mkdir -p "$OUT/seeds"
