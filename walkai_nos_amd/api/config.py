@@ -77,7 +77,7 @@ class GpuPartitionerConfig(ManagerConfig):
     #: auto): sliceReserveAfterSeconds, sliceReserveLifetimes (the threshold in median pod run times
     #: once learned; 0 = the constant), sliceReserveBacklog (GPUs of waiting work per sliced GPU
     #: above which the threshold stretches; 0 = never), sliceReserveStretch (its largest factor),
-    #: sliceReserveHold, sliceFreeDrain, sliceFreeDrainAfterLifetimes, sliceWholeOvertakeSeconds,
+    #: sliceReserveHold, sliceReserveHoldMaxGpus, sliceFreeDrain, sliceFreeDrainAfterLifetimes, sliceWholeOvertakeSeconds,
     #: sliceWholeOvertakeLifetimes, sliceFill
     packing: Dict[str, Any] = field(default_factory=dict)
     #: xcp layout of a node that carries no nos.nebuly.com/xcp-layout label: slices (SPX GPUs carved
@@ -96,6 +96,7 @@ class GpuPartitionerConfig(ManagerConfig):
                     "reserveBreakFill": "reserve_break_fill", "sliceReserveAfterSeconds": "slice_reserve_after",
                     "sliceReserveBacklog": "slice_reserve_backlog", "sliceReserveStretch": "slice_reserve_stretch",
                     "sliceReserveLifetimes": "slice_reserve_lifetimes", "sliceReserveHold": "slice_reserve_hold",
+                    "sliceReserveHoldMaxGpus": "slice_reserve_hold_max_gpus",
                     "sliceFreeDrain": "slice_free_drain", "sliceFreeDrainAfterLifetimes": "slice_free_drain_after",
                     "sliceWholeOvertakeSeconds": "slice_whole_overtake",
                     "sliceWholeOvertakeLifetimes": "slice_whole_overtake_lifetimes", "sliceFill": "slice_fill"}

@@ -197,7 +197,9 @@ class PackParams:
                                     # many median pod run times instead (0 = keep the constant)
     slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
     slice_reserve_stretch: float = 2.0  # ... at most this many times
-    slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed
+    slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed ...
+    slice_reserve_hold_max_gpus: int = 2  # ... on clusters of at most this many sliced GPUs (0 = any size): with
+                                    # more, another GPU empties soon enough and a held drain idles capacity
     slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
     slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
     slice_whole_overtake: float = 960.0  # seconds: a whole-GPU slice left free goes to the next whole-GPU pod

@@ -128,7 +128,8 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     # backlog let reservations lapse, and small pods refilled the GPU in between: the drain never
     # ended, and the groups its pods freed idled all along)
     held: Dict[Tuple[str, int], str] = {}
-    if params.slice_reserve_hold:
+    if params.slice_reserve_hold and (params.slice_reserve_hold_max_gpus <= 0
+                                      or len(sliced) <= params.slice_reserve_hold_max_gpus):
         for name, m in original.items():
             for og in m.gpus:
                 if getattr(og, "sliced", False) and og.target is not None and og.target_sliced:
