@@ -80,3 +80,40 @@ def test_fifo_planner_pairs_pods_past_the_skipped_count(waiting, placed):
     g = changed["n0"].gpus[0]
     # the pods the pass placed are "used" in the model; the third waits (7 would split again)
     assert g.used.get("16gb", 0) - 4 == placed and g.shared_count() == 6
+
+
+def _events(c, reason):
+    return [e for e in c.api.list("Event") if e.get("reason") == reason]
+
+
+def test_a_lone_fifth_memory_only_pod_waits_with_an_event_and_a_sixth_releases_both():
+    """End to end on the simulated cumask node: four memory-only pods run, a fifth waits with one
+    ``SharedSliceCountSkipped`` event on it (not one per pass), and a sixth arriving lets the planner
+    carve both slices at once."""
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=1, kind="cumask")
+    c.run(30)
+    for i in range(4):
+        c.submit({"amd.com/gpu-16gb": 1}, name=f"m{i}")
+    c.run(60)
+    assert len(c.running_pods()) == 4
+    c.submit({"amd.com/gpu-16gb": 1}, name="m4")
+    c.run(120)
+    assert len(c.running_pods()) == 4 and len(c.pending_pods()) == 1
+    ev = _events(c, "SharedSliceCountSkipped")
+    assert len(ev) == 1 and ev[0]["involvedObject"]["name"] == "m4" and "5 memory-only pods" in ev[0]["message"]
+    c.submit({"amd.com/gpu-16gb": 1}, name="m5")
+    c.run(120)
+    assert len(c.running_pods()) == 6 and not c.pending_pods()
+
+
+def test_slice_cap_wait_is_explained_once_per_pod():
+    from walkai_nos_amd.sim.cluster import SimCluster
+    c = SimCluster(n_nodes=1, gpus_per_node=1, kind="cumask")
+    c.run(30)
+    for i in range(9):
+        c.submit({"amd.com/gpu-8gb": 1}, name=f"m{i}")
+    c.run(240)
+    assert len(c.running_pods()) == 8
+    ev = _events(c, "SliceCapReached")
+    assert [e["involvedObject"]["name"] for e in ev] == ["m8"]

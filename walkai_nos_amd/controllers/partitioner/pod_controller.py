@@ -605,6 +605,7 @@ class PodController:
         self._window_start: Optional[float] = None
         self._window_last: Optional[float] = None
         self.plans_written = 0
+        self._explained: Dict[str, str] = {}     # pending pod uid -> the wait reason already recorded
         # (API revision, {request: result}) of read-only reconciles: see reconcile()
         self._idle: Tuple[Optional[int], Dict[Request, Result]] = (None, {})
 
@@ -657,6 +658,58 @@ class PodController:
             for k, v in requested_profiles(self.kind, p).items():
                 out[k] = out.get(k, 0) + v
         return out
+
+    def _explain_waits(self, models: Mapping[str, NodeModel]) -> None:
+        """CU-mask nodes: record once, as a Normal event on the pod, why a pending pod gets no
+        slice although a GPU has room for it — every GPU holds its slice cap
+        (``nos.nebuly.com/max-slices-per-gpu``), or the memory-only slice would make a count the
+        planner skips (``sharedSliceSkipCounts``: it waits for a second such pod or for a running one
+        to finish)."""
+        from ...models.slicing.profile import parse_profile
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if self.should_consider(p)]
+        live = {p["metadata"].get("uid") or "/".join(ko.key(p)) for p in pods}
+        self._explained = {k: v for k, v in self._explained.items() if k in live}
+        gpus = [g for m in models.values() for g in m.gpus]
+        for p in pods:
+            uid = p["metadata"].get("uid") or "/".join(ko.key(p))
+            req = requested_profiles(self.kind, p)
+            if uid in self._explained or len(req) != 1:
+                continue
+            (prof, q), = req.items()
+            if any(g.free.get(prof, 0) >= q for g in gpus):
+                continue   # a free slice waits for it: the scheduler binds it
+            reason = message = None
+            shared = not parse_profile(prof).dedicated
+            fits_unskipped = []
+            for g in gpus:
+                c = g.clone()
+                c.skip_shared = ()
+                fits_unskipped.append(c._can_create(prof, q))
+            if shared and any(fits_unskipped) and not any(g._can_create(prof, q) for g in gpus):
+                n = min(g.shared_count() + q for g, ok in zip(gpus, fits_unskipped) if ok)
+                reason, message = "SharedSliceCountSkipped", (
+                    f"no memory-only slice carved for {prof}: {n} memory-only pods on one GPU split into two rate "
+                    "classes by start order (sharedSliceSkipCounts); waiting for a second such pod or for a "
+                    "running one to finish")
+            elif gpus and all(g.slice_count() >= g.max_slices for g in gpus) and \
+                    any(g.spare_memory_gb() >= parse_profile(prof).memory_gb * q for g in gpus):
+                reason, message = "SliceCapReached", (
+                    f"every GPU holds its {gpus[0].max_slices} slices (one pod process each; past eight the hardware "
+                    "scheduler time-slices processes): label nos.nebuly.com/max-slices-per-gpu to allow more")
+            if reason is None:
+                continue
+            self._explained[uid] = reason
+            try:
+                self.client.create({
+                    "apiVersion": "v1", "kind": "Event",
+                    "metadata": {"generateName": f"{ko.name(p)}.", "namespace": ko.namespace(p)},
+                    "involvedObject": {"apiVersion": "v1", "kind": "Pod", "name": ko.name(p),
+                                       "namespace": ko.namespace(p), "uid": p["metadata"].get("uid", "")},
+                    "reason": reason, "message": message, "type": "Normal",
+                    "source": {"component": "nos-gpu-partitioner"}})
+            except Exception as e:  # noqa: BLE001 - an event is a courtesy
+                log.debug("event for %s not recorded: %s", uid, e)
 
     def _models(self, nodes: List[Dict[str, Any]]) -> Dict[str, NodeModel]:
         out: Dict[str, NodeModel] = {}
@@ -874,6 +927,8 @@ class PodController:
                 return Result()
             changed = plan_cluster(models, need)
         REGISTRY.phase_seconds.labels(phase="plan").observe(time.perf_counter() - t0)
+        if self.kind == api.PARTITIONING_KIND_CUMASK and req == self.plan_key and not changed:
+            self._explain_waits(models)   # a pass that could carve nothing: say why, once per pod
         if not changed:
             log.debug("%s: no node can provide %s now", req.name, need)
             return Result(requeue_after=self.retry_after)
