@@ -38,8 +38,9 @@ evicted. The signal is one-sided — a bypassing process with few waves per CU r
 never accuses a masked pod. Per GPU the guard also says whether the signal exists at all: a GPU
 busy for ``cu_probe_checks`` checks whose processes all read 0 (amd-smi without the KFD's
 occupancy, e.g. unprivileged) is ``unavailable``, never "clean". The processes' ``evicted_time``
-(queues time-sliced out by the hardware scheduler, the cost of more processes than hardware queue
-slots, ``profiles/procs_cap_r4.json``) is exported per pod.
+(queues switched out by the hardware scheduler) is exported per pod as reported; on the MI355X
+box it read 0 even for 10-12 pod processes that were visibly time-sliced
+(``profiles/fair_probe_r5_10_12.json``), so nothing is decided on it.
 """
 from __future__ import annotations
 
