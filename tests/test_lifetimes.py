@@ -1,0 +1,103 @@
+"""The planner's pod-lifetime model (``controllers/partitioner/lifetimes.py``): run times learned from
+the pods that finished, conditional residuals of running pods, the Monte Carlo cost of draining a
+GPU, the tracker's bookkeeping, and the sliced planner choosing its drain victim by that cost."""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+from walkai_nos_amd.controllers.partitioner.lifetimes import LifetimeModel, LifetimeTracker, drain_cost
+from walkai_nos_amd.kube import objects as ko
+
+
+def _model(values, window=256, min_samples=8):
+    m = LifetimeModel(window=window, min_samples=min_samples)
+    for v in values:
+        m.observe(v)
+    return m
+
+
+def test_model_quantiles_readiness_and_window():
+    m = _model([100.0, 200.0, 300.0, 400.0], min_samples=8)
+    assert not m.ready() and m.n == 4 and m.median() == 300.0 and m.quantile(0.0) == 100.0
+    m.observe(-5.0)                       # a non-positive run time is ignored
+    assert m.n == 4
+    m = _model(range(1, 11), window=4)    # the window keeps the last four observations
+    assert m.n == 4 and m.quantile(0.0) == 7 and m.quantile(1.0) == 10
+    assert LifetimeModel().median() is None
+
+
+def test_residuals_are_conditional_on_the_age():
+    m = _model([100.0, 200.0, 300.0, 400.0])
+    rng = random.Random(0)
+    # a pod that ran 250 s finishes at 300 or 400: its residual is 50 or 150, never negative
+    draws = {m.sample_residual(250.0, rng) for _ in range(200)}
+    assert draws == {50.0, 150.0}
+    assert m.expected_residual(250.0) == pytest.approx(100.0)
+    assert m.expected_residual(0.0) == pytest.approx(250.0)
+    # older than every observation: half its age again (at least a second)
+    assert m.sample_residual(1000.0, rng) == 500.0 and m.expected_residual(1.0 + 400.0) == pytest.approx(200.5)
+
+
+def test_drain_cost_basics():
+    m = _model([240.0] * 16)
+    assert drain_cost([(4, 10.0)], capacity=8, need=4, model=m) == (0.0, 0.0)   # room already there
+    # one pod of 8 groups, 100 s into a 240 s run: 140 s with nothing free
+    cost, wait = drain_cost([(8, 100.0)], capacity=8, need=8, model=m)
+    assert wait == pytest.approx(140.0) and cost == pytest.approx(0.0)
+    # two pods of 4: the first frees 4 groups that idle until the second ends
+    cost, wait = drain_cost([(4, 200.0), (4, 40.0)], capacity=8, need=8, model=m)
+    assert wait == pytest.approx(200.0) and cost == pytest.approx(4 * (200.0 - 40.0))
+    # deterministic for a seed, and a bigger need never costs less
+    m2 = _model([60.0, 120.0, 240.0, 360.0, 480.0] * 4)
+    pods = [(1, 30.0), (2, 100.0), (4, 10.0)]
+    assert drain_cost(pods, 8, 4, m2) == drain_cost(pods, 8, 4, m2)
+    assert drain_cost(pods, 8, 8, m2)[0] >= drain_cost(pods, 8, 4, m2)[0]
+
+
+def _pod(name, phase, start=None, finished=None, uid=None):
+    p = {"metadata": {"name": name, "namespace": "default", "uid": uid or name},
+         "status": {"phase": phase}}
+    if start is not None:
+        p["status"]["startTime"] = ko.now_rfc3339(start)
+    if finished is not None:
+        p["status"]["containerStatuses"] = [{"state": {"terminated": {"finishedAt": ko.now_rfc3339(finished)}}}]
+    return p
+
+
+def test_tracker_learns_run_times_from_finished_and_vanished_pods():
+    t = LifetimeTracker(_model([], min_samples=1))
+    ages = t.update([_pod("a", "Running", start=1000.0), _pod("b", "Running", start=1100.0)], now=1200.0)
+    assert ages == {"default/a": pytest.approx(200.0), "default/b": pytest.approx(100.0)}
+    # a finishes with a recorded finish time; b vanishes (deleted): its last-seen time counts
+    t.update([_pod("a", "Succeeded", start=1000.0, finished=1250.0)], now=1300.0)
+    assert sorted(t.model._sorted) == [pytest.approx(100.0), pytest.approx(250.0)]
+    assert t.update([], now=1400.0) == {} and t.model.n == 2
+
+
+def test_sliced_planner_drains_the_gpu_whose_pods_end_soonest():
+    """Two sliced GPUs, neither with room for a whole-GPU pod past its threshold. GPU 0 has fewer
+    groups in use but young pods; GPU 1 has more groups in use, all near the end of their run:
+    learned lifetimes make GPU 1 the cheaper drain (without them the planner would pick GPU 0)."""
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, plan_cluster_pack
+    from walkai_nos_amd.models.partitioned import PartitionedNode
+    from walkai_nos_amd.models.xcp import node as xcp_node
+    from walkai_nos_amd.models.xcp.slices import new_sliced_gpu
+
+    def node():
+        g0 = new_sliced_gpu("MI355X", 0, used={"qpx_nps1": 2}, free={"qpx_nps1": 2})
+        g1 = new_sliced_gpu("MI355X", 1, used={"qpx_nps1": 3}, free={"qpx_nps1": 1})
+        return PartitionedNode("n", [g0, g1], layout="slices", weight=xcp_node.fraction_weight,
+                               is_resource=lambda r: r.startswith("amd.com/"), as_resource=lambda p: "amd.com/" + p)
+
+    pods = {0: [(2, 10.0), (2, 20.0)], 1: [(2, 230.0), (2, 235.0), (2, 225.0)]}
+    life = _model([240.0] * 16)
+    p = PackParams(slice_reserve_after=900.0, slice_reserve_lifetimes=0.0, slice_free_drain=False)
+    pending = [({"spx_nps1": 1}, 1000.0)]
+    ch = plan_cluster_pack({"n": node()}, list(pending), params=p, pods_of=lambda n, g: pods[g], life=life)
+    targets = [g.target for g in ch["n"].gpus]
+    assert targets[1] is not None and targets[0] is None
+    ch = plan_cluster_pack({"n": node()}, list(pending), params=p)          # no lifetimes: fewest groups
+    targets = [g.target for g in ch["n"].gpus]
+    assert targets[0] is not None and targets[1] is None
