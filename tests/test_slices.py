@@ -369,3 +369,33 @@ def test_a_held_reservation_lapses_on_bigger_clusters():
     ch = plan_cluster_pack({"n": _sliced_node(draining(), *full)}, list(pending), params=p0)
     out = (ch.get("n") or _sliced_node(draining(), *full)).gpus[0]
     assert out.target == {"cpx_nps1": 3, "spx_nps1": 1}          # 0: held at any cluster size
+
+
+def test_free_drain_reserves_room_no_waiting_pod_fits():
+    """Every waiting pod is bigger than the GPU's unused room (one group): that room idles whatever
+    the planner does, so the oldest waiting pod reserves the GPU without waiting for its threshold."""
+    def run(free_drain):
+        g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 7}, free={"cpx_nps1": 1})
+        p = PackParams(slice_reserve_after=900.0, slice_free_drain=free_drain)
+        ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"dpx_nps1": 1}, 10.0)], params=p)
+        return ch["n"].gpus[0].target if "n" in ch else None
+    assert run(True) == {"cpx_nps1": 7, "dpx_nps1": 1}
+    assert run(False) is None
+
+
+def test_reservation_threshold_in_learned_lifetimes():
+    from walkai_nos_amd.controllers.partitioner.lifetimes import LifetimeModel
+    life = LifetimeModel(min_samples=1)
+    for _ in range(8):
+        life.observe(100.0)
+    p = PackParams(slice_reserve_after=900.0, slice_reserve_lifetimes=3.75, slice_reserve_backlog=0.0,
+                   slice_free_drain=False)
+
+    def target(age, learned):
+        g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 3}, free={"cpx_nps1": 5})
+        ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"spx_nps1": 1}, age)], params=p,
+                               pods_of=lambda n, i: [(1, 50.0)] * 3, life=life if learned else None)
+        return ch["n"].gpus[0].target if "n" in ch else None
+    assert target(400.0, True) is not None        # 3.75 x the 100 s median = 375 s
+    assert target(300.0, True) is None
+    assert target(400.0, False) is None           # not learned: the 900 s constant
