@@ -685,8 +685,8 @@ class PodController:
             for g in gpus:
                 c = g.clone()
                 c.skip_shared = ()
-                fits_unskipped.append(c._can_create(prof, q))
-            if shared and any(fits_unskipped) and not any(g._can_create(prof, q) for g in gpus):
+                fits_unskipped.append(c.can_create(prof, q))
+            if shared and any(fits_unskipped) and not any(g.can_create(prof, q) for g in gpus):
                 n = min(g.shared_count() + q for g, ok in zip(gpus, fits_unskipped) if ok)
                 reason, message = "SharedSliceCountSkipped", (
                     f"no memory-only slice carved for {prof}: {n} memory-only pods on one GPU split into two rate "

@@ -103,6 +103,11 @@ class SlicingGPU:
     def can_create_more_slices(self) -> bool:
         return self.spare_memory_gb() >= MIN_SLICE_MEMORY_GB and self.slice_count() < self.max_slices
 
+    def can_create(self, profile: str, num: int = 1) -> bool:
+        """Whether ``num`` more slices of ``profile`` fit (memory, CUs, the slice cap, skipped
+        memory-only counts)."""
+        return self._can_create(profile, num)
+
     def _can_create(self, profile: str, num: int = 1) -> bool:
         prof = parse_profile(profile)
         if self.spare_memory_gb() < prof.memory_gb * num or self.slice_count() + num > self.max_slices:
