@@ -123,22 +123,25 @@ def test_partitioner_and_agent_processes_flip_drain_and_flip_back():
             c.stop()
 
 
-def test_sliced_gpu_runs_cpx_and_dpx_pods_at_once_over_processes():
+@pytest.mark.parametrize("layout", ["slices", None])
+def test_sliced_gpu_runs_cpx_and_dpx_pods_at_once_over_processes(layout):
     """VERDICT r3 #1 (mixed geometry): the real partitioner and partition agent processes on a
-    1-GPU node labelled ``nos.nebuly.com/xcp-layout=slices``. A 1/2 pod and two 1/8 pods run on the
-    one GPU at the same time, on disjoint CU masks handed out by the plugin's ``Allocate``, with no
-    amd-smi switch; a 1/4 pod is then re-carved in next to them (no drain); when they finish, a
-    whole-GPU pod takes the GPU."""
+    1-GPU node labelled ``nos.nebuly.com/xcp-layout=slices`` — or carrying no layout label at all
+    (the partitioner's ``defaultXcpLayout``, slices). A 1/2 pod and two 1/8 pods run on the one GPU
+    at the same time, on disjoint CU masks handed out by the plugin's ``Allocate``, with no amd-smi
+    switch; a 1/4 pod is then re-carved in next to them (no drain); when they finish, a whole-GPU
+    pod takes the GPU."""
     import json
     from walkai_nos_amd.api import v1alpha1 as api
     from walkai_nos_amd.cmd.devcluster import fast_partitioner_config
     from walkai_nos_amd.models.slicing.cumask import XCDS
     with tempfile.TemporaryDirectory() as d:
-        c = DevCluster(d, nodes=1, gpus=1, bookmark_every=2.0, layout="slices",
+        c = DevCluster(d, nodes=1, gpus=1, bookmark_every=2.0, layout=layout,
                        partitioner=fast_partitioner_config(sliceReserveAfterSeconds=1))
         try:
             c.start()
             kubelet = c.kubelets[NODE]
+            assert (api.LABEL_XCP_LAYOUT in ko.labels(c.client.get("Node", NODE))) == (layout is not None)
             c.run_until(lambda: ko.annotations(c.client.get("Node", NODE)).get(api.ANNOTATION_SLICED_GPUS_STATUS) == "0",
                         30, "the GPU to be served sliced")
             c.submit("half", "dpx_nps1")

@@ -45,11 +45,13 @@ REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 def node_labels(gpus: int, model: str = "MI355X", kind: str = api.PARTITIONING_KIND_XCP,
-                layout: str = "partitions") -> Dict[str, str]:
+                layout: Optional[str] = "partitions") -> Dict[str, str]:
+    """Labels of a fake MI355X node; ``layout`` None leaves ``nos.nebuly.com/xcp-layout`` off (the
+    partitioner's ``defaultXcpLayout`` applies)."""
     out = {api.LABEL_GPU_PARTITIONING: kind,
            constant.LABEL_AMD_GPU_PRODUCT: f"AMD_Instinct_{model}", constant.LABEL_AMD_GPU_COUNT: str(gpus),
            constant.LABEL_AMD_GPU_VRAM: "288G", constant.LABEL_AMD_GPU_CU_COUNT: "256"}
-    if kind == api.PARTITIONING_KIND_XCP:     # explicit: the partitioner's default layout is slices
+    if kind == api.PARTITIONING_KIND_XCP and layout is not None:   # explicit (the default is slices)
         out[api.LABEL_XCP_LAYOUT] = layout
     return out
 
@@ -66,7 +68,7 @@ class DevCluster:
     def __init__(self, root: str, nodes: int = 1, gpus: int = 1,
                  partitioner: Optional[GpuPartitionerConfig] = None, report_interval: float = 1.0,
                  bookmark_every: float = 5.0, amd_smi_backend: str = "fake", quota: bool = False,
-                 kind: str = api.PARTITIONING_KIND_XCP, layout: str = "partitions"):
+                 kind: str = api.PARTITIONING_KIND_XCP, layout: Optional[str] = "partitions"):
         self.root = root
         self.n_nodes, self.gpus = nodes, gpus
         self.partitioner_cfg = partitioner or fast_partitioner_config()
@@ -263,12 +265,16 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--quota", action="store_true", help="also run nos-operator and nos-scheduler")
     ap.add_argument("--kind", default=api.PARTITIONING_KIND_XCP, choices=api.PARTITIONING_KINDS,
                     help="xcp: compute partitions (partition agents); cumask: CU-mask slices (slice agents)")
+    ap.add_argument("--layout", default="partitions", choices=("partitions", "slices", "auto", "default"),
+                    help="xcp nodes' nos.nebuly.com/xcp-layout label (default: no label, the partitioner's "
+                         "defaultXcpLayout); the demo shows the flips of hardware partitions")
     ap.add_argument("--log-level", default="info")
     a = ap.parse_args(argv)
     logging.basicConfig(level=getattr(logging, a.log_level.upper(), logging.INFO))
     root = a.dir or tempfile.mkdtemp(prefix="nos-devcluster-")
     os.makedirs(root, exist_ok=True)
-    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus, quota=a.quota, kind=a.kind).start()
+    c = DevCluster(root, nodes=a.nodes, gpus=a.gpus, quota=a.quota, kind=a.kind,
+                   layout=None if a.layout == "default" else a.layout).start()
     print(f"nos dev cluster: {a.nodes} node(s) x {a.gpus} GPU(s); KUBECONFIG={c.kubeconfig}; logs in {root}",
           flush=True)
     try:
