@@ -348,9 +348,10 @@ def test_default_layout_of_unlabelled_nodes_comes_from_the_partitioner_config():
 
 def test_a_held_reservation_lapses_on_bigger_clusters():
     """``slice_reserve_hold_max_gpus``: a drain in progress keeps its target until a pod of its profile
-    is placed while the cluster has at most two sliced GPUs; with more, it is re-decided each pass
-    (here: the whole-GPU pod is not overdue, so the draining GPU takes the small pod again)."""
-    p = PackParams(slice_reserve_after=900.0)
+    is placed while the cluster has at most that many sliced GPUs; with more, it is re-decided each
+    pass (here: the whole-GPU pod is not overdue, so the draining GPU takes the small pod again).
+    The default (0) holds at any cluster size."""
+    p = PackParams(slice_reserve_after=900.0, slice_reserve_hold_max_gpus=2)
 
     def draining():
         g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 3})
@@ -365,7 +366,7 @@ def test_a_held_reservation_lapses_on_bigger_clusters():
     ch = plan_cluster_pack({"n": _sliced_node(draining(), *full)}, list(pending), params=p)
     out = ch["n"].gpus[0]
     assert out.target is None and out.used.get("cpx_nps1", 0) + out.free.get("cpx_nps1", 0) >= 4
-    p0 = PackParams(slice_reserve_after=900.0, slice_reserve_hold_max_gpus=0)
+    p0 = PackParams(slice_reserve_after=900.0)
     ch = plan_cluster_pack({"n": _sliced_node(draining(), *full)}, list(pending), params=p0)
     out = (ch.get("n") or _sliced_node(draining(), *full)).gpus[0]
     assert out.target == {"cpx_nps1": 3, "spx_nps1": 1}          # 0: held at any cluster size
@@ -399,3 +400,55 @@ def test_reservation_threshold_in_learned_lifetimes():
     assert target(400.0, True) is not None        # 3.75 x the 100 s median = 375 s
     assert target(300.0, True) is None
     assert target(400.0, False) is None           # not learned: the 900 s constant
+
+
+def test_no_reservation_that_only_its_own_profile_blocks():
+    """A whole-GPU pod never reserves a GPU another whole-GPU pod runs on: nothing idles while that
+    pod runs and its slice goes to the next whole-GPU pod anyway, but the plugin would withhold the
+    slice in use, and kube-scheduler (its request counted, the device not) would stop seeing the
+    node's other free whole-GPU slices. With learned lifetimes that GPU is the cheapest drain (no
+    group idles), so it was the one picked; a held reservation of it lapses too."""
+    from walkai_nos_amd.controllers.partitioner.lifetimes import LifetimeModel
+    life = LifetimeModel(min_samples=1)
+    for _ in range(8):
+        life.observe(240.0)
+    p = PackParams(slice_reserve_after=900.0, slice_reserve_lifetimes=0.0, slice_free_drain=False)
+    pods = {0: [(8, 200.0)], 1: [(1, 10.0)] * 3}
+    pending = [({"spx_nps1": 1}, 1000.0)]
+
+    def node(held=False):
+        g0 = new_sliced_gpu("MI355X", 0, used={"spx_nps1": 1})
+        if held:
+            g0.target, g0.target_sliced = {"spx_nps1": 2}, True
+        return _sliced_node(g0, new_sliced_gpu("MI355X", 1, used={"cpx_nps1": 3}, free={"cpx_nps1": 5}))
+
+    for held in (False, True):
+        ch = plan_cluster_pack({"n": node(held)}, list(pending), params=p, pods_of=lambda n, g: pods[g], life=life)
+        targets = [g.target for g in ch["n"].gpus]
+        assert targets[0] is None and targets[1] == {"cpx_nps1": 3, "spx_nps1": 1}
+    # a half-GPU pod may still reserve the other half of a GPU a half-GPU pod runs on
+    g = new_sliced_gpu("MI355X", 0, used={"dpx_nps1": 1, "cpx_nps1": 2}, free={"cpx_nps1": 2})
+    ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"dpx_nps1": 1}, 1000.0)], params=p)
+    assert ch["n"].gpus[0].target == {"dpx_nps1": 2, "cpx_nps1": 2}
+
+
+def test_free_drain_wait_grows_with_the_gpus_up_to_a_cap():
+    """The wait before a free drain is ``sliceFreeDrainAfterLifetimes`` per other sliced GPU (with more
+    GPUs one empties on its own sooner), capped at ``sliceFreeDrainCapLifetimes``: eight GPUs whose
+    one free group no waiting pod fits idle 1/8 of the cluster until a drain starts."""
+    from walkai_nos_amd.controllers.partitioner.lifetimes import LifetimeModel
+    life = LifetimeModel(min_samples=1)
+    for _ in range(8):
+        life.observe(100.0)
+
+    def drains(cap, age):
+        gpus = [new_sliced_gpu("MI355X", i, used={"cpx_nps1": 7}, free={"cpx_nps1": 1}) for i in range(8)]
+        p = PackParams(slice_reserve_after=900.0, slice_reserve_lifetimes=0.0, slice_free_drain_cap=cap)
+        ch = plan_cluster_pack({"n": _sliced_node(*gpus)}, [({"dpx_nps1": 1}, age)], params=p,
+                               pods_of=lambda n, g: [(1, 50.0)] * 7, life=life)
+        return sum(1 for g in ch["n"].gpus if g.target is not None) if "n" in ch else 0
+    assert drains(0.75, 80.0) == 1          # 0.5 x 7 = 3.5 lifetimes, capped at 0.75 = 75 s
+    assert drains(0.75, 70.0) == 0
+    assert drains(0.0, 80.0) == 0           # uncapped: 350 s
+    assert drains(0.0, 360.0) == 1
+

@@ -198,10 +198,11 @@ class PackParams:
     slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
     slice_reserve_stretch: float = 2.0  # ... at most this many times
     slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed ...
-    slice_reserve_hold_max_gpus: int = 2  # ... on clusters of at most this many sliced GPUs (0 = any size): with
-                                    # more, another GPU empties soon enough and a held drain idles capacity
+    slice_reserve_hold_max_gpus: int = 0  # ... on clusters of at most this many sliced GPUs (0 = any size; 4 GPUs
+                                    # over 8 seeds x 200 quanta: 96.3% with holds, 94.5% without, one seed 78%)
     slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
     slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
+    slice_free_drain_cap: float = 0.75  # ... but at most this many (0 = no cap)
     slice_whole_overtake: float = 960.0  # seconds: a whole-GPU slice left free goes to the next whole-GPU pod
                                     # unless the oldest waiting pod is this much older (0 = strict FIFO)
     slice_whole_overtake_lifetimes: float = 4.0  # ... this many median pod run times once learned (0 = constant)

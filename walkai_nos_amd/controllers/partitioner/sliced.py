@@ -139,6 +139,16 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     by_key = {(name, g.index): g for name, g in sliced}
     name_of = {id(g): name for name, g in sliced}
 
+    def futile(name: str, g: Any, p: str, q: int) -> bool:
+        """A drain of ``g`` for ``q`` slices of ``p`` that only its own ``p`` pods block: the slices of
+        ``p`` in use leave no room for them even once every other pod has left (a whole-GPU pod
+        reserving a GPU another whole-GPU pod runs on). Such a drain idles nothing while they run
+        and gains nothing when they end (their free slice goes to the next pod of ``p`` anyway), but
+        the plugin withholds those slices in use, and kube-scheduler, which counts their requests
+        against a node allocatable without them, stops seeing the free ``p`` slices of the node's
+        other GPUs for as long as it lasts."""
+        return groups_of(p) * (used_now.get((name, g.index), {}).get(p, 0) + q) > g.capacity
+
     def reserve(name: str, g: Any, p: str, q: int) -> None:
         """Drain ``g`` for ``q`` slices of ``p``: its spec becomes the slices in use plus those."""
         want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
@@ -190,7 +200,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
             unserved.remove((req, age))
             continue
         hk = next((k for k in sorted(held) if held[k] == p and claimed.get(k, -1.0) < age and by_key.get(k) is not None
-                   and by_key[k].target is None), None)
+                   and by_key[k].target is None and not futile(k[0], by_key[k], p, q)), None)
         if hk is not None:
             reserve(hk[0], by_key[hk], p, q)
             continue
@@ -198,7 +208,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
             waiting.append((req, age))
             continue
         victims = [(bool(g.degraded), drain_key(name, g, need), name, g.index, g) for name, g in sliced
-                   if g.target is None and claimed.get((name, g.index), -1.0) < age]
+                   if g.target is None and claimed.get((name, g.index), -1.0) < age and not futile(name, g, p, q)]
         if not victims and any(g.target is None for _, g in sliced):
             waiting.append((req, age))
             continue  # every sliced GPU just took an older pod: reconsider on the next pass
@@ -224,7 +234,10 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         draining = {max((x for x, n in g.target.items() if n > g.used.get(x, 0)), key=groups_of, default=None)
                     for _, g in sliced if g.target is not None}
         # with more GPUs one empties on its own sooner: the wait before a free drain scales with them
-        free_after = params.slice_free_drain_after * (median if learned else 240.0) * max(0, len(sliced) - 1)
+        per = params.slice_free_drain_after * max(0, len(sliced) - 1)
+        if params.slice_free_drain_cap > 0:
+            per = min(per, params.slice_free_drain_cap)
+        free_after = per * (median if learned else 240.0)
         for req, age in waiting:
             p, q = _single(req)
             if p in draining or age < free_after:
