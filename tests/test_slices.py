@@ -452,3 +452,12 @@ def test_free_drain_wait_grows_with_the_gpus_up_to_a_cap():
     assert drains(0.0, 80.0) == 0           # uncapped: 350 s
     assert drains(0.0, 360.0) == 1
 
+
+
+def test_a_pod_of_several_slices_may_reserve_a_gpu_its_profile_fills():
+    """Two cpx slices for one pod on a GPU full of one-slice cpx pods: each slice those pods free goes
+    to a one-slice pod unless the GPU is reserved, so the reservation is kept."""
+    p = PackParams(slice_reserve_after=900.0, slice_free_drain=False)
+    g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 8})
+    ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"cpx_nps1": 2}, 1000.0)], params=p)
+    assert ch["n"].gpus[0].target == {"cpx_nps1": 10}

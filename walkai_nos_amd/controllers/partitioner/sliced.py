@@ -140,14 +140,15 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     name_of = {id(g): name for name, g in sliced}
 
     def futile(name: str, g: Any, p: str, q: int) -> bool:
-        """A drain of ``g`` for ``q`` slices of ``p`` that only its own ``p`` pods block: the slices of
-        ``p`` in use leave no room for them even once every other pod has left (a whole-GPU pod
+        """A drain of ``g`` for one slice of ``p`` that only its own ``p`` pods block: the slices of
+        ``p`` in use leave no room for another even once every other pod has left (a whole-GPU pod
         reserving a GPU another whole-GPU pod runs on). Such a drain idles nothing while they run
-        and gains nothing when they end (their free slice goes to the next pod of ``p`` anyway), but
-        the plugin withholds those slices in use, and kube-scheduler, which counts their requests
-        against a node allocatable without them, stops seeing the free ``p`` slices of the node's
-        other GPUs for as long as it lasts."""
-        return groups_of(p) * (used_now.get((name, g.index), {}).get(p, 0) + q) > g.capacity
+        and gains nothing when one ends (its free slice is what the pod needs, and kube-scheduler
+        binds the oldest pod of ``p`` to it anyway), but the plugin withholds those slices in use,
+        and kube-scheduler, which counts their requests against a node allocatable without them,
+        stops seeing the free ``p`` slices of the node's other GPUs for as long as it lasts. A pod
+        of several slices does need the drain: one freed slice would go to a one-slice pod."""
+        return q == 1 and groups_of(p) * (used_now.get((name, g.index), {}).get(p, 0) + 1) > g.capacity
 
     def reserve(name: str, g: Any, p: str, q: int) -> None:
         """Drain ``g`` for ``q`` slices of ``p``: its spec becomes the slices in use plus those."""
