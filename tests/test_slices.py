@@ -261,6 +261,10 @@ def test_whole_gpu_pod_gets_the_sliced_gpu_through_a_reservation():
     assert ko.pod_node_name(c.api.get("Pod", "big", "default")) == "node-0"
     assert [ko.name(p) for p in c.running_pods()] == ["big"]
     assert c.nodes["node-0"].smi.set_calls == [] and c.admission_failures == 0
+    # the pod the GPU drained for was told so, once (then "late", overdue behind it, reserves it next)
+    ev = [e for e in c.api.list("Event") if e.get("reason") == "SlicedGPUReserved"]
+    assert [e["involvedObject"]["name"] for e in ev] == ["big", "late"]
+    assert "GPU 0 of node node-0 is draining for this pod's spx_nps1 slice: 4 pods still run" in ev[0]["message"]
 
 
 def test_slices_node_turns_an_idle_hardware_gpu_into_a_sliced_one():

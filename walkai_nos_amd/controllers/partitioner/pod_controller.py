@@ -701,16 +701,53 @@ class PodController:
             if reason is None:
                 continue
             self._explained[uid] = reason
-            try:
-                self.client.create({
-                    "apiVersion": "v1", "kind": "Event",
-                    "metadata": {"generateName": f"{ko.name(p)}.", "namespace": ko.namespace(p)},
-                    "involvedObject": {"apiVersion": "v1", "kind": "Pod", "name": ko.name(p),
-                                       "namespace": ko.namespace(p), "uid": p["metadata"].get("uid", "")},
-                    "reason": reason, "message": message, "type": "Normal",
-                    "source": {"component": "nos-gpu-partitioner"}})
-            except Exception as e:  # noqa: BLE001 - an event is a courtesy
-                log.debug("event for %s not recorded: %s", uid, e)
+            self._event(p, reason, message)
+
+    def _event(self, pod: Dict[str, Any], reason: str, message: str) -> None:
+        try:
+            self.client.create({
+                "apiVersion": "v1", "kind": "Event",
+                "metadata": {"generateName": f"{ko.name(pod)}.", "namespace": ko.namespace(pod)},
+                "involvedObject": {"apiVersion": "v1", "kind": "Pod", "name": ko.name(pod),
+                                   "namespace": ko.namespace(pod), "uid": pod["metadata"].get("uid", "")},
+                "reason": reason, "message": message, "type": "Normal",
+                "source": {"component": "nos-gpu-partitioner"}})
+        except Exception as e:  # noqa: BLE001 - an event is a courtesy
+            log.debug("event for %s not recorded: %s", ko.name(pod), e)
+
+    def _explain_reservations(self, models: Mapping[str, NodeModel], changed: Mapping[str, NodeModel]) -> None:
+        """Sliced GPUs: when a pass starts draining a GPU for a pod (a reservation: the spec asks for
+        the slices in use plus one that does not fit yet), record it once as a Normal event on the
+        oldest pending pod of that profile, with what still runs there — the pod is waiting for that
+        GPU to empty, and no new pod is placed on it meanwhile."""
+        from ...models.xcp.slices import groups_of
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Pending", copy=False)
+                if self.should_consider(p)]
+        pods.sort(key=lambda p: (-podutil.priority(p), p["metadata"].get("creationTimestamp", ""), ko.name(p)))
+        live = {p["metadata"].get("uid") or "/".join(ko.key(p)) for p in pods}
+        self._explained = {k: v for k, v in self._explained.items() if k in live}
+        for name, m in sorted(changed.items()):
+            before = {g.index: g for g in getattr(models.get(name), "gpus", [])}
+            for g in m.gpus:
+                if not getattr(g, "sliced", False) or g.target is None or not g.target_sliced:
+                    continue
+                old = before.get(g.index)
+                if old is not None and old.target == g.target:
+                    continue   # a drain already in force
+                extra = [x for x, n in g.target.items() if n > g.used.get(x, 0)]
+                if not extra:
+                    continue
+                prof = max(extra, key=lambda x: (groups_of(x), x))
+                for p in pods:
+                    uid = p["metadata"].get("uid") or "/".join(ko.key(p))
+                    if uid in self._explained or set(requested_profiles(self.kind, p)) != {prof}:
+                        continue
+                    running = sum(n for n in g.used.values() if n > 0)
+                    self._explained[uid] = "SlicedGPUReserved"
+                    self._event(p, "SlicedGPUReserved",
+                                f"GPU {g.index} of node {name} is draining for this pod's {prof} slice: {running} "
+                                "pods still run on it, and no new pod is placed there until the slice fits")
+                    break
 
     def _models(self, nodes: List[Dict[str, Any]]) -> Dict[str, NodeModel]:
         out: Dict[str, NodeModel] = {}
@@ -933,6 +970,9 @@ class PodController:
         if not changed:
             log.debug("%s: no node can provide %s now", req.name, need)
             return Result(requeue_after=self.retry_after)
+        if self.kind == api.PARTITIONING_KIND_XCP and any(getattr(m, "sliced", False) for c in changed.values()
+                                                          for m in c.gpus):
+            self._explain_reservations(models, changed)
         by_name = {ko.name(n): n for n in nodes}
         for name, model in changed.items():
             plan_id = new_plan_id(self.clock)
