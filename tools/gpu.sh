@@ -13,6 +13,7 @@
 #   bench_torch        bench.py on the PyTorch (hipBLASLt) backend, for comparison
 #   seeds              the bench window over churn seeds 1-5 and 1234 (NOS_SEEDS overrides)
 #   operator           tools/operator_gpu_report.py: device map, commit barrier, probes
+#   pod_start          tools/pod_start_probe.py: a pod process's boot phase by phase (1/8-GPU slice)
 #   multiproc          tools/multiproc.py: pods as separate processes (sharing table, config 3)
 #   curve              tools/sharing_curve.py: thread-emulated 1/3/5/7 sharing curve
 #   prof               rocprofv3 kernel trace + stats of a short bench run
@@ -76,6 +77,7 @@ for s in "$@"; do
         step "seed_$seed" 300 python bench.py --no-density --seed "$seed" --out "$OUT/seeds/b_$seed.json"
       done ;;
     operator) step operator 600 python tools/operator_gpu_report.py --out "$OUT/operator.json" ;;
+    pod_start) step pod_start 400 python tools/pod_start_probe.py --runs 3 --out "$OUT/pod_start_probe.json" ;;
     multiproc) step multiproc 900 python tools/multiproc.py --out "$OUT/multiproc.json" ${NOS_MP_ARGS:-} ;;
     curve) step sharing_curve 500 python tools/sharing_curve.py --seconds 4 --out "$OUT/sharing_curve.json" ;;
     prof)
