@@ -15,7 +15,7 @@
 //    across the query tiles of that head. The production launch is stream-K (attn_fwd_sk): a
 //    persistent grid sized to the slice's resident-wave capacity splits the (query tile x key
 //    block) work evenly, so a 32-CU CPX slice and the whole 256-CU GPU are both tail-free.
-//  * layernorm_f32: one wave per row, values kept in registers (two-pass mean/variance), wave64
+//  * layernorm_f32: two rows per wave in flight, values kept in registers (two-pass mean/variance), wave64
 //    shuffles; writes fp32 or the x3 planes the next GEMM consumes.
 //  * bias_gelu_f32: in-place exact (erf) GELU(y + b) epilogue, dwordx4 vectorised.
 #include <hip/hip_runtime.h>
@@ -25,6 +25,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
@@ -76,8 +77,10 @@ __device__ __forceinline__ void store_x3(__bf16* __restrict__ y, size_t plane, s
 // ------------------------------------------------------------------------------------------
 // LayerNorm (output fp32 y, or x3 planes yp with plane stride rows*D when yp != nullptr). Lane l
 // owns the column pairs (2l + 128i, 2l + 128i + 1): 8-B loads, and packed 4-B bf16-pair stores per
-// plane on the x3 path.
-template <int NPL>
+// plane on the x3 path. R rows per wave per iteration, all R loaded before any is reduced: a slice
+// sharing the GPU runs a few waves per CU over many rows each, and each iteration is one memory
+// round trip, so R rows in flight cut the round trips per wave by R.
+template <int NPL, int R>
 __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x, const float* __restrict__ w,
                                                      const float* __restrict__ b, float* __restrict__ y,
                                                      __bf16* __restrict__ yp, int rows, float eps, unsigned pin) {
@@ -88,49 +91,65 @@ __global__ __launch_bounds__(256) void layernorm_f32(const float* __restrict__ x
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const float2* w2 = reinterpret_cast<const float2*>(w);
   const float2* b2 = reinterpret_cast<const float2*>(b);
+  const size_t plane2 = size_t(rows) * D / 2;  // plane stride in bf16 pairs
   // grid-stride over rows: a slice sharing the GPU launches a few workgroups per CU instead of one
-  // per 4 rows (workgroup dispatch is what concurrent partitions contend for)
-  for (int row = pb.id * 4 + wave; row < rows; row += pb.n * 4) {
-  const float2* xr = reinterpret_cast<const float2*>(x + size_t(row) * D);
-  float2 v[NP];
-  float s = 0.f;
+  // per 4R rows (workgroup dispatch is what concurrent partitions contend for)
+  const int stride = pb.n * 4;
+  for (int row0 = pb.id * 4 + wave; row0 < rows; row0 += R * stride) {
+    float2 v[R][NP];
+    float mean[R], rstd[R];
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    v[i] = xr[i * 64 + lane];
-    s += v[i].x + v[i].y;
-  }
-  const float mean = wave_sum(s) * (1.0f / D);
-  float q = 0.f;
+    for (int k = 0; k < R; ++k) {
+      // rows past the end re-read the last row (in bounds) and are never stored
+      const float2* xr = reinterpret_cast<const float2*>(x + size_t(min(row0 + k * stride, rows - 1)) * D);
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    v[i].x -= mean;
-    v[i].y -= mean;
-    q += v[i].x * v[i].x + v[i].y * v[i].y;
-  }
-  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
-  if (yp) {
-    const size_t plane2 = size_t(rows) * D / 2;  // plane stride in bf16 pairs
-    uint32_t* dst = reinterpret_cast<uint32_t*>(yp) + size_t(row) * (D / 2);
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int c2 = i * 64 + lane;
-      const float2 ww = w2[c2], bb = b2[c2];
-      const f32x2 val = {v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y};
-      bf16x2 h0, h1, h2;
-      split3(val, h0, h1, h2);
-      dst[c2] = __builtin_bit_cast(uint32_t, h0);
-      dst[plane2 + c2] = __builtin_bit_cast(uint32_t, h1);
-      dst[2 * plane2 + c2] = __builtin_bit_cast(uint32_t, h2);
+      for (int i = 0; i < NP; ++i) v[k][i] = xr[i * 64 + lane];
     }
-    continue;
-  }
-  float2* yr = reinterpret_cast<float2*>(y + size_t(row) * D);
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int c2 = i * 64 + lane;
-    const float2 ww = w2[c2], bb = b2[c2];
-    yr[c2] = make_float2(v[i].x * rstd * ww.x + bb.x, v[i].y * rstd * ww.y + bb.y);
-  }
+    for (int k = 0; k < R; ++k) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) s += v[k][i].x + v[k][i].y;
+      mean[k] = wave_sum(s) * (1.0f / D);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        v[k][i].x -= mean[k];
+        v[k][i].y -= mean[k];
+        q += v[k][i].x * v[k][i].x + v[k][i].y * v[k][i].y;
+      }
+      rstd[k] = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int row = row0 + k * stride;
+      if (row >= rows) break;
+      if (yp) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(yp) + size_t(row) * (D / 2);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int c2 = i * 64 + lane;
+          const float2 ww = w2[c2], bb = b2[c2];
+          const f32x2 val = {v[k][i].x * rstd[k] * ww.x + bb.x, v[k][i].y * rstd[k] * ww.y + bb.y};
+          bf16x2 h0, h1, h2;
+          split3(val, h0, h1, h2);
+          dst[c2] = __builtin_bit_cast(uint32_t, h0);
+          dst[plane2 + c2] = __builtin_bit_cast(uint32_t, h1);
+          dst[2 * plane2 + c2] = __builtin_bit_cast(uint32_t, h2);
+        }
+      } else {
+        float2* yr = reinterpret_cast<float2*>(y + size_t(row) * D);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int c2 = i * 64 + lane;
+          const float2 ww = w2[c2], bb = b2[c2];
+          yr[c2] = make_float2(v[k][i].x * rstd[k] * ww.x + bb.x, v[k][i].y * rstd[k] * ww.y + bb.y);
+        }
+      }
+    }
   }
 }
 
@@ -1640,20 +1659,33 @@ int nos_layernorm_f32_grid(const float* x, const float* w, const float* b, float
   }
   if (rows <= 0) return 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int full = (rows + 3) / 4;
+  // rows in flight per wave (NOS_LN_ROWS, 1 or 2; read once)
+  static const int R = [] {
+    const char* e = std::getenv("NOS_LN_ROWS");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  const int full = (rows + 4 * R - 1) / (4 * R);
   const dim3 grid(pinned_grid(pinned_cap(wgs > 0 ? std::min(wgs, full) : full, g_pin), g_pin)), block(256);
   __bf16* p = reinterpret_cast<__bf16*>(yp);
   const unsigned pin = g_pin;
+#define NOS_LN_CASE(DD, NPL)                                                                      \
+  case DD:                                                                                        \
+    if (R == 2)                                                                                   \
+      hipLaunchKernelGGL((layernorm_f32<NPL, 2>), grid, block, 0, s, x, w, b, y, p, rows, eps, pin); \
+    else                                                                                          \
+      hipLaunchKernelGGL((layernorm_f32<NPL, 1>), grid, block, 0, s, x, w, b, y, p, rows, eps, pin); \
+    break;
   switch (D) {
-    case 384: hipLaunchKernelGGL(layernorm_f32<6>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
-    case 768: hipLaunchKernelGGL(layernorm_f32<12>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
-    case 1024: hipLaunchKernelGGL(layernorm_f32<16>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
-    case 1536: hipLaunchKernelGGL(layernorm_f32<24>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
-    case 2048: hipLaunchKernelGGL(layernorm_f32<32>, grid, block, 0, s, x, w, b, y, p, rows, eps, pin); break;
+    NOS_LN_CASE(384, 6)
+    NOS_LN_CASE(768, 12)
+    NOS_LN_CASE(1024, 16)
+    NOS_LN_CASE(1536, 24)
+    NOS_LN_CASE(2048, 32)
     default:
       g_err = "layernorm: unsupported hidden size " + std::to_string(D);
       return -1;
   }
+#undef NOS_LN_CASE
   return check_launch("layernorm_f32");
 }
 
