@@ -101,3 +101,29 @@ def test_sliced_planner_drains_the_gpu_whose_pods_end_soonest():
     ch = plan_cluster_pack({"n": node()}, list(pending), params=p)          # no lifetimes: fewest groups
     targets = [g.target for g in ch["n"].gpus]
     assert targets[0] is not None and targets[1] is None
+
+
+def test_drain_victim_avoids_hiding_slices_pods_wait_for():
+    """On a node of several sliced GPUs a drain withholds its slices in use, and kube-scheduler, which
+    still counts their pods, sees as many fewer free slices of those profiles on the node. GPU 0's
+    eight 1/8 pods end sooner than GPU 1's four 1/4 pods, but 1/8 pods are waiting: with the strand
+    weight the drain goes to GPU 1 (whose profile nobody waits for)."""
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams, plan_cluster_pack
+    from walkai_nos_amd.models.partitioned import PartitionedNode
+    from walkai_nos_amd.models.xcp import node as xcp_node
+    from walkai_nos_amd.models.xcp.slices import new_sliced_gpu
+
+    def node():
+        g0 = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 8})
+        g1 = new_sliced_gpu("MI355X", 1, used={"qpx_nps1": 4})
+        return PartitionedNode("n", [g0, g1], layout="slices", weight=xcp_node.fraction_weight,
+                               is_resource=lambda r: r.startswith("amd.com/"), as_resource=lambda p: "amd.com/" + p)
+
+    pods = {0: [(1, 200.0)] * 8, 1: [(2, 150.0)] * 4}
+    life = _model([240.0] * 16)
+    pending = [({"spx_nps1": 1}, 1000.0), ({"cpx_nps1": 1}, 10.0)]
+    for w, want in ((0.0, [True, False]), (1.0, [False, True])):
+        p = PackParams(slice_reserve_after=900.0, slice_reserve_lifetimes=0.0, slice_free_drain=False,
+                       slice_strand_weight=w)
+        ch = plan_cluster_pack({"n": node()}, list(pending), params=p, pods_of=lambda n, g: pods[g], life=life)
+        assert [g.target is not None for g in ch["n"].gpus] == want

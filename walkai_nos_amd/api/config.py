@@ -78,7 +78,8 @@ class GpuPartitionerConfig(ManagerConfig):
     #: once learned; 0 = the constant), sliceReserveBacklog (GPUs of waiting work per sliced GPU
     #: above which the threshold stretches; 0 = never), sliceReserveStretch (its largest factor),
     #: sliceReserveHold, sliceReserveHoldMaxGpus, sliceFreeDrain, sliceFreeDrainAfterLifetimes,
-    #: sliceFreeDrainCapLifetimes, sliceWholeOvertakeSeconds, sliceWholeOvertakeLifetimes, sliceFill
+    #: sliceFreeDrainCapLifetimes, sliceStrandWeight, sliceWholeOvertakeSeconds, sliceWholeOvertakeLifetimes,
+    #: sliceFill
     packing: Dict[str, Any] = field(default_factory=dict)
     #: xcp layout of a node that carries no nos.nebuly.com/xcp-layout label: slices (SPX GPUs carved
     #: into CU-mask slices, mixed geometries, no flips), partitions (hardware compute partitions
@@ -99,6 +100,7 @@ class GpuPartitionerConfig(ManagerConfig):
                     "sliceReserveHoldMaxGpus": "slice_reserve_hold_max_gpus",
                     "sliceFreeDrain": "slice_free_drain", "sliceFreeDrainAfterLifetimes": "slice_free_drain_after",
                     "sliceFreeDrainCapLifetimes": "slice_free_drain_cap",
+                    "sliceStrandWeight": "slice_strand_weight",
                     "sliceWholeOvertakeSeconds": "slice_whole_overtake",
                     "sliceWholeOvertakeLifetimes": "slice_whole_overtake_lifetimes", "sliceFill": "slice_fill"}
     BOOL_PACKING_KEYS = ("spxReserve", "sliceFill", "sliceReserveHold", "sliceFreeDrain")

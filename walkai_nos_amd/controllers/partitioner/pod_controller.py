@@ -203,6 +203,9 @@ class PackParams:
     slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
     slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
     slice_free_drain_cap: float = 0.75  # ... but at most this many (0 = no cap)
+    slice_strand_weight: float = 1.0  # drain victim on a multi-GPU node: its slices in use of profiles pods wait
+                                    # for count as idle this many times over the drain (kube-scheduler sees as
+                                    # many fewer free slices of them on the node while the drain withholds them)
     slice_whole_overtake: float = 960.0  # seconds: a whole-GPU slice left free goes to the next whole-GPU pod
                                     # unless the oldest waiting pod is this much older (0 = strict FIFO)
     slice_whole_overtake_lifetimes: float = 4.0  # ... this many median pod run times once learned (0 = constant)

@@ -112,6 +112,10 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     if params.slice_reserve_backlog > 0:
         reserve_after *= min(params.slice_reserve_stretch, max(1.0, backlog / params.slice_reserve_backlog))
     aged = learned and pods_of is not None
+    waiting_profiles = {s[0] for s in (_single(r) for r, _ in unserved) if s is not None}
+    sliced_on: Dict[str, List[Any]] = {}
+    for name, g in sliced:
+        sliced_on.setdefault(name, []).append(g)
 
     def drain_key(name: str, g: Any, need: int) -> float:
         """How much a drain of ``g`` for ``need`` groups idles: the expected idle group-seconds
@@ -120,7 +124,14 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         if not aged:
             return float(g.used_groups())
         from .lifetimes import drain_cost
-        return drain_cost(pods_of(name, g.index), g.capacity, need, life)[0]
+        cost, wait = drain_cost(pods_of(name, g.index), g.capacity, need, life)
+        if params.slice_strand_weight > 0 and len(sliced_on.get(name, ())) > 1:
+            # the drain withholds its slices in use, and kube-scheduler stops seeing as many free
+            # slices of their profiles on the node's other GPUs: groups of profiles pods wait for
+            strand = sum(groups_of(p) * n for p, n in used_now.get((name, g.index), {}).items()
+                         if n > 0 and p in waiting_profiles)
+            cost += params.slice_strand_weight * strand * wait
+        return cost
 
     # reservations in force: a sliced GPU whose spec asks for its slices in use plus one that does
     # not fit yet is draining for the biggest such slice, and keeps draining for a pod of that
