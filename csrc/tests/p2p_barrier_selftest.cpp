@@ -98,7 +98,8 @@ int main(int argc, char** argv) {
   setenv("NOS_BARRIER_DEADLINE_MS", "200", 1);
   o = barrier(n, yes);
   unsetenv("NOS_BARRIER_DEADLINE_MS");
-  report("hung_device_deadline", n, o, o.rc == -3 && o.ms < 2000.0 &&
+  // (well under the 10 s default: the 200 ms deadline applied; loose enough for a loaded sanitizer run)
+  report("hung_device_deadline", n, o, o.rc == -3 && o.ms < 5000.0 &&
                                            o.res.err.find("did not complete") != std::string::npos);
 
   // 7. a second barrier on the same devices: links already enabled are reused, not an error
@@ -120,7 +121,7 @@ int main(int argc, char** argv) {
   hipEventRecord(ev, nullptr);
   hipError_t q = hipErrorNotReady;
   for (auto t = std::chrono::steady_clock::now(); q == hipErrorNotReady &&
-       std::chrono::steady_clock::now() - t < std::chrono::seconds(5);) {
+       std::chrono::steady_clock::now() - t < std::chrono::seconds(20);) {
     q = hipEventQuery(ev);
     std::this_thread::yield();
   }

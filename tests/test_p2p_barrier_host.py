@@ -45,4 +45,4 @@ def test_barrier_host_paths_on_a_multi_device_fake(tmp_path, flags, tag, n):
     got = {row["scenario"]: row for row in rows if "scenario" in row}
     assert set(got) == SCENARIOS and all(row["ok"] for row in got.values()), rows
     assert got["full_ring"]["peer"] == n and got["hung_device_deadline"]["rc"] == -3
-    assert got["hung_device_deadline"]["ms"] < 2000
+    assert got["hung_device_deadline"]["ms"] < 5000   # the 200 ms deadline, not the 10 s default
