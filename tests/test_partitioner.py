@@ -250,6 +250,25 @@ def test_packing_config_maps_to_pack_params():
         GpuPartitionerConfig(packing={"drainGain": -1}).validate()
 
 
+def test_every_packing_key_names_a_pack_param():
+    """Each ``packing`` key of the config (and so of the chart) maps to a ``PackParams`` field, and a
+    value set through it reaches the planner (booleans stay booleans)."""
+    import dataclasses
+
+    from walkai_nos_amd.api.config import GpuPartitionerConfig
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams
+    fields = {f.name for f in dataclasses.fields(PackParams)}
+    assert set(GpuPartitionerConfig.PACKING_KEYS.values()) <= fields
+    for key, name in GpuPartitionerConfig.PACKING_KEYS.items():
+        boolean = key in GpuPartitionerConfig.BOOL_PACKING_KEYS
+        value = False if boolean else 3.0
+        cfg = GpuPartitionerConfig(packing={key: value})
+        cfg.validate()
+        assert getattr(cfg.pack_params(), name) == value, key
+    p = GpuPartitionerConfig(packing={"sliceStrandWeight": 0, "sliceFreeDrainCapLifetimes": 0}).pack_params()
+    assert (p.slice_strand_weight, p.slice_free_drain_cap) == (0.0, 0.0)
+
+
 def test_pack_gain_drain_rotates_an_underused_gpu():
     # one GPU in CPX mode holding a single 1/8 pod, SPX pods waiting past drain_gain_after: the GPU
     # is drained for SPX (target set, no new CPX pods), which it would never be by the backlog rule
