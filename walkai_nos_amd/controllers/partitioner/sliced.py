@@ -17,7 +17,11 @@ planned per *pod* rather than per mode:
    use plus the pod's slice, which does not fit yet, so the partition plugin withholds every slice
    of that GPU (no new pod lands there) until enough of its pods have left; every pass recomputes
    it from what is in use, and the pod is placed as soon as it fits.  Without it a whole-GPU pod
-   would wait behind an endless stream of smaller ones;
+   would wait behind an endless stream of smaller ones.  A drain withholds the GPU's slices in use
+   too, and kube-scheduler still counts their pods' requests, so on a node of several GPUs it sees
+   that many fewer free slices of those profiles elsewhere: a GPU only pods of the waiting pod's own
+   profile fill is never reserved (nothing to gain), and the victim's hidden slices of profiles pods
+   wait for count in its drain cost;
 4. **fill**: the groups left over are carved into ``cpx_nps1`` slices, so small pods are scheduled
    without waiting for a planning pass.
 
@@ -120,7 +124,8 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
     def drain_key(name: str, g: Any, need: int) -> float:
         """How much a drain of ``g`` for ``need`` groups idles: the expected idle group-seconds
         until its running pods free the room (their ages against the observed run times,
-        ``lifetimes.drain_cost``), else the groups in use."""
+        ``lifetimes.drain_cost``), plus, on a node of several GPUs, ``slice_strand_weight`` x the
+        groups in use of profiles pods wait for x the expected wait; else the groups in use."""
         if not aged:
             return float(g.used_groups())
         from .lifetimes import drain_cost
