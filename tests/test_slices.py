@@ -352,10 +352,11 @@ def test_default_layout_of_unlabelled_nodes_comes_from_the_partitioner_config():
 
 def test_a_held_reservation_lapses_on_bigger_clusters():
     """``slice_reserve_hold_max_gpus``: a drain in progress keeps its target until a pod of its profile
-    is placed while the cluster has at most that many sliced GPUs; with more, it is re-decided each
-    pass (here: the whole-GPU pod is not overdue, so the draining GPU takes the small pod again).
-    The default (0) holds at any cluster size."""
-    p = PackParams(slice_reserve_after=900.0, slice_reserve_hold_max_gpus=2)
+    is placed while the cluster has at most that many sliced GPUs (default 2); with more, it is
+    re-decided each pass (here: the whole-GPU pod is not overdue, so the draining GPU takes the small
+    pod again). 0 holds at any cluster size."""
+    assert PackParams().slice_reserve_hold_max_gpus == 2
+    p = PackParams(slice_reserve_after=900.0)
 
     def draining():
         g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 3})
@@ -370,7 +371,7 @@ def test_a_held_reservation_lapses_on_bigger_clusters():
     ch = plan_cluster_pack({"n": _sliced_node(draining(), *full)}, list(pending), params=p)
     out = ch["n"].gpus[0]
     assert out.target is None and out.used.get("cpx_nps1", 0) + out.free.get("cpx_nps1", 0) >= 4
-    p0 = PackParams(slice_reserve_after=900.0)
+    p0 = PackParams(slice_reserve_after=900.0, slice_reserve_hold_max_gpus=0)
     ch = plan_cluster_pack({"n": _sliced_node(draining(), *full)}, list(pending), params=p0)
     out = (ch.get("n") or _sliced_node(draining(), *full)).gpus[0]
     assert out.target == {"cpx_nps1": 3, "spx_nps1": 1}          # 0: held at any cluster size

@@ -198,8 +198,9 @@ class PackParams:
     slice_reserve_backlog: float = 3.0  # ... stretched by backlog / this (GPUs of waiting work per sliced GPU; 0 = fixed)
     slice_reserve_stretch: float = 2.0  # ... at most this many times
     slice_reserve_hold: bool = True  # a reservation holds until a pod of its profile is placed ...
-    slice_reserve_hold_max_gpus: int = 0  # ... on clusters of at most this many sliced GPUs (0 = any size; load 1.0,
-                                    # 8 seeds x 200 quanta: 4 / 8 GPUs 97.9 / 98.8% holding always, 96.8 / 98.1 at 2)
+    slice_reserve_hold_max_gpus: int = 2  # ... on clusters of at most this many sliced GPUs (0 = any size): holding
+                                    # always gains under a point at load 1.0 on 4-8 GPUs but at load 1.2 every
+                                    # GPU ends up held for some profile (4 / 8 GPUs 85 / 83% vs 95 / 97% at 2)
     slice_free_drain: bool = True   # the oldest waiting pod reserves a GPU whose unused room no waiting pod fits,
     slice_free_drain_after: float = 0.5  # ... once it waited this many median pod run times per other sliced GPU
     slice_free_drain_cap: float = 0.75  # ... but at most this many (0 = no cap)
