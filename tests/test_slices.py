@@ -466,3 +466,19 @@ def test_a_pod_of_several_slices_may_reserve_a_gpu_its_profile_fills():
     g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 8})
     ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"cpx_nps1": 2}, 1000.0)], params=p)
     assert ch["n"].gpus[0].target == {"cpx_nps1": 10}
+
+
+def test_reservation_threshold_stretches_up_to_four_times_under_backlog():
+    """``sliceReserveStretch`` (4): with a long queue the threshold grows with the backlog (GPUs of
+    waiting work per sliced GPU over ``sliceReserveBacklog``), at most 4x — so under sustained
+    overload drains stay rare."""
+    assert PackParams().slice_reserve_stretch == 4.0
+    p = PackParams(slice_reserve_after=100.0, slice_reserve_backlog=1.0, slice_free_drain=False)
+
+    def target(age):
+        g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 8})
+        backlog = [({"cpx_nps1": 1}, 1.0)] * 80        # 10 GPUs of waiting work on one GPU
+        ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"spx_nps1": 1}, age)] + backlog, params=p)
+        return ch["n"].gpus[0].target if "n" in ch else None
+    assert target(350.0) is None                      # under 4 x 100 s
+    assert target(410.0) == {"cpx_nps1": 8, "spx_nps1": 1}
