@@ -573,3 +573,34 @@ def test_attention_reciprocal_bookkeeping_bit_identical(K, B, T, waves):
     assert torch.equal(outs[0], outs[1])
     ref = _ref_attention(qkv, H, Dh, 0.125).double()
     assert (outs[0].double().sum(0) - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("B,T,H,waves", [(1, 3401, 6, None), (1, 3401, 6, 7), (2, 300, 3, 64), (1, 77, 1, 3),
+                                         (1, 1000, 2, 333)])
+def test_attention_wide_kernel_bit_identical_to_two_wave_kernel(K, B, T, H, waves):
+    # attn_fwd_x3w (one wave per SIMD, two query tiles per wave) runs each tile's arithmetic in the
+    # order of attn_fwd_x3p<8> and writes the same partial slots: fp32 and x3-plane outputs are
+    # bit-identical for every stream-K split, and fp32-accurate against fp64
+    torch.manual_seed(21)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    w = waves or K.attention_x3_waves(K.slice_cus(), B, T, H)
+    ref = _ref_attention(qkv, H, 64, 0.125)
+    try:
+        for x3 in (False, True):
+            outs = []
+            for wide in (True, False):
+                K.set_attention_x3_wide(wide)
+                out = (torch.full((3, B, T, H * 64), float("nan"), dtype=torch.bfloat16, device="cuda") if x3
+                       else torch.full((B, T, H * 64), float("nan"), device="cuda"))
+                outs.append(K.attention_x3f(qkv, out, H, 64, 0.125, w))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (x3, w)
+            o = outs[0].double().sum(0) if x3 else outs[0].double()
+            assert (o - ref.double()).abs().max().item() < 2e-6, (x3, w)
+            if x3:
+                # the planes are the exact split of the fp32 output (direct and merged tiles alike)
+                assert torch.equal(outs[0], K.split3(f32)), w
+            else:
+                f32 = outs[0]
+    finally:
+        K.set_attention_x3_wide(os.environ.get("NOS_ATTN_WIDE") == "1")

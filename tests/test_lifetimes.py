@@ -36,8 +36,9 @@ def test_residuals_are_conditional_on_the_age():
     assert draws == {50.0, 150.0}
     assert m.expected_residual(250.0) == pytest.approx(100.0)
     assert m.expected_residual(0.0) == pytest.approx(250.0)
-    # older than every observation: half its age again (at least a second)
-    assert m.sample_residual(1000.0, rng) == 500.0 and m.expected_residual(1.0 + 400.0) == pytest.approx(200.5)
+    # older than every observation: its age again (at least a second) — a pod that outlived every
+    # finished one is evidence of a long tail, not of an imminent end
+    assert m.sample_residual(1000.0, rng) == 1000.0 and m.expected_residual(1.0 + 400.0) == pytest.approx(401.0)
 
 
 def test_drain_cost_basics():
@@ -74,6 +75,66 @@ def test_tracker_learns_run_times_from_finished_and_vanished_pods():
     t.update([_pod("a", "Succeeded", start=1000.0, finished=1250.0)], now=1300.0)
     assert sorted(t.model._sorted) == [pytest.approx(100.0), pytest.approx(250.0)]
     assert t.update([], now=1400.0) == {} and t.model.n == 2
+
+
+def test_terminal_pod_seen_only_after_it_finished_is_learned_once():
+    # a pod that starts and finishes between two passes is still a run time (its own
+    # startTime to finishedAt), counted once however many passes list it before it is deleted
+    t = LifetimeTracker(_model([], min_samples=1))
+    done = _pod("c", "Succeeded", start=1000.0, finished=1030.0)
+    t.update([done], now=1100.0)
+    t.update([done], now=1200.0)
+    assert t.model._sorted == [pytest.approx(30.0)]
+
+
+def test_running_pods_are_censored_observations():
+    """30% of the pods never end (long-running inference Deployments). Learning from
+    finished pods alone gives the median of the short ones; with the running pods as right-censored
+    observations (Kaplan-Meier) the learned median tracks the whole population's, and so do the
+    reservation thresholds built on it."""
+    rng = random.Random(7)
+    t = LifetimeTracker(LifetimeModel(window=4096, min_samples=8))
+    pods, now, seq = {}, 0.0, 0
+    life = {}
+    for step in range(600):                       # one pass every 5 s for 50 minutes
+        now = step * 5.0
+        for _ in range(2):                        # two pods arrive per pass
+            seq += 1
+            name = f"p{seq}"
+            life[name] = float("inf") if rng.random() < 0.3 else rng.uniform(10.0, 50.0)
+            pods[name] = now
+        seen = []
+        for name, start in list(pods.items()):
+            if now - start >= life[name]:
+                seen.append(_pod(name, "Succeeded", start=start, finished=start + life[name]))
+                del pods[name]
+            else:
+                seen.append(_pod(name, "Running", start=start))
+        t.update(seen, now)
+    # the population: 70% uniform(10, 50) s, 30% never end -> median = 10 + 40 * 0.5 / 0.7
+    true_median = 10.0 + 40.0 * 0.5 / 0.7
+    assert t.model.median() == pytest.approx(true_median, rel=0.06)
+    finished_only = LifetimeModel(window=4096)
+    for v in t.model._sorted:
+        finished_only.observe(v)
+    assert finished_only.median() == pytest.approx(30.0, rel=0.06)    # the survival-biased estimate
+    # a pod that outlived every finished one is expected to run on (not to end within seconds)
+    assert t.model.expected_residual(60.0) >= 60.0
+    # the sliced planner's threshold (slice_reserve_lifetimes x the learned median) follows
+    from walkai_nos_amd.controllers.partitioner.pod_controller import PackParams
+    p = PackParams()
+    assert p.slice_reserve_lifetimes * t.model.median() > p.slice_reserve_lifetimes * finished_only.median() * 1.2
+
+
+def test_drain_cost_counts_groups_the_pod_list_misses():
+    # ADVICE r5: a stale or empty status-pods annotation must not make a busy GPU look free
+    m = _model([240.0] * 16)
+    assert drain_cost([], capacity=8, need=8, model=m) == (0.0, 0.0)               # no model of use
+    cost, wait = drain_cost([], capacity=8, need=8, model=m, used=8)                # all 8 groups in use
+    assert wait > 0.0
+    # partly listed: the unlisted 4 groups count as a pod that has just started
+    _, w_listed = drain_cost([(4, 230.0)], capacity=8, need=8, model=m, used=8)
+    assert w_listed == pytest.approx(240.0)
 
 
 def test_sliced_planner_drains_the_gpu_whose_pods_end_soonest():

@@ -394,3 +394,27 @@ def test_agent_blocks_every_gpu_while_a_memory_partition_change_waits_for_an_idl
     plan = new_xcp_config_plan(state, {0: "spx_nps1", 1: "spx_nps1"}, spec, "nps2", "nps1")
     assert plan.memory_partition is None and plan.changes == []
     assert sorted(g for g, _ in plan.blocked) == [0, 1]
+
+
+def test_two_planners_with_different_defaults_in_one_process():
+    """defaultXcpLayout / sharedSliceSkipCounts are passed to each planner's node
+    models, not set as module globals — two planners in one process each see their own."""
+    from walkai_nos_amd.api.config import GpuPartitionerConfig
+    from walkai_nos_amd.controllers.partitioner.pod_controller import new_node_model
+    from walkai_nos_amd.models.defaults import ModelDefaults
+    api_ = InMemoryAPIServer()
+    api_.create(xnode())                       # no xcp-layout label
+    sliced = ModelDefaults.from_config(GpuPartitionerConfig())          # chart default: slices
+    parts = ModelDefaults.from_config(GpuPartitionerConfig(defaultXcpLayout="partitions", sharedSliceSkipCounts=[]))
+    pa, pb = PodController(api_, defaults=sliced), PodController(api_, defaults=parts)
+    n = api_.get("Node", "n0")
+    assert new_node_model("xcp", n, defaults=pa.defaults).layout == "slices"
+    assert new_node_model("xcp", n, defaults=pb.defaults).layout == "partitions"
+    assert new_node_model("xcp", n).layout == "partitions"             # library default
+    # interleaved: building one planner's models never changes the other's
+    assert pa._models([n])["n0"].layout == "slices"
+    assert pb._models([n])["n0"].layout == "partitions"
+    assert pa._models([n])["n0"].layout == "slices"
+    assert sliced.shared_skip_counts == (5, 7) and parts.shared_skip_counts == ()
+    # the node initialiser of each planner uses its own defaults too
+    assert NodeInitializer(api_, defaults=sliced).defaults is sliced

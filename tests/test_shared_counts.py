@@ -47,17 +47,18 @@ def test_counts_below_five_and_dedicated_slices_are_unaffected():
     assert g.update_geometry_for({"32cu.24gb": 1}) and g.free == {"32cu.24gb": 1}
 
 
-def test_skip_list_can_be_disabled_per_gpu_and_globally():
+def test_skip_list_can_be_disabled_per_gpu_and_per_planner():
     g = _gpu(4, skip=())
     assert g.update_geometry_for({"16gb": 1}) and g.shared_count() == 5
-    old = sp.SKIP_SHARED_COUNTS
-    try:
-        sg.set_skip_shared_counts([])
-        g = _gpu(4)
-        assert g.update_geometry_for({"16gb": 1}) and g.shared_count() == 5
-        assert g.clone().skip_shared is None
-    finally:
-        sp.SKIP_SHARED_COUNTS = old
+    assert g.clone().skip_shared == ()
+    # a planner's ModelDefaults reach every GPU of the node models it builds
+    from walkai_nos_amd.kube import objects as ko
+    from walkai_nos_amd.api import v1alpha1 as api
+    from walkai_nos_amd.models.defaults import ModelDefaults
+    node = ko.new_node("n", {api.LABEL_GPU_PARTITIONING: "cumask", "amd.com/gpu.product-name": "AMD_Instinct_MI355X",
+                             "amd.com/gpu.count": "2", "amd.com/gpu.vram": "288G"})
+    assert [g.skip_shared for g in sg.new_node(node).gpus] == [(5, 7), (5, 7)]
+    assert [g.skip_shared for g in sg.new_node(node, ModelDefaults(shared_skip_counts=())).gpus] == [(), ()]
 
 
 def test_config_rejects_bad_skip_counts():

@@ -331,13 +331,9 @@ def test_default_layout_of_unlabelled_nodes_comes_from_the_partitioner_config():
     n = ko.new_node("n", {api.LABEL_GPU_PARTITIONING: "xcp", "amd.com/gpu.product-name": "AMD_Instinct_MI355X",
                           "amd.com/gpu.count": "1"})
     assert xcp_node.get_layout(n) == "partitions"          # library default: unchanged
-    try:
-        xcp_node.set_default_layout("slices")
-        assert xcp_node.get_layout(n) == "slices"
-        n["metadata"]["labels"][api.LABEL_XCP_LAYOUT] = "partitions"
-        assert xcp_node.get_layout(n) == "partitions"      # the label wins
-    finally:
-        xcp_node.set_default_layout("partitions")
+    assert xcp_node.get_layout(n, "slices") == "slices"    # the planner's default, passed explicitly
+    n["metadata"]["labels"][api.LABEL_XCP_LAYOUT] = "partitions"
+    assert xcp_node.get_layout(n, "slices") == "partitions"  # the label wins
     import os
 
     import yaml
@@ -387,6 +383,33 @@ def test_free_drain_reserves_room_no_waiting_pod_fits():
         return ch["n"].gpus[0].target if "n" in ch else None
     assert run(True) == {"cpx_nps1": 7, "dpx_nps1": 1}
     assert run(False) is None
+
+
+def test_free_drain_lapses_when_a_smaller_pod_arrives_on_one_gpu():
+    """a free drain is held only while no waiting pod fits the GPU's room. On a one-GPU
+    cluster (where reservations are held) the free drain made for a half-GPU pod lapses on the next
+    pass once a 1/8 pod arrives that the free group fits — the small pod is placed at once."""
+    p = PackParams(slice_reserve_after=900.0)
+    fd: set = set()                       # the controller's record of free drains, across passes
+    g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 7}, free={"cpx_nps1": 1})
+    ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"dpx_nps1": 1}, 10.0)], params=p, free_drains=fd)
+    assert ch["n"].gpus[0].target == {"cpx_nps1": 7, "dpx_nps1": 1}     # the free drain
+    assert fd == {("n", 0)}
+
+    def held():
+        h = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 7})
+        h.target, h.target_sliced = {"cpx_nps1": 7, "dpx_nps1": 1}, True
+        return h
+    # next pass: the model reports the reservation in force; a 1/8 pod now waits too
+    pending = [({"dpx_nps1": 1}, 20.0), ({"cpx_nps1": 1}, 1.0)]
+    ch = plan_cluster_pack({"n": _sliced_node(held())}, list(pending), params=p, free_drains=fd)
+    out = ch["n"].gpus[0]
+    assert out.target is None and out.used.get("cpx_nps1", 0) + out.free.get("cpx_nps1", 0) == 8
+    assert fd == set()                    # lapsed and forgotten
+    # the same reservation made by the threshold (not a free drain) is held: the small pod waits
+    ch = plan_cluster_pack({"n": _sliced_node(held())}, list(pending), params=p, free_drains=set())
+    out = (ch.get("n") or _sliced_node(held())).gpus[0]
+    assert out.target == {"cpx_nps1": 7, "dpx_nps1": 1}
 
 
 def test_reservation_threshold_in_learned_lifetimes():

@@ -218,11 +218,17 @@ class GpuAgentConfig(AgentConfig):
     count (docs/partitioning-modes-comparison.md, ``profiles/fairness_r4_repeat.json``)."""
     hbmLimitShimPath: str = "/usr/lib/nos/libnos_hbmlimit.so"
     sharedSliceHwQueues: int = -1
+    #: memory-only containers of one GPU start one after another through the slice plugin's
+    #: PreStartContainer (deviceplugin/startgate.py): the longest wait for the previous one's
+    #: compute queues, seconds (0 = no gate; kubelet gives the call 30 s)
+    sharedSliceStartGateSeconds: float = 20.0
 
     def validate(self) -> None:
         super().validate()
         if not -1 <= self.sharedSliceHwQueues <= 4:
             raise ValueError("sharedSliceHwQueues must be -1 (auto), 0 (HIP default) or 1..4")
+        if not 0 <= self.sharedSliceStartGateSeconds < 30:
+            raise ValueError("sharedSliceStartGateSeconds must be in [0, 30) (kubelet's PreStartContainer timeout)")
 
 
 @dataclass

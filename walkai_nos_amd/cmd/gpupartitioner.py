@@ -11,6 +11,7 @@ import sys
 
 from ..api.config import GpuPartitionerConfig, load_config_file
 from ..controllers.partitioner.setup import setup_partitioner
+from ..models.defaults import ModelDefaults
 from ..models.xcp.known_configs import load_known_geometries_file, set_known_geometries
 from .common import (apply_manager_flags, base_parser, make_client, make_manager, run_until_signal,
                      serve_endpoints, setup_logging)
@@ -28,12 +29,14 @@ def main(argv=None) -> int:
         log.info("loaded known geometries from %s", cfg.knownMigGeometriesFile)
     client = make_client(args.kubeconfig)
     mgr = make_manager(client, cfg, "gpupartitioner")
-    from ..models.xcp.node import set_default_layout
-    set_default_layout(cfg.defaultXcpLayout)
-    from ..models.slicing.gpu import set_skip_shared_counts
-    set_skip_shared_counts(cfg.sharedSliceSkipCounts)
+    defaults = ModelDefaults.from_config(cfg)
+    if defaults.xcp_layout != "partitions":
+        # upgrade note (docs/upgrade.md): unlabeled xcp nodes follow defaultXcpLayout
+        log.warning("xcp nodes without the nos.nebuly.com/xcp-layout label are planned as %r "
+                    "(defaultXcpLayout); label a node xcp-layout=partitions to keep hardware partitions",
+                    defaults.xcp_layout)
     setup_partitioner(mgr, batch_timeout=cfg.batchWindowTimeoutSeconds, batch_idle=cfg.batchWindowIdleSeconds,
-                      scoring=cfg.scoring, policy=cfg.planningPolicy, pack=cfg.pack_params())
+                      scoring=cfg.scoring, policy=cfg.planningPolicy, pack=cfg.pack_params(), defaults=defaults)
     serve_endpoints(mgr, cfg)
     return run_until_signal(mgr)
 

@@ -46,10 +46,13 @@ def main(argv=None) -> int:
     mgr = make_manager(client, cfg, "sliceagent")
     # render nodes and slice health come from the device map (a slice whose GPU left the map is
     # Unhealthy); the sysfs listing is only the fallback for a map without render minors
+    from ..deviceplugin.startgate import StartGate
     plugins = PluginManager(store, render_nodes_from_sysfs(), socket_dir=cfg.devicePluginDir,
                             kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
                             cu_count=gpus[0].cu_count or 256, shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map,
-                            shared_hw_queues=cfg.sharedSliceHwQueues)
+                            shared_hw_queues=cfg.sharedSliceHwQueues,
+                            start_gate=StartGate(timeout=cfg.sharedSliceStartGateSeconds)
+                            if cfg.sharedSliceStartGateSeconds > 0 else None)
 
     class Notify:
         def restart(self, node_name, timeout=60):

@@ -9,9 +9,14 @@ groups those pods free stay idle.  How long that takes, and how much capacity it
 on how long the pods on the GPU still have to run, which the planner can only estimate from the
 run times of the pods that already finished and from how long each running pod has run so far.
 
-* :class:`LifetimeModel` — the last ``window`` observed run times (seconds); the conditional
-  residual of a pod that has run ``age`` seconds is drawn from the observed run times longer
-  than ``age`` (a pod older than every observation is given half its age again);
+* :class:`LifetimeModel` — a Kaplan–Meier estimate of the run-time distribution from the last
+  ``window`` finished pods (events) and the pods running now (right-censored at their age: each
+  has run at least that long). Learning from finished pods alone is survival-biased — a node whose
+  long-running inference Deployments never finish would feed the model only its short pods, and
+  the median, which sets the reservation thresholds (``sliced.py``), would fire early. The
+  conditional residual of a pod that has run ``age`` seconds is drawn from the estimate beyond
+  ``age``; past the estimate's support (the mass of pods that outlive every observation) a pod is
+  given its age again (a heavy tail's expected residual, not the half-age of an exhausted sample);
 * :func:`drain_cost` — Monte Carlo over those residuals (a fixed seed: the planner is
   deterministic): expected idle group-seconds until ``need`` groups are free, and the expected
   time until then;
@@ -36,7 +41,9 @@ class LifetimeModel:
         self.window = window
         self.min_samples = min_samples
         self._recent: Deque[float] = collections.deque(maxlen=window)
-        self._sorted: List[float] = []
+        self._sorted: List[float] = []        # finished run times (events)
+        self._censored: List[float] = []      # ages of the pods running now (sorted)
+        self._km: Optional[Tuple[List[float], List[float]]] = None
 
     def observe(self, seconds: float) -> None:
         if seconds <= 0:
@@ -48,42 +55,107 @@ class LifetimeModel:
                 self._sorted.pop(i)
         self._recent.append(seconds)
         bisect.insort(self._sorted, seconds)
+        self._km = None
+
+    def censor(self, ages: Iterable[float]) -> None:
+        """The ages of the pods running now (replaces the previous set): right-censored observations."""
+        self._censored = sorted(a for a in ages if a > 0)
+        self._km = None
 
     @property
     def n(self) -> int:
+        """Finished pods observed (the estimate is ready once ``min_samples`` have finished)."""
         return len(self._sorted)
 
     def ready(self) -> bool:
         return self.n >= self.min_samples
 
+    def survival(self) -> Tuple[List[float], List[float]]:
+        """The Kaplan–Meier step function: event times t_k and S(t_k) just after each."""
+        if self._km is None:
+            times: List[float] = []
+            surv: List[float] = []
+            s = 1.0
+            ev, ce = self._sorted, self._censored
+            n_at_risk = len(ev) + len(ce)
+            i = c = 0
+            while i < len(ev):
+                t = ev[i]
+                while c < len(ce) and ce[c] < t:     # censored before t: leave the risk set
+                    n_at_risk -= 1
+                    c += 1
+                d = 0
+                while i < len(ev) and ev[i] == t:
+                    d += 1
+                    i += 1
+                if n_at_risk > 0:
+                    s *= 1.0 - d / n_at_risk
+                times.append(t)
+                surv.append(s)
+                n_at_risk -= d
+            self._km = (times, surv)
+        return self._km
+
+    def _s_at(self, t: float) -> float:
+        times, surv = self.survival()
+        k = bisect.bisect_right(times, t)
+        return surv[k - 1] if k else 1.0
+
     def quantile(self, q: float) -> Optional[float]:
+        """Smallest run time t with P(T <= t) > q (without censored pods: the order statistic
+        ``sorted[int(q * n)]``); beyond the estimate's support (at least 1 - q of the pods outlive
+        every finished one) the largest age seen, a lower bound."""
         if not self._sorted:
             return None
-        return self._sorted[min(self.n - 1, max(0, int(q * self.n)))]
+        times, surv = self.survival()
+        for t, s in zip(times, surv):
+            if 1.0 - s > q + 1e-12:
+                return t
+        return max(times[-1], self._censored[-1] if self._censored else 0.0)
 
     def median(self) -> Optional[float]:
         return self.quantile(0.5)
 
     def sample_residual(self, age: float, rng: random.Random) -> float:
         """Seconds a pod that has run ``age`` seconds still runs (one draw)."""
-        i = bisect.bisect_right(self._sorted, age)
-        if i >= self.n:
-            return max(1.0, 0.5 * age)
-        return self._sorted[rng.randrange(i, self.n)] - age
+        times, surv = self.survival()
+        s0 = self._s_at(age)
+        k0 = bisect.bisect_right(times, age)
+        if k0 >= len(times) or s0 <= 0.0:
+            return max(1.0, age)
+        u = rng.random() * s0                 # S(T) = u: the draw's survival level
+        for k in range(k0, len(times)):
+            if surv[k] <= u:
+                return times[k] - age
+        return max(1.0, age, times[-1] - age)  # it outlives every finished pod
 
     def expected_residual(self, age: float) -> float:
-        i = bisect.bisect_right(self._sorted, age)
-        if i >= self.n:
-            return max(1.0, 0.5 * age)
-        tail = self._sorted[i:]
-        return sum(tail) / len(tail) - age
+        times, surv = self.survival()
+        s0 = self._s_at(age)
+        k0 = bisect.bisect_right(times, age)
+        if k0 >= len(times) or s0 <= 0.0:
+            return max(1.0, age)
+        e, prev = 0.0, s0
+        for k in range(k0, len(times)):
+            e += (prev - surv[k]) / s0 * (times[k] - age)
+            prev = surv[k]
+        e += prev / s0 * max(1.0, age, times[-1] - age)
+        return e
 
 
 def drain_cost(pods: Sequence[PodAge], capacity: int, need: int, model: LifetimeModel,
-               samples: int = 96, seed: int = 0) -> Tuple[float, float]:
+               samples: int = 96, seed: int = 0, used: Optional[int] = None) -> Tuple[float, float]:
     """(expected idle group-seconds, expected seconds) until ``need`` of ``capacity`` groups are
-    free on a GPU running ``pods`` if no new pod is placed on it meanwhile."""
-    free0 = capacity - sum(g for g, _ in pods)
+    free on a GPU running ``pods`` if no new pod is placed on it meanwhile. ``used`` (the GPU
+    model's used groups) is authoritative for what is occupied: groups ``pods`` does not account
+    for — a pod bound but not yet Running, or one the agent's status-pods annotation does not list
+    yet — count as a pod that has just started, so a stale annotation never makes a busy GPU look
+    free (and the cheapest drain victim)."""
+    held = sum(g for g, _ in pods)
+    if used is not None and used > held:
+        pods = list(pods) + [(used - held, 0.0)]
+        held = used
+    free0 = capacity - held
     if free0 >= need:
         return 0.0, 0.0
     rng = random.Random(seed)
@@ -103,17 +175,20 @@ def drain_cost(pods: Sequence[PodAge], capacity: int, need: int, model: Lifetime
 
 
 class LifetimeTracker:
-    """Start times of the running pods the planner watches, and the run times of finished ones."""
+    """Start times of the running pods the planner watches, the run times of finished ones, and
+    the ages of the running ones as the model's censored observations."""
 
     def __init__(self, model: Optional[LifetimeModel] = None):
         self.model = model or LifetimeModel()
         self._running: Dict[str, Tuple[float, float]] = {}   # uid -> (start, last seen running)
+        self._done: Dict[str, float] = {}                      # terminal pods already counted
 
     def update(self, pods: Iterable[Dict[str, Any]], now: float) -> Dict[str, float]:
-        """Feed every pod the planner can see that uses its resources; returns ``ns/name`` ->
-        seconds run so far of the running ones. A pod that was running and is now terminal (or
-        gone) adds its run time: start to its finish time when the pod records one, else to the
-        last time it was seen running."""
+        """Feed every pod the planner can see that uses its resources — running and terminal
+        (Succeeded / Failed) alike; returns ``ns/name`` -> seconds run so far of the running ones.
+        A pod that was running and is now terminal adds its run time, start to the finish time it
+        records; a terminal pod never seen running adds start to finish too (it ran between two
+        passes), once; a pod that vanished adds start to the last time it was seen running."""
         ages: Dict[str, float] = {}
         seen = set()
         for p in pods:
@@ -126,13 +201,22 @@ class LifetimeTracker:
                 self._running[uid] = (start, now)
                 seen.add(uid)
                 ages["/".join(ko.key(p))] = max(0.0, now - start)
-            elif phase in ("Succeeded", "Failed") and uid in self._running:
-                begun, _ = self._running.pop(uid)
+            elif phase in ("Succeeded", "Failed"):
+                seen.add(uid)
                 end = _finished_at(p)
-                self.model.observe((end if end is not None else now) - begun)
+                if uid in self._running:
+                    begun, _ = self._running.pop(uid)
+                    self.model.observe((end if end is not None else now) - begun)
+                    self._done[uid] = now
+                elif uid not in self._done and start is not None and end is not None:
+                    self.model.observe(end - start)   # started and finished between two passes
+                    self._done[uid] = now
         for uid in [u for u in self._running if u not in seen]:
             begun, last = self._running.pop(uid)
             self.model.observe(last - begun)
+        for uid in [u for u, t in self._done.items() if u not in seen and now - t > 0]:
+            del self._done[uid]               # terminal pods are forgotten once they are deleted
+        self.model.censor(ages.values())
         return ages
 
 

@@ -30,6 +30,7 @@ from ...kube import objects as ko
 from ...kube.errors import NotFound
 from ...kube.runtime import Request, Result
 from ...models import annotation as ann
+from ...models.defaults import ModelDefaults
 from ...models.partitioned import PartitionedNode
 from ...models.slicing import gpu as slicing_gpu
 from ...models.slicing.gpu import SlicingNode
@@ -67,10 +68,13 @@ def requested_profiles(kind: str, pod: Dict[str, Any]) -> Dict[str, int]:
     return out
 
 
-def new_node_model(kind: str, node: Dict[str, Any], scoring: str = "fraction") -> NodeModel:
+def new_node_model(kind: str, node: Dict[str, Any], scoring: str = "fraction",
+                   defaults: Optional[ModelDefaults] = None) -> NodeModel:
+    """The node's model under the planner's ``defaults`` (layout of unlabeled xcp nodes, memory-only
+    counts skipped on cumask GPUs); none given: the library defaults."""
     if kind == api.PARTITIONING_KIND_XCP:
-        return xcp_node.new_node(node, scoring)
-    return slicing_gpu.new_node(node)
+        return xcp_node.new_node(node, scoring, defaults)
+    return slicing_gpu.new_node(node, defaults)
 
 
 def _changed_gpus(before: NodeModel, after: NodeModel) -> int:
@@ -312,7 +316,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
                       mode_age: Optional[Callable[[str, int], float]] = None,
                       last_served: Optional[Mapping[str, float]] = None,
                       pods_of: Optional[Callable[[str, int], List[Tuple[int, float]]]] = None,
-                      life: Any = None) -> Dict[str, NodeModel]:
+                      life: Any = None, free_drains: Optional[set] = None) -> Dict[str, NodeModel]:
     """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
     reference's "first node that can change wins").
 
@@ -401,7 +405,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         return changed
     if any(getattr(m, "layout", "partitions") != "partitions" for m in current.values()):
         from .sliced import plan_sliced
-        plan_sliced(current, models, changed, unserved, params, mode_age, pods_of, life, placed_on)
+        plan_sliced(current, models, changed, unserved, params, mode_age, pods_of, life, placed_on, free_drains)
         if not unserved:
             return changed
     # the homogeneous rules below only touch GPUs of nodes laid out as hardware partitions
@@ -589,10 +593,12 @@ class PodController:
     def __init__(self, client: Any, kind: str = api.PARTITIONING_KIND_XCP, partitioner: Optional[Partitioner] = None,
                  clock: Callable[[], float] = time.time, batch_timeout: float = 0.0, batch_idle: float = 0.0,
                  retry_after: float = 5.0, scoring: str = "fraction", policy: str = "fifo",
-                 pack: Optional[PackParams] = None):
+                 pack: Optional[PackParams] = None, defaults: Optional[ModelDefaults] = None):
         self.client = client
         self.kind = kind
         self.scoring = scoring
+        #: this planner's model defaults (``GpuPartitionerConfig`` through ``ModelDefaults.from_config``)
+        self.defaults = defaults or ModelDefaults()
         if policy not in POLICIES:
             raise ValueError(f"unknown planning policy {policy!r}")
         self.policy = policy
@@ -602,6 +608,7 @@ class PodController:
         self._last_served: Dict[str, float] = {}  # profile -> last time a GPU was in its mode
         self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
         self.lifetimes = LifetimeTracker()        # run times of finished pods (sliced-GPU drains)
+        self._free_drains: set = set()            # (node, GPU) reservations that are free drains
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -757,7 +764,7 @@ class PodController:
         out: Dict[str, NodeModel] = {}
         for n in nodes:
             try:
-                out[ko.name(n)] = new_node_model(self.kind, n, self.scoring)
+                out[ko.name(n)] = new_node_model(self.kind, n, self.scoring, self.defaults)
             except ValueError as e:
                 log.warning("skipping node %s: %s", ko.name(n), e)
         return out
@@ -820,7 +827,9 @@ class PodController:
 
         from ...models.xcp.slices import groups_of
         names = {ko.name(n) for n in nodes}
-        pods = [p for p in self.client.list("Pod", field_selector="status.phase=Running", copy=False)
+        # running AND terminal pods: a pod that finished is a run time for the lifetime model (with
+        # its own finishedAt), however briefly it ran between two passes
+        pods = [p for p in self.client.list("Pod", field_selector="status.phase!=Pending", copy=False)
                 if ko.pod_node_name(p) in names]
         groups: Dict[str, int] = {}
         mine = []
@@ -828,7 +837,8 @@ class PodController:
             r = requested_profiles(self.kind, p)
             if r:
                 mine.append(p)
-                groups["/".join(ko.key(p))] = sum(groups_of(k) * q for k, q in r.items())
+                if ko.pod_phase(p) == "Running":
+                    groups["/".join(ko.key(p))] = sum(groups_of(k) * q for k, q in r.items())
         ages = self.lifetimes.update(mine, now)
         by: Dict[Tuple[str, int], List[Tuple[int, float]]] = {}
         for n in nodes:
@@ -950,7 +960,7 @@ class PodController:
                 if any(getattr(m, "layout", "partitions") != "partitions" for m in models.values()) else None
             changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand,
                                         self._mode_ages(models, now), self._served(models, now),
-                                        pods_of, self.lifetimes.model)
+                                        pods_of, self.lifetimes.model, self._free_drains)
             need = requested
         elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}

@@ -30,7 +30,7 @@ homogeneous pack planner on the same churn.
 """
 from __future__ import annotations
 
-from typing import Any, Callable, Dict, List, Mapping, Optional, Tuple
+from typing import Any, Callable, Dict, List, Mapping, Optional, Set, Tuple
 
 from ...models.xcp.slices import LAYOUT_AUTO, LAYOUT_PARTITIONS, SLICE_NPS, groups_of, is_slice_profile, new_sliced_gpu
 
@@ -59,11 +59,16 @@ def _hardware_gpu(g: Any, profile: str) -> Any:
 def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: Dict[str, Any], unserved: Pending,
                 params: Any, mode_age: Optional[Callable[[str, int], float]] = None,
                 pods_of: Optional[Callable[[str, int], List[Tuple[int, float]]]] = None, life: Any = None,
-                placed_on: Optional[Mapping[Tuple[str, int], float]] = None) -> None:
+                placed_on: Optional[Mapping[Tuple[str, int], float]] = None,
+                free_drains: Optional[Set[Tuple[str, int]]] = None) -> None:
     """Layout choice, backfill, reservation and fill for the sliced GPUs of ``current`` (module
     docstring); places the pods it can (removing them from ``unserved``) and records the nodes
     whose spec changed in ``changed``. ``placed_on``: (node, GPU) -> age of the oldest pending pod
-    the caller already gave a free slice there in this pass."""
+    the caller already gave a free slice there in this pass. ``free_drains``: the caller's record,
+    kept across passes, of the reservations that are free drains (3b) — those are recomputed every
+    pass, never held (updated in place)."""
+    if free_drains is None:
+        free_drains = set()
     before = {n: [_spec(g) for g in m.gpus] for n, m in original.items()}
 
     def past_stint(name: str, idx: int) -> bool:
@@ -129,7 +134,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         if not aged:
             return float(g.used_groups())
         from .lifetimes import drain_cost
-        cost, wait = drain_cost(pods_of(name, g.index), g.capacity, need, life)
+        cost, wait = drain_cost(pods_of(name, g.index), g.capacity, need, life, used=g.used_groups())
         if params.slice_strand_weight > 0 and len(sliced_on.get(name, ())) > 1:
             # the drain withholds its slices in use, and kube-scheduler stops seeing as many free
             # slices of their profiles on the node's other GPUs: groups of profiles pods wait for
@@ -150,7 +155,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
             for og in m.gpus:
                 if getattr(og, "sliced", False) and og.target is not None and og.target_sliced:
                     extra = [x for x, n in og.target.items() if n > og.used.get(x, 0) and is_slice_profile(x)]
-                    if extra:
+                    if extra and (name, og.index) not in free_drains:
                         held[(name, og.index)] = max(extra, key=lambda x: (groups_of(x), x))
     by_key = {(name, g.index): g for name, g in sliced}
     name_of = {id(g): name for name, g in sliced}
@@ -170,6 +175,7 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
         """Drain ``g`` for ``q`` slices of ``p``: its spec becomes the slices in use plus those."""
         want = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
         want[p] = want.get(p, 0) + q
+        free_drains.discard((name, g.index))
         g.used = {k: v for k, v in used_now.get((name, g.index), {}).items() if v > 0}
         g.free = {}
         g.target, g.target_sliced = want, True
@@ -266,7 +272,11 @@ def plan_sliced(current: Dict[str, Any], original: Mapping[str, Any], changed: D
                 break
             g = min(idle, key=lambda c: c[:4])[-1]
             reserve(name_of[id(g)], g, p, q)
+            free_drains.add((name_of[id(g)], g.index))
             draining.add(p)
+    # a recorded free drain that is no reservation any more (placed, lapsed) is forgotten
+    for k in [k for k in free_drains if k not in by_key or by_key[k].target is None]:
+        free_drains.discard(k)
     # 4. fill
     if params.slice_fill:
         for _, g in sliced:

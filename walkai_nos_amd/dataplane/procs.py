@@ -20,7 +20,7 @@ import subprocess
 import sys
 import time
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SHIM = os.path.join(ROOT, "walkai_nos_amd", "_native", "libnos_hbmlimit.so")
@@ -42,27 +42,34 @@ class PodProc:
     result: Dict[str, Any] = field(default_factory=dict)
 
 
+def _place(profiles: Sequence[str], cu_count: int):
+    from ..device.slicing_client import MemorySliceStore
+    from ..models.slicing.cumask import place
+    wanted = [(f"{BDF}::s{i}", p) for i, p in enumerate(profiles)]
+    slices = place([], wanted, cu_count)
+    store = MemorySliceStore()
+    store.save({0: slices})
+    return wanted, {s.id: s for s in slices}, store
+
+
+def _plugin(prof: str, store: Any, cu_count: int, shim_path: str, start_gate: Any = None) -> Any:
+    from ..deviceplugin.server import SliceDevicePlugin
+    from ..models.slicing.profile import as_resource_name
+    return SliceDevicePlugin(as_resource_name(prof), store, {0: "/dev/dri/renderD128"}, cu_count=cu_count,
+                             shim_path=shim_path, socket_dir="/tmp", start_gate=start_gate)
+
+
 def allocate_envs(profiles: Sequence[str], cu_count: int = 256, shim: bool = True,
                   shim_path: str = SHIM) -> List[Dict[str, str]]:
     """Place one slice per profile on GPU 0 (``cumask.place``, largest first, rows never moved) and
     return, per pod in order, the container env the device plugin's ``Allocate`` hands kubelet."""
     from ..device.protos import dp
-    from ..device.slicing_client import MemorySliceStore
-    from ..deviceplugin.server import SliceDevicePlugin
-    from ..models.slicing.cumask import place
-    from ..models.slicing.profile import as_resource_name
-    wanted = [(f"{BDF}::s{i}", p) for i, p in enumerate(profiles)]
-    slices = place([], wanted, cu_count)
-    store = MemorySliceStore()
-    store.save({0: slices})
-    by_id = {s.id: s for s in slices}
+    wanted, by_id, store = _place(profiles, cu_count)
     envs = []
     for sid, prof in wanted:
-        plug = SliceDevicePlugin(as_resource_name(prof), store, {0: "/dev/dri/renderD128"}, cu_count=cu_count,
-                                 shim_path=shim_path, socket_dir="/tmp")
         req = dp.AllocateRequest()
         req.container_requests.add(devicesIDs=[by_id[sid].id])
-        env = dict(plug.Allocate(req, None).container_responses[0].envs)
+        env = dict(_plugin(prof, store, cu_count, shim_path).Allocate(req, None).container_responses[0].envs)
         if not shim:
             env.pop("LD_PRELOAD", None)
         envs.append(env)
@@ -72,12 +79,27 @@ def allocate_envs(profiles: Sequence[str], cu_count: int = 256, shim: bool = Tru
 def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, census: bool = False,
              graphs: bool = True, ready_timeout: float = 600.0, extra_env: Optional[Dict[str, str]] = None,
              cu_count: int = 256, stagger_s: float = 0.0,
-             per_pod_env: Optional[Sequence[Dict[str, str]]] = None, sequential: bool = False) -> Dict[str, Any]:
+             per_pod_env: Optional[Sequence[Dict[str, str]]] = None, sequential: bool = False,
+             gate: bool = False, churn: Optional[Tuple[Sequence[int], Sequence[str]]] = None,
+             gate_timeout: float = 20.0) -> Dict[str, Any]:
     """Start one process per profile, release them together, collect their JSON lines.
     ``stagger_s``: wait this long between pod starts (pods of a node start at different times);
     ``per_pod_env``: env overrides of pod i (after ``extra_env``); ``sequential``: start pod i+1
-    only once pod i is READY (its queues exist), so the pods' start order is their index."""
-    envs = allocate_envs(profiles, cu_count, shim)
+    only once pod i is READY (its queues exist), so the pods' start order is their index.
+    ``gate``: start every pod at once, as kubelet starts a Deployment, each through the slice
+    plugin's ``PreStartContainer`` with one start gate for the GPU (``deviceplugin/startgate.py``,
+    its real KFD readiness probe): the order is whatever the gate imposes. ``churn``: (indices,
+    profiles) — once the first pods are READY, stop those pods and start new ones of those profiles
+    (through the gate when ``gate``; the indices are then positions in the gate's start order, so
+    "three pods of one start parity" is ``[0, 2, 4]``); the window measures the pods running after
+    the churn."""
+    from ..device.protos import dp
+    from ..deviceplugin.startgate import StartGate
+    new_profiles = list(churn[1]) if churn else []
+    all_profiles = list(profiles) + new_profiles
+    envs = allocate_envs(all_profiles, cu_count, shim)
+    wanted, _, store = _place(all_profiles, cu_count)
+    start_gate = StartGate(timeout=gate_timeout) if gate else None
     pods: List[PodProc] = []
     base = dict(os.environ)
     base["PYTHONPATH"] = ROOT + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
@@ -88,39 +110,90 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
     if not graphs:
         cmd.append("--no-graph")
     import tempfile
-    logs = []
-    try:
-        for i, (prof, env) in enumerate(zip(profiles, envs)):
-            e = {**base, **env, "NOS_POD_SEED": str(i), **(extra_env or {}),  # extra_env overrides Allocate's
-                 **(per_pod_env[i] if per_pod_env and i < len(per_pod_env) else {})}
-            log = tempfile.TemporaryFile(mode="w+")  # a full stderr pipe would stall the pod
-            logs.append(log)
-            p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
-                                 stderr=log, text=True)
-            pods.append(PodProc(PodSpec(prof, f"pod{i}"), env.get("NOS_SLICE_IDS", ""), env, p))
+    import threading
+    logs: List[Any] = [None] * len(all_profiles)
+    procs: List[Optional[PodProc]] = [None] * len(all_profiles)
+    waited: List[float] = [0.0] * len(all_profiles)
+
+    def start(i: int) -> None:
+        prof, env = all_profiles[i], envs[i]
+        if start_gate is not None:
+            req = dp.PreStartContainerRequest(devicesIDs=[env.get("NOS_SLICE_IDS", "")])
+            t0 = time.time()
+            _plugin(prof, store, cu_count, SHIM, start_gate).PreStartContainer(req, None)
+            waited[i] = time.time() - t0
+        e = {**base, **env, "NOS_POD_SEED": str(i), **(extra_env or {}),  # extra_env overrides Allocate's
+             **(per_pod_env[i] if per_pod_env and i < len(per_pod_env) else {})}
+        log = tempfile.TemporaryFile(mode="w+")  # a full stderr pipe would stall the pod
+        logs[i] = log
+        p = subprocess.Popen(cmd, cwd=ROOT, env=e, stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                             stderr=log, text=True)
+        procs[i] = PodProc(PodSpec(prof, f"pod{i}"), env.get("NOS_SLICE_IDS", ""), env, p)
+
+    def start_all(idx: Sequence[int]) -> None:
+        if gate:                        # every container asks at once, the gate orders them
+            ts = [threading.Thread(target=start, args=(i,)) for i in idx]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            return
+        for i in idx:
+            start(i)
             if sequential:
-                _wait_ready(pods[-1:], pods, logs, ready_timeout)
+                _wait_ready([procs[i]], [p for p in procs if p], _live(logs), ready_timeout)
             if stagger_s > 0:
                 time.sleep(stagger_s)
-        _wait_ready([p for p in pods if not sequential], pods, logs, ready_timeout)
+
+    stopped: List[int] = list(churn[0]) if churn else []
+    try:
+        first = list(range(len(profiles)))
+        start_all(first)
+        live = [procs[i] for i in first]
+        _wait_ready([p for p in live if not sequential or gate], live, [logs[i] for i in first], ready_timeout)
+        if churn:
+            if gate:                    # start-order positions -> pod indices (slice s<i> is pod i)
+                order = [int(sid.rsplit("::s", 1)[1]) for _, sid in start_gate.order]
+                stopped = [order[k] for k in stopped]
+            for i in stopped:
+                procs[i].proc.kill()
+                procs[i].proc.wait()
+            later = list(range(len(profiles), len(all_profiles)))
+            start_all(later)
+            _wait_ready([procs[i] for i in later], [procs[i] for i in later], [logs[i] for i in later],
+                        ready_timeout)
+        running = [i for i in range(len(all_profiles)) if procs[i] is not None and i not in stopped]
         go = time.time() + 1.0
-        for p in pods:
-            p.proc.stdin.write(f"GO {go:.6f}\n")
-            p.proc.stdin.flush()
-        for i, p in enumerate(pods):
+        for i in running:
+            procs[i].proc.stdin.write(f"GO {go:.6f}\n")
+            procs[i].proc.stdin.flush()
+        for i in running:
+            p = procs[i]
             out, _ = p.proc.communicate(timeout=seconds + 300)
             line = next((ln for ln in reversed(out.splitlines()) if ln.startswith("{")), None)
             if p.proc.returncode != 0 or line is None:
                 raise RuntimeError(f"{p.spec.name} failed (rc={p.proc.returncode}): {_tail(logs[i])}")
             p.result = json.loads(line)
     finally:
-        for p in pods:
-            if p.proc is not None and p.proc.poll() is None:
+        for p in procs:
+            if p is not None and p.proc.poll() is None:
                 p.proc.kill()
                 p.proc.wait()
         for log in logs:
-            log.close()
-    return summarize(pods, seconds)
+            if log is not None:
+                log.close()
+    out = summarize([procs[i] for i in running], seconds)
+    if gate:
+        order = [s for _, s in start_gate.order]
+        out["gate"] = {"order": order, "waited_s": [round(waited[i], 3) for i in range(len(all_profiles))],
+                       "timeouts": start_gate.timeouts}
+    if churn:
+        out["churn"] = {"stopped": stopped, "started": list(range(len(profiles), len(all_profiles)))}
+    return out
+
+
+def _live(logs: List[Any]) -> List[Any]:
+    return [log for log in logs if log is not None]
 
 
 def _tail(log) -> str:
@@ -132,6 +205,7 @@ def _wait_ready(subset: List[PodProc], pods: List[PodProc], logs: list, timeout:
     """Until every pod of ``subset`` printed READY (a pod that exits first raises with its log)."""
     deadline = time.time() + timeout
     waiting = {id(p.proc.stdout): p for p in subset}
+    index = {id(p): i for i, p in enumerate(pods)}
     while waiting:
         left = deadline - time.time()
         if left <= 0:
@@ -142,8 +216,9 @@ def _wait_ready(subset: List[PodProc], pods: List[PodProc], logs: list, timeout:
             ln = f.readline()
             if not ln:
                 pod.proc.wait()
+                log = logs[index[id(pod)]] if index.get(id(pod), len(logs)) < len(logs) else None
                 raise RuntimeError(f"{pod.spec.name} exited before READY (rc={pod.proc.returncode}): "
-                                   f"{_tail(logs[pods.index(pod)])}")
+                                   f"{_tail(log) if log is not None else ''}")
             if ln.strip() == "READY":
                 del waiting[id(f)]
 

@@ -43,6 +43,7 @@ from ..device.protos import dp
 from ..device.slicing_client import SliceStore
 from ..models.slicing.cumask import Slice, cus_of, hsa_cu_mask
 from ..models.slicing.profile import as_resource_name, extract_gpu_id
+from .startgate import StartGate
 
 log = logging.getLogger("nos.deviceplugin")
 
@@ -110,9 +111,16 @@ class PluginServer:
             self._version += 1
             self._changed.notify_all()
 
+    #: kubelet calls PreStartContainer before each container of this resource starts
+    pre_start_required = False
+
+    def options(self) -> Any:
+        return dp.DevicePluginOptions(pre_start_required=self.pre_start_required,
+                                      get_preferred_allocation_available=True)
+
     # -- gRPC handlers -------------------------------------------------------------------------
     def GetDevicePluginOptions(self, req, ctx):
-        return dp.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=True)
+        return self.options()
 
     def ListAndWatch(self, req, ctx):
         last: Optional[List[DeviceState]] = None
@@ -178,8 +186,7 @@ class PluginServer:
                                           request_serializer=dp.RegisterRequest.SerializeToString,
                                           response_deserializer=dp.Empty.FromString)
                     stub(dp.RegisterRequest(version=dp.VERSION, endpoint=os.path.basename(self.socket),
-                                            resource_name=self.resource_name,
-                                            options=dp.DevicePluginOptions(get_preferred_allocation_available=True)),
+                                            resource_name=self.resource_name, options=self.options()),
                          timeout=timeout)
                 self.registered_inode = _inode(kubelet_socket)
                 self.registrations += 1
@@ -218,7 +225,8 @@ class SliceDevicePlugin(PluginServer):
     def __init__(self, resource_name: str, store: SliceStore, gpu_render_nodes: Dict[int, str],
                  cu_count: int = 256, shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so",
                  socket_dir: str = DEVICE_PLUGIN_DIR, poll_interval: float = 1.0,
-                 device_map: Optional[Callable[[], Any]] = None, shared_hw_queues: int = -1):
+                 device_map: Optional[Callable[[], Any]] = None, shared_hw_queues: int = -1,
+                 start_gate: Optional[StartGate] = None):
         super().__init__(resource_name, socket_dir, poll_interval)
         self.store = store
         self.render = gpu_render_nodes
@@ -226,6 +234,9 @@ class SliceDevicePlugin(PluginServer):
         self.shim_path = shim_path
         self.device_map = device_map
         self.shared_hw_queues = shared_hw_queues
+        #: memory-only containers of one GPU start one after another (deviceplugin/startgate.py)
+        self.start_gate = start_gate
+        self.pre_start_required = start_gate is not None
 
     # -- device view ------------------------------------------------------------------------
     def _map(self) -> Any:
@@ -270,6 +281,18 @@ class SliceDevicePlugin(PluginServer):
         gpu = next((g for g, ss in slices.items() if any(s.id == mine[0].id for s in ss)), None) if mine else None
         n = sum(1 for s in slices.get(gpu, []) if not s.rows)
         return 2 if n <= 3 else 1
+
+    def PreStartContainer(self, req, ctx):
+        """Memory-only slices pass the start gate of their GPU: the container starts once the
+        previous memory-only container of that GPU has its compute queues (or the gate's timeout);
+        dedicated-CU slices start at once."""
+        if self.start_gate is not None:
+            slices = self.store.load()
+            by_id = {s.id: (g, s) for g, ss in slices.items() for s in ss}
+            mine = [by_id[d] for d in req.devicesIDs if d in by_id]
+            if mine and all(not s.rows for _, s in mine):
+                self.start_gate.enter(mine[0][0], [s.id for _, s in mine])
+        return dp.PreStartContainerResponse()
 
     def GetPreferredAllocation(self, req, ctx):
         gpu_of = {s.id: g for g, ss in self.store.load().items() for s in ss}
@@ -374,9 +397,11 @@ class PluginManager:
                  shim_path: str = "/usr/lib/nos/libnos_hbmlimit.so", device_map: Optional[Callable[[], Any]] = None,
                  resources: Optional[Callable[[], List[str]]] = None,
                  factory: Optional[Callable[[str], PluginServer]] = None,
-                 register_attempts: int = 5, register_backoff: float = 0.5, shared_hw_queues: int = -1):
+                 register_attempts: int = 5, register_backoff: float = 0.5, shared_hw_queues: int = -1,
+                 start_gate: Optional[StartGate] = None):
         self.store = store
         self.shared_hw_queues = shared_hw_queues
+        self.start_gate = start_gate   # one gate for every slice resource of the node
         self.render = gpu_render_nodes or {}
         self.socket_dir = socket_dir
         self.kubelet_socket = kubelet_socket
@@ -395,7 +420,8 @@ class PluginManager:
 
     def _slice_plugin(self, r: str) -> PluginServer:
         return SliceDevicePlugin(r, self.store, self.render, self.cu_count, self.shim_path, self.socket_dir,
-                                 device_map=self.device_map, shared_hw_queues=self.shared_hw_queues)
+                                 device_map=self.device_map, shared_hw_queues=self.shared_hw_queues,
+                                 start_gate=self.start_gate)
 
     def sync(self, attempts: Optional[int] = None) -> None:
         """``attempts``: registration attempts per plugin this call (default: the manager's); the

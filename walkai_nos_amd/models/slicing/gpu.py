@@ -17,15 +17,11 @@ from ...kube import objects as ko
 from .. import annotation as ann
 from .. import gpu_util
 from .. import resource as res
+from ..defaults import LIBRARY_DEFAULTS, ModelDefaults
 from ..geometry import Geometry
 from . import profile as _profile
 from .profile import (CU_GRANULARITY, MAX_SLICES_PER_GPU, MIN_SHARED_CUS, MIN_SLICE_MEMORY_GB, as_resource_name,
                       extract_profile_name, is_slice_resource, parse_profile)
-
-
-def set_skip_shared_counts(counts) -> None:
-    """The partitioner's ``sharedSliceSkipCounts`` (see :data:`~.profile.SKIP_SHARED_COUNTS`)."""
-    _profile.SKIP_SHARED_COUNTS = tuple(sorted({int(c) for c in counts}))
 
 
 @dataclass
@@ -39,7 +35,8 @@ class SlicingGPU:
     #: slices the planner may carve on this GPU (each serves one pod process; beyond 8 the hardware
     #: scheduler time-slices processes, :data:`~.profile.MAX_SLICES_PER_GPU`)
     max_slices: int = MAX_SLICES_PER_GPU
-    #: memory-only slice counts never left on the GPU (None: :data:`~.profile.SKIP_SHARED_COUNTS`)
+    #: memory-only slice counts never left on the GPU (None: :data:`~.profile.SKIP_SHARED_COUNTS`; a
+    #: planner's node models carry its ``ModelDefaults.shared_skip_counts``)
     skip_shared: Optional[Tuple[int, ...]] = None
 
     @classmethod
@@ -240,8 +237,10 @@ class SlicingNode:
         raise ValueError("not enough free slices")
 
 
-def new_node(node: Dict[str, Any]) -> SlicingNode:
-    """Reference ``slicing.NewNode`` (node.go:48-105): also needs the GPU memory label."""
+def new_node(node: Dict[str, Any], defaults: Optional[ModelDefaults] = None) -> SlicingNode:
+    """Reference ``slicing.NewNode`` (node.go:48-105): also needs the GPU memory label. Every GPU
+    carries ``defaults.shared_skip_counts`` (the owning planner's; none given: the library default)."""
+    skip = (defaults or LIBRARY_DEFAULTS).shared_skip_counts
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
     mem = gpu_util.get_memory_gb(node)
@@ -252,11 +251,12 @@ def new_node(node: Dict[str, Any]) -> SlicingNode:
     for idx, items in sorted(ann.group_by_gpu_index(status).items()):
         used = {a.profile: a.quantity for a in items if a.is_used()}
         free = {a.profile: a.quantity for a in items if a.is_free()}
-        g = SlicingGPU(model, idx, mem, cus, used, free, cap)
+        g = SlicingGPU(model, idx, mem, cus, used, free, cap, skip)
         g.validate()
         gpus[idx] = g
     for i in range(count):
-        gpus.setdefault(i, SlicingGPU.full(model, i, mem, cus, cap))
+        if i not in gpus:
+            gpus[i] = SlicingGPU(model, i, mem, cus, max_slices=cap, skip_shared=skip)
     return SlicingNode(ko.name(node), [gpus[i] for i in sorted(gpus)], res.from_k8s(ko.node_allocatable(node)))
 
 

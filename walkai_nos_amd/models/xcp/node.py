@@ -7,13 +7,14 @@ The allowed geometries are the model's geometries for the node's current NPS mod
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Mapping
+from typing import Any, Dict, List, Mapping, Optional
 
 from ...api import v1alpha1 as api
 from ...kube import objects as ko
 from .. import annotation as ann
 from .. import gpu_util
 from .. import resource as res
+from ..defaults import LIBRARY_DEFAULTS, ModelDefaults
 from ..partitioned import PartitionedGPU, PartitionedNode
 from .known_configs import get_allowed_geometries
 from .profile import as_resource_name, extract_profile_name, is_xcp_resource
@@ -36,23 +37,13 @@ def fraction_weight(profile: str) -> float:
 SCORING = {"pods": None, "fraction": fraction_weight}
 
 
-#: layout of a node without the ``nos.nebuly.com/xcp-layout`` label (the partitioner's
-#: ``defaultXcpLayout``, set once at start-up by ``cmd/gpupartitioner.py``)
-DEFAULT_LAYOUT = LAYOUT_PARTITIONS
-
-
-def set_default_layout(layout: str) -> None:
-    global DEFAULT_LAYOUT
-    if layout not in LAYOUTS:
-        raise ValueError(f"unknown xcp layout {layout!r}")
-    DEFAULT_LAYOUT = layout
-
-
-def get_layout(node: Dict[str, Any]) -> str:
-    """The node's ``nos.nebuly.com/xcp-layout`` (absent: :data:`DEFAULT_LAYOUT`; unknown values:
-    hardware partitions only). Slices need NPS1 (a sliced GPU is in SPX, which other memory modes
-    do not offer)."""
-    v = (ko.labels(node).get(api.LABEL_XCP_LAYOUT) or DEFAULT_LAYOUT).lower()
+def get_layout(node: Dict[str, Any], default: str = LAYOUT_PARTITIONS) -> str:
+    """The node's ``nos.nebuly.com/xcp-layout`` (absent: ``default`` — the owning planner's
+    ``ModelDefaults.xcp_layout``; unknown values: hardware partitions only). Slices need NPS1 (a
+    sliced GPU is in SPX, which other memory modes do not offer)."""
+    if default not in LAYOUTS:
+        raise ValueError(f"unknown xcp layout {default!r}")
+    v = (ko.labels(node).get(api.LABEL_XCP_LAYOUT) or default).lower()
     if v not in LAYOUTS or gpu_util.get_memory_partition(node) != SLICE_NPS:
         return LAYOUT_PARTITIONS
     return v
@@ -72,13 +63,16 @@ def degraded_gpus(annotations: Mapping[str, str]) -> Dict[int, str]:
     return out
 
 
-def new_node(node: Dict[str, Any], scoring: str = "fraction") -> PartitionedNode:
+def new_node(node: Dict[str, Any], scoring: str = "fraction", defaults: Optional[ModelDefaults] = None) -> PartitionedNode:
+    """The node's model; an unlabeled node takes ``defaults.xcp_layout`` (the planner's; none given:
+    the library default, hardware partitions)."""
+    defaults = defaults or LIBRARY_DEFAULTS
     model = gpu_util.get_model(node)
     count = gpu_util.get_count(node)
     nps = gpu_util.get_memory_partition(node)
     anns = ko.annotations(node)
     status, spec = ann.parse_node_annotations(anns)
-    layout = get_layout(node)
+    layout = get_layout(node, defaults.xcp_layout)
     sliced_now = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_STATUS)) if layout != LAYOUT_PARTITIONS else set()
     sliced_spec = parse_gpu_set(anns.get(api.ANNOTATION_SLICED_GPUS_SPEC))
     gpus: Dict[int, PartitionedGPU] = {}

@@ -180,6 +180,17 @@ def set_attention_x3_group(g: int) -> None:
     _x3_wg = None
 
 
+def set_attention_x3_wide(on: bool) -> None:
+    """fp32-input 8-tile attention: True (``NOS_ATTN_WIDE=1``) runs ``attn_fwd_x3w`` — one wave per
+    SIMD carrying two 32-query tiles — False (default) the two-waves-per-SIMD ``attn_fwd_x3p<8>``.
+    Same units, partials and per-tile arithmetic: the outputs are bit-identical."""
+    _check(_L().nos_attention_x3_set_wide(1 if on else 0))
+
+
+def attention_x3_wide() -> bool:
+    return bool(_L().nos_attention_x3_wide())
+
+
 def attention_x3_group() -> int:
     return int(_L().nos_attention_x3_group())
 
@@ -371,6 +382,7 @@ def _L() -> ctypes.CDLL:
             L.nos_split3_f32.argtypes = [vp, vp, ctypes.c_size_t, vp]
             L.nos_attention_x3_set_pipelined.argtypes = [i32]
             L.nos_attention_x3_set_group.argtypes = [i32]
+            L.nos_attention_x3_set_wide.argtypes = [i32]
             L.nos_attention_x3_sk.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                                                     i32, vp]

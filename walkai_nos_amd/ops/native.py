@@ -24,7 +24,9 @@ class NativeUnavailable(RuntimeError):
 
 
 def lib_path(name: str) -> str:
-    return os.path.join(NATIVE_DIR, name)
+    # NOS_NATIVE_DIR: an alternative build of the same libraries (A/B timing runs only; such a build
+    # is not stamp-verified, so it also needs NOS_ALLOW_STALE_NATIVE=1)
+    return os.path.join(os.environ.get("NOS_NATIVE_DIR") or NATIVE_DIR, name)
 
 
 def available(name: str) -> bool:

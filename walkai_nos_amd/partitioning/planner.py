@@ -113,10 +113,11 @@ class NodeInitializer:
     """C5: initialise GPUs that have no geometry yet with the fewest-slices geometry."""
 
     def __init__(self, client: Any, partitioner: Optional[Partitioner] = None,
-                 clock: Callable[[], float] = time.time):
+                 clock: Callable[[], float] = time.time, defaults: Any = None):
         self.client = client
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
+        self.defaults = defaults  # the planner's ModelDefaults (None: the library defaults)
 
     def init_node_partitioning(self, node: Dict[str, Any]) -> bool:
         from ..models.geometry import get_partitioning_kind
@@ -125,7 +126,7 @@ class NodeInitializer:
 
         kind = get_partitioning_kind(ko.labels(node))
         if kind == api.PARTITIONING_KIND_XCP:
-            model = xcp_node.new_node(node)
+            model = xcp_node.new_node(node, defaults=self.defaults)
             changed = False
             for g in model.gpus:
                 if not g.geometry():
@@ -138,7 +139,7 @@ class NodeInitializer:
         if kind == api.PARTITIONING_KIND_CUMASK:
             # a fresh CU-mask GPU has no slices: publish an explicit empty spec so the node counts as
             # initialised, i.e. every GPU index appears in the spec (one whole-GPU slice each)
-            smodel = slicing_gpu.new_node(node)
+            smodel = slicing_gpu.new_node(node, self.defaults)
             changed = False
             for g in smodel.gpus:
                 if not g.geometry():
