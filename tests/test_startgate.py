@@ -100,7 +100,7 @@ def test_slice_plugin_asks_for_prestart_and_gates_only_memory_only_slices():
     store.save({0: slices})
     seen = []
     gate = StartGate(ready=lambda s: True, timeout=1.0)
-    gate.enter = lambda gpu, ids: seen.append((gpu, list(ids))) or 0.0
+    gate.enter = lambda gpu, ids, bdf=None: seen.append((gpu, list(ids), bdf)) or 0.0
     shared = SliceDevicePlugin("amd.com/gpu-16gb", store, {0: "/dev/dri/renderD128"}, socket_dir="/tmp",
                                start_gate=gate)
     assert shared.GetDevicePluginOptions(None, None).pre_start_required
@@ -108,7 +108,7 @@ def test_slice_plugin_asks_for_prestart_and_gates_only_memory_only_slices():
     shared.PreStartContainer(dp.PreStartContainerRequest(devicesIDs=["bdf::m1"]), None)
     ded = SliceDevicePlugin("amd.com/gpu-32cu.36gb", store, {}, socket_dir="/tmp", start_gate=gate)
     ded.PreStartContainer(dp.PreStartContainerRequest(devicesIDs=["bdf::d0"]), None)
-    assert seen == [(0, ["bdf::m1"])]
+    assert seen == [(0, ["bdf::m1"], "bdf")]
 
 
 def test_slice_agent_config_validates_the_gate():
@@ -118,3 +118,36 @@ def test_slice_agent_config_validates_the_gate():
     assert GpuAgentConfig().sharedSliceStartGateSeconds == 20.0
     with pytest.raises(ValueError):
         GpuAgentConfig(sharedSliceStartGateSeconds=45).validate()
+
+
+def test_kfd_probe_without_a_shared_pid_namespace(tmp_path):
+    """The agent's PIDs are not the KFD's (a PID namespace of its own): the previous container's
+    process is the one on its GPU that reached its queues since it was let through."""
+    from walkai_nos_amd.deviceplugin.startgate import KfdProbe, kfd_gpu_id
+    kfd, topo, proc = tmp_path / "kfd", tmp_path / "topo", tmp_path / "proc"
+    proc.mkdir()
+    for node, (gid, loc) in enumerate((("0", 0), ("17010", (0x65 << 8)), ("9999", (0x75 << 8)))):
+        d = topo / str(node)
+        d.mkdir(parents=True)
+        (d / "gpu_id").write_text(gid + "\n")
+        (d / "properties").write_text(f"cpu_cores_count 0\nlocation_id {loc}\ndomain 0\n")
+    assert kfd_gpu_id("0000:65:00.0", str(topo)) == "17010" and kfd_gpu_id("0000:99:00.0", str(topo)) is None
+
+    def add(pid, gid, types):
+        for i, t in enumerate(types):
+            q = kfd / str(pid) / "queues" / str(i)
+            q.mkdir(parents=True)
+            (q / "type").write_text(t)
+            (q / "gpuid").write_text(gid)
+    add(500, "17010", ["0", "0", "1"])           # an older pod, ready
+    p = KfdProbe(proc=str(proc), kfd=str(kfd), topology=str(topo))
+    bdf = "0000:65:00.0"
+    snap = p.snapshot(bdf)
+    assert snap == {500}
+    assert not p.ready("bdf::s1", bdf, snap)
+    add(777, "9999", ["0", "0"])                 # another GPU's process: not ours
+    assert not p.ready("bdf::s1", bdf, snap)
+    add(600, "17010", ["0"])                     # ours, one queue so far
+    assert not p.ready("bdf::s1", bdf, snap)
+    add(601, "17010", ["0", "0"])
+    assert p.ready("bdf::s1", bdf, snap)

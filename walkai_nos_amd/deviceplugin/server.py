@@ -291,7 +291,7 @@ class SliceDevicePlugin(PluginServer):
             by_id = {s.id: (g, s) for g, ss in slices.items() for s in ss}
             mine = [by_id[d] for d in req.devicesIDs if d in by_id]
             if mine and all(not s.rows for _, s in mine):
-                self.start_gate.enter(mine[0][0], [s.id for _, s in mine])
+                self.start_gate.enter(mine[0][0], [s.id for _, s in mine], bdf=extract_gpu_id(mine[0][1].id))
         return dp.PreStartContainerResponse()
 
     def GetPreferredAllocation(self, req, ctx):

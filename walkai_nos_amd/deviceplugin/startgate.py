@@ -12,11 +12,16 @@ their queue creation, and one run of eight dealt one pod a pipe of its own, 115 
 kubelet starts the pods of a Deployment concurrently, so the order has to be imposed by the node:
 the slice device plugin asks kubelet for ``PreStartContainer`` (``pre_start_required``) and its
 handler passes every memory-only container through this gate. Per GPU, a container is let through
-once the previous memory-only container let through on that GPU is *ready* — its process (found by
-the ``NOS_SLICE_IDS`` its ``Allocate`` env carries) has its compute queues in the KFD
-(``/sys/class/kfd/kfd/proc/<pid>/queues/*/type`` = 0) — or after ``timeout`` seconds (a container
-that never opens the GPU, or one that failed, does not hold the others back for longer; kubelet
-gives the call 30 s). Dedicated-CU slices pass at once: their CUs are their own.
+once the previous memory-only container let through on that GPU is *ready* — it has its compute
+queues in the KFD (``/sys/class/kfd/kfd/proc/<pid>/queues/*/type`` = 0, on that GPU's KFD
+``gpuid``) — or ``timeout`` seconds after it was let through (a container that never opens the GPU,
+or one that failed, does not hold the others back for longer; kubelet gives the call 30 s).
+Dedicated-CU slices pass at once: their CUs are their own.
+
+Which KFD process is the previous container's: with hostPID (the agent's DaemonSet) the process
+whose environment carries the slice in ``NOS_SLICE_IDS``; where the agent's PIDs are not the KFD's
+(a PID namespace of its own), the first process on that GPU to reach its queues that was not there
+when the container was let through (:class:`KfdProbe`).
 
 Churn needs no extra rule: a departure removes its process's queues, and the next start through the
 gate is created after every running pod's queues, as at first start (``tests/test_gpu_native.py``
@@ -30,7 +35,7 @@ import logging
 import os
 import threading
 import time
-from typing import Callable, Dict, Iterable, List, Optional, Tuple
+from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
 
 log = logging.getLogger("nos.startgate")
 
@@ -78,22 +83,111 @@ def kfd_slice_ready(slice_id: str, min_queues: int = 2, proc: str = "/proc", kfd
     return any(kfd_compute_queues(pid, kfd) >= min_queues for pid in pids_with_slice(slice_id, proc))
 
 
+def kfd_gpu_id(bdf: str, topology: str = "/sys/class/kfd/kfd/topology/nodes") -> Optional[str]:
+    """The KFD ``gpu_id`` of the GPU at PCI ``bdf`` (``dddd:bb:dd.f``), from the topology nodes'
+    ``location_id`` (bus << 8 | device << 3 | function) and ``domain``; None when not found."""
+    try:
+        dom, bus, df = bdf.split(":")
+        dev, fn = df.split(".")
+        loc, domain = (int(bus, 16) << 8) | (int(dev, 16) << 3) | int(fn, 16), int(dom, 16)
+    except ValueError:
+        return None
+    for n in glob.glob(os.path.join(topology, "*")):
+        try:
+            with open(os.path.join(n, "gpu_id")) as f:
+                gid = f.read().strip()
+            with open(os.path.join(n, "properties")) as f:
+                props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+        except OSError:
+            continue
+        if gid and gid != "0" and int(props.get("location_id", -1)) == loc and int(props.get("domain", 0)) == domain:
+            return gid
+    return None
+
+
+class KfdProbe:
+    """Readiness of a container's GPU process from the KFD (module docstring)."""
+
+    def __init__(self, min_queues: int = 2, proc: str = "/proc", kfd: str = KFD_PROC,
+                 topology: str = "/sys/class/kfd/kfd/topology/nodes"):
+        self.min_queues = min_queues
+        self.proc, self.kfd, self.topology = proc, kfd, topology
+        self._gpu_ids: Dict[str, Optional[str]] = {}
+
+    def _gpu_id(self, bdf: Optional[str]) -> Optional[str]:
+        if not bdf:
+            return None
+        if bdf not in self._gpu_ids:
+            self._gpu_ids[bdf] = kfd_gpu_id(bdf, self.topology)
+        return self._gpu_ids[bdf]
+
+    def ready_pids(self, bdf: Optional[str] = None) -> frozenset:
+        """KFD processes with their compute queues (on the GPU at ``bdf`` when its gpu_id is known)."""
+        gid = self._gpu_id(bdf)
+        out = set()
+        for d in glob.glob(os.path.join(self.kfd, "*")):
+            pid = os.path.basename(d)
+            if not pid.isdigit():
+                continue
+            n = 0
+            for q in glob.glob(os.path.join(d, "queues", "*")):
+                try:
+                    with open(os.path.join(q, "type")) as f:
+                        if f.read().strip() != KFD_COMPUTE:
+                            continue
+                    if gid is not None:
+                        with open(os.path.join(q, "gpuid")) as f:
+                            if f.read().strip() != gid:
+                                continue
+                except OSError:
+                    continue
+                n += 1
+            if n >= self.min_queues:
+                out.add(int(pid))
+        return frozenset(out)
+
+    def snapshot(self, bdf: Optional[str]) -> frozenset:
+        return self.ready_pids(bdf)
+
+    def ready(self, slice_id: str, bdf: Optional[str], snap: frozenset) -> bool:
+        now = self.ready_pids(bdf)
+        mine = set(pids_with_slice(slice_id, self.proc))
+        if mine & now:
+            return True
+        # a PID namespace of our own: the container's process is the one that appeared since
+        return bool(now - snap - mine)
+
+
+class _CallableProbe:
+    def __init__(self, fn: Callable[[str], bool]):
+        self.fn = fn
+
+    def snapshot(self, bdf: Optional[str]) -> frozenset:
+        return frozenset()
+
+    def ready(self, slice_id: str, bdf: Optional[str], snap: frozenset) -> bool:
+        return self.fn(slice_id)
+
+
 class StartGate:
     """Per-GPU FIFO of memory-only container starts (module docstring).
 
-    ``ready(slice_id)``: whether the container of that slice has its queues (default: the KFD
-    probe); ``timeout``: longest wait for the previous container, seconds."""
+    ``probe``: readiness of a let-through container (default :class:`KfdProbe`); ``ready``: a plain
+    ``slice_id -> bool`` instead (tests); ``timeout``: longest hold, seconds after the previous
+    container was let through."""
 
     def __init__(self, ready: Optional[Callable[[str], bool]] = None, timeout: float = 20.0, poll: float = 0.05,
-                 clock: Callable[[], float] = time.monotonic, sleep: Callable[[float], None] = time.sleep):
-        self.ready = ready or kfd_slice_ready
+                 clock: Callable[[], float] = time.monotonic, sleep: Callable[[float], None] = time.sleep,
+                 probe: Any = None):
+        self.probe = probe or (_CallableProbe(ready) if ready is not None else KfdProbe())
         self.timeout = timeout
         self.poll = poll
         self.clock = clock
         self.sleep = sleep
         self._locks: Dict[int, threading.Lock] = {}
         self._guard = threading.Lock()
-        self._last: Dict[int, Tuple[str, float]] = {}  # GPU -> (slice of the last container let through, when)
+        # GPU -> (slice of the last container let through, when, its GPU's BDF, KFD snapshot then)
+        self._last: Dict[int, Tuple[str, float, Optional[str], frozenset]] = {}
         self.order: List[Tuple[int, str]] = []  # (GPU, slice) in the order they were let through
         self.waits = 0
         self.timeouts = 0
@@ -103,10 +197,11 @@ class StartGate:
         with self._guard:
             return self._locks.setdefault(gpu, threading.Lock())
 
-    def enter(self, gpu: int, slice_ids: Iterable[str]) -> float:
+    def enter(self, gpu: int, slice_ids: Iterable[str], bdf: Optional[str] = None) -> float:
         """Block until the previous memory-only container of ``gpu`` is ready, or ``timeout``
         seconds after it was let through (a container let through long ago — a churn start — holds
-        nothing back), then record ``slice_ids`` as the last one; returns the seconds waited."""
+        nothing back), then record ``slice_ids`` as the last one; returns the seconds waited.
+        ``bdf``: the GPU's PCI address (the slice ids' prefix), for the KFD probe's GPU filter."""
         ids = list(slice_ids)
         with self._lock(gpu):
             prev = self._last.get(gpu)
@@ -114,12 +209,14 @@ class StartGate:
             waited, timed_out = 0.0, False
             if prev is not None and prev[0] not in ids:
                 deadline = prev[1] + self.timeout
-                while self.clock() < deadline and not self.ready(prev[0]):
+                ok = self.probe.ready(prev[0], prev[2], prev[3])
+                while not ok and self.clock() < deadline:
                     self.sleep(self.poll)
-                timed_out = self.clock() >= deadline and not self.ready(prev[0])
+                    ok = self.probe.ready(prev[0], prev[2], prev[3])
+                timed_out = not ok
                 waited = self.clock() - t0
             if ids:
-                self._last[gpu] = (ids[0], self.clock())
+                self._last[gpu] = (ids[0], self.clock(), bdf, self.probe.snapshot(bdf))
             self.order.append((gpu, ids[0] if ids else ""))
             self.waits += 1 if waited > 0 else 0
             self.timeouts += 1 if timed_out else 0
