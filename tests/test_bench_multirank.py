@@ -136,4 +136,17 @@ def test_bench_py_eight_rank_rehearsal_prints_one_json_line():
     assert out["n_gpus"] == 8 and out["steps"] == 20 and out["warmup"] == 5
     assert out["data"].startswith("REHEARSAL") and out["value"] > 0
     assert out["gpu_utilization_pct"] > 50 and out["config"]["parallelism"].endswith("8 GPU node")
+    # who ran is readable from the JSON
+    d = out["dist"]
+    assert d["backend"] == "gloo" and d["world_size"] == 8
+    assert sorted(r["rank"] for r in d["ranks"]) == list(range(8))
+    assert sorted(r["local_rank"] for r in d["ranks"]) == list(range(8))
+    # BASELINE config 4 beside the headline: the same window on hardware partitions, its own clock
+    pw = out["partitions_window"]
+    assert pw["layout"] == "partitions" and pw["value"] > 0 and pw["window_s"] > 0
+    assert pw["flips"] >= 0 and "time_in_flip_pct" in pw and pw["commit_barriers"] >= pw["flips"] > 0
+    assert "estimated" in pw["flip_cost"] and set(pw["per_profile"]) == {"cpx_nps1", "dpx_nps1", "spx_nps1"}
+    # rank 0's post-window models ran within their budget (or say what they skipped)
+    pwb = out["post_window"]
+    assert pwb["budget_s"] == 60.0 and (pwb["spent_s"] <= pwb["budget_s"] + 60 or pwb["skipped"])
     assert wall < 600, wall

@@ -320,14 +320,19 @@ def test_detection_token_template_cached_per_parameter_version():
 
 
 def test_density_phase_control_plane_at_four_gpus():
-    # saturation through the real control plane: 8 CPX pods per GPU, 16 CU-mask pods per GPU on
-    # average (first-fit may leave the last GPU lighter: the minimum is reported beside the mean)
+    # saturation through the real control plane: 8 CPX pods per GPU; CU-mask slices at the chart's
+    # cap of 8 per GPU (what a default node schedules), and 16 per GPU only with the cap lifted by
+    # label, named so (first-fit may leave the last GPU lighter: the minimum is
+    # reported beside the mean)
     from walkai_nos_amd.bench_core import BenchConfig, density_phase
     d = density_phase(BenchConfig(gpus=4), None)
     assert d["xcp"]["pods_per_gpu"] == 8 and d["xcp"]["pending"] == 0 and d["xcp"]["pods_per_node"] == 32
     for v in ("cumask", "cumask_shared"):
+        assert d[v]["pending"] == 0 and d[v]["pods_per_node"] == 32 and d[v]["pods_per_gpu"] == 8
+        assert d[v]["max_slices_per_gpu"] == 8
+    for v in ("cumask_threads_cap_lifted", "cumask_shared_threads_cap_lifted"):
         assert d[v]["pending"] == 0 and d[v]["pods_per_node"] == 64 and d[v]["pods_per_gpu"] == 16
-        assert 0 < d[v]["pods_per_gpu_min"] <= 16
+        assert 0 < d[v]["pods_per_gpu_min"] <= 16 and "not what a default node schedules" in d[v]["served_as"]
 
 
 def test_inference_latency_summary_per_mode():

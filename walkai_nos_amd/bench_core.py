@@ -68,8 +68,16 @@ BASELINE_LABEL = "MPS 7-pod aggregate throughput on 1x A100-80GB (BASELINE.md), 
 MIX = (("cpx_nps1", 0.5), ("dpx_nps1", 0.3), ("spx_nps1", 0.2))
 
 #: CU-mask density phases: dedicated-CU slices plus memory-only slices on the shared rows, and
-#: memory-only slices alone (the reference's MPS semantics: HBM budgets, compute shared by all)
-CUMASK_DENSITY = {"cumask": (("32cu.24gb", 6), ("8gb", 10)), "cumask_shared": (("16gb", 16),)}
+#: memory-only slices alone (the reference's MPS semantics: HBM budgets, compute shared by all) —
+#: name -> (per-GPU mix, the node's nos.nebuly.com/max-slices-per-gpu or None for the chart default
+#: of 8). The default-cap rows are what a default-configured node schedules; the *_threads_cap_lifted
+#: rows lift the cap to 16 by label and serve the pods as threads of the bench process — as
+#: processes, past eight per GPU the hardware scheduler time-slices them (profiles/procs_cap_r4.json:
+#: 12 memory-only pods 292 inf/s against 383 at 8), so they are never a saturation figure
+CUMASK_DENSITY = {"cumask": ((("32cu.24gb", 4), ("8gb", 4)), None),
+                  "cumask_shared": ((("16gb", 8),), None),
+                  "cumask_threads_cap_lifted": ((("32cu.24gb", 6), ("8gb", 10)), 16),
+                  "cumask_shared_threads_cap_lifted": ((("16gb", 16),), 16)}
 
 
 #: How a compute partition is emulated on the SPX device (the box is not root, so modes cannot be
@@ -168,6 +176,7 @@ class BenchConfig:
     data_plane: bool = True              # False: a rehearsal of the launch path without a GPU (inferences
                                          # priced with MODE_RATES, never a measurement)
     commit_barrier_s: float = -1.0       # this run's measured node commit barrier (<0: the component constant)
+    partitions_window: bool = True       # also time the same window on hardware partitions (config 4)
     pod_start_s: float = -1.0            # cluster seconds a newly bound pod holds its slice before it serves
                                          # (<0: POD_START_S; bench.py measures it on the box before the window)
 
@@ -996,14 +1005,15 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
             dt = time.perf_counter() - t0
             out[name]["inf_per_s_per_gpu"] = round(sum(got.values()) / dt, 1)
             out[name]["per_pod"] = _per_pod_spread(got, keys, dt)
-    # CU-mask slices beyond 8 per GPU: the node is labelled to allow 16 (the default cap is 8
-    # because pods are processes and beyond 8 processes the hardware scheduler time-slices them,
-    # profiles/procs_cap_r4.json; the bench serves these pods as threads of one process)
-    for variant, mix in CUMASK_DENSITY.items():
+    # CU-mask slices at the chart's cap (8 per GPU), then beyond it with the cap lifted by label —
+    # the bench serves these pods as threads of one process; as processes, past 8 the hardware
+    # scheduler time-slices them (profiles/procs_cap_r4.json), which CUMASK_DENSITY's names say
+    for variant, (mix, cap) in CUMASK_DENSITY.items():
         c2 = SimCluster(n_nodes=1, gpus_per_node=cfg.gpus, refresh_interval=5.0, kind=api.PARTITIONING_KIND_CUMASK,
                         policy="fifo")
-        for n in c2.nodes:
-            c2.api.patch("Node", n, {"metadata": {"labels": {api.LABEL_MAX_SLICES_PER_GPU: "16"}}})
+        if cap is not None:
+            for n in c2.nodes:
+                c2.api.patch("Node", n, {"metadata": {"labels": {api.LABEL_MAX_SLICES_PER_GPU: str(cap)}}})
         c2.run(30)
         k = 0
         for _ in range(cfg.gpus):
@@ -1020,7 +1030,11 @@ def density_phase(cfg: BenchConfig, data: Optional[DataPlane], serve_s: float = 
         out[variant] = {"pods_per_gpu": round(sum(per_gpu2.values()) / cfg.gpus, 2),
                         "pods_per_gpu_min": min(per_gpu2.get(g, 0) for g in range(cfg.gpus)),
                         "pods_per_node": sum(per_gpu2.values()), "pending": len(c2.pending_pods()),
-                        "profiles": {p: n for p, n in mix}}
+                        "profiles": {p: n for p, n in mix},
+                        "max_slices_per_gpu": cap or 8,
+                        "served_as": "threads of the bench process" + (
+                            ": beyond the default cap of 8, not what a default node schedules; as processes "
+                            "the hardware time-slices past 8 (profiles/procs_cap_r4.json)" if cap else "")}
         if data is not None:
             slices = sn2.plugin.store.load().get(cfg.rank, [])
             mine = {d for devs in sn2.kubelet.allocations.values() for _, d in devs
@@ -1142,46 +1156,12 @@ def sustainable_load_row(cfg: BenchConfig, load: float = 0.85, seeds=(1, 2, 3, 4
             "pending_mean": round(_mean(pend), 2), "tts_p99_lifetimes_worst_seed": p99}
 
 
-def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
+def _timed_window(cfg: BenchConfig, bf: Any, gpu: bool, distributed: bool) -> Tuple[Any, float, float, Any, Any]:
+    """Preroll, warm-up and the timed window of ``cfg``'s layout on a fresh simulated node: returns
+    (the NodeBench, window seconds (max over ranks), inferences (sum over ranks), hardware busy %,
+    the busy sampler). Every rank runs it in lock-step (barriers around the window)."""
     import torch
     import torch.distributed as dist
-
-    if os.environ.get("NOS_X3_ABLATE", "0") != "0":
-        raise SystemExit("NOS_X3_ABLATE skips GEMM work (a timing-study switch): the bench refuses to run with it")
-
-    from .parallel.barrier import LocalBarrier, RankCommitBarrier
-
-    distributed = cfg.world > 1
-    gpu = cfg.data_plane
-    if cfg.flip_cost_default and gpu:
-        # charge flips this run's own commit barrier (the node's devices, spawned as the agent does)
-        measured = measure_commit_barrier() if cfg.rank == 0 else None
-        if distributed:
-            t = torch.tensor([measured if measured is not None else -1.0], dtype=torch.float64,
-                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
-            dist.broadcast(t, 0)
-            measured = float(t.item()) if t.item() >= 0 else None
-        if measured is not None:
-            cfg.commit_barrier_s = measured
-            cfg.flip_cost_s = default_flip_cost(measured)
-    pod_start = None
-    if cfg.pod_start_default and gpu:
-        # charge pods this box's own start-up (one pod process spawned as kubelet would, rank 0)
-        pod_start = measure_pod_start() if cfg.rank == 0 else None
-        ps = pod_start["pod_start_s"] if pod_start else -1.0
-        if distributed:
-            t = torch.tensor([ps], dtype=torch.float64,
-                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
-            dist.broadcast(t, 0)
-            ps = float(t.item())
-        if ps > 0:
-            cfg.pod_start_s = ps
-    if distributed:
-        # the agent's commit path (Actuator._commit -> barrier.vote_all(per-device votes)); each
-        # rank contributes the votes of its own GPU's partitions, all-reduced over RCCL
-        bf = lambda n: RankCommitBarrier(rank=cfg.rank, world=cfg.world)  # noqa: E731
-    else:
-        bf = lambda n: LocalBarrier(n)  # noqa: E731
     nb = NodeBench(cfg, barrier_factory=bf, gpu_data_plane=gpu)
 
     def sync() -> None:
@@ -1228,6 +1208,115 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
             nb.profile_inferences[p] = int(s[2 + i].item())
     else:
         total_inf = float(nb.inferences)
+    return nb, elapsed, total_inf, hw_busy, busy
+
+
+def partitions_window(cfg: BenchConfig, gpu: bool, distributed: bool) -> Dict[str, Any]:
+    """BASELINE config 4 beside the headline: the same seed's window on hardware compute partitions
+    (``--layout partitions``: SPX/DPX/QPX/CPX flips under churn, drains enforced by the partition
+    plugin, every flip through the node commit barrier and dark for the flip cost), on a fresh
+    node, timed by its own clock. The amd-smi setter needs root, which the box does not give, so the
+    flip's outage is the components' cost (``flip_cost.estimated`` names the estimated ones); the
+    flips, the drains and the commit barriers are the control plane's own."""
+    import dataclasses
+
+    from .parallel.barrier import LocalBarrier, RankCommitBarrier
+    c = dataclasses.replace(cfg, layout="partitions", density=False)
+    commits = [0]
+
+    def bf(n):
+        commits[0] += 1
+        return RankCommitBarrier(rank=c.rank, world=c.world) if distributed else LocalBarrier(n)
+    t0 = time.perf_counter()
+    nb, elapsed, total_inf, hw_busy, _ = _timed_window(c, bf, gpu, distributed)
+    try:
+        return {"layout": "partitions", "value": round(total_inf / elapsed, 3), "unit": "inferences/s",
+                "window_s": round(elapsed, 3), "wall_s_incl_setup": round(time.perf_counter() - t0, 1),
+                "gpu_utilization_pct": round(_mean(nb.util_samples), 2),
+                "allocation_pct_incl_outage": round(_mean(nb.raw_util_samples), 2),
+                "hw_busy_pct": hw_busy, "flips": nb.flips,
+                "time_in_flip_pct": round(100.0 * nb.outage_gpu_quanta / max(1, nb.gpu_quanta), 2),
+                "commit_barriers": commits[0], "flip_cost": flip_cost_report(c),
+                "pending_pods_mean": round(_mean(nb.pending_samples), 2),
+                "pods_per_node": round(_mean(nb.pods_samples), 2),
+                "per_profile": nb.profile_report(elapsed), "idle": nb.idle_report(),
+                "layout_drains": nb.data.drains if nb.data is not None else 0}
+    finally:
+        nb.close()
+
+
+def dist_report(cfg: BenchConfig, barrier_node: Optional[Dict[str, Any]]) -> Dict[str, Any]:
+    """Who ran: the process group's backend and size, each rank's LOCAL_RANK, the devices it sees
+    and the one it serves (gathered over the group), and the devices of the node commit barrier."""
+    import torch
+    import torch.distributed as dist
+    me = {"rank": cfg.rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+          "visible_devices": torch.cuda.device_count() if torch.cuda.is_available() else 0,
+          "device": torch.cuda.current_device() if torch.cuda.is_available() and cfg.data_plane else None,
+          "hip_visible_devices": os.environ.get("HIP_VISIBLE_DEVICES")}
+    ranks = [me]
+    backend = None
+    if cfg.world > 1 and dist.is_initialized():
+        backend = dist.get_backend()
+        ranks = [None] * cfg.world
+        dist.all_gather_object(ranks, me)
+    return {"backend": backend, "world_size": cfg.world, "ranks": ranks,
+            "commit_barrier_node_devices": (barrier_node or {}).get("devices")}
+
+
+#: wall seconds rank 0 may spend on the control-plane models after the windows (the other ranks
+#: wait): models past the budget are skipped and named in ``post_window.skipped``
+POST_WINDOW_BUDGET_S = {1: 120.0, 2: 120.0, 4: 90.0, 8: 60.0}
+
+
+def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
+    import torch
+    import torch.distributed as dist
+
+    if os.environ.get("NOS_X3_ABLATE", "0") != "0":
+        raise SystemExit("NOS_X3_ABLATE skips GEMM work (a timing-study switch): the bench refuses to run with it")
+
+    from .parallel.barrier import LocalBarrier, RankCommitBarrier
+
+    distributed = cfg.world > 1
+    gpu = cfg.data_plane
+    if cfg.flip_cost_default and gpu:
+        # charge flips this run's own commit barrier (the node's devices, spawned as the agent does)
+        measured = measure_commit_barrier() if cfg.rank == 0 else None
+        if distributed:
+            t = torch.tensor([measured if measured is not None else -1.0], dtype=torch.float64,
+                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, 0)
+            measured = float(t.item()) if t.item() >= 0 else None
+        if measured is not None:
+            cfg.commit_barrier_s = measured
+            cfg.flip_cost_s = default_flip_cost(measured)
+    pod_start = None
+    if cfg.pod_start_default and gpu:
+        # charge pods this box's own start-up (one pod process spawned as kubelet would, rank 0)
+        pod_start = measure_pod_start() if cfg.rank == 0 else None
+        ps = pod_start["pod_start_s"] if pod_start else -1.0
+        if distributed:
+            t = torch.tensor([ps], dtype=torch.float64,
+                             device=f"cuda:{torch.cuda.current_device()}" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, 0)
+            ps = float(t.item())
+        if ps > 0:
+            cfg.pod_start_s = ps
+    commits = [0]
+    if distributed:
+        # the agent's commit path (Actuator._commit -> barrier.vote_all(per-device votes)); each
+        # rank contributes the votes of its own GPU's partitions, all-reduced over RCCL
+        def bf(n):
+            commits[0] += 1
+            return RankCommitBarrier(rank=cfg.rank, world=cfg.world)
+    else:
+        def bf(n):
+            commits[0] += 1
+            return LocalBarrier(n)
+    t_run = time.perf_counter()
+    nb, elapsed, total_inf, hw_busy, busy = _timed_window(cfg, bf, gpu, distributed)
+    commits_main = commits[0]
     latency = inference_latency(nb.data)
     per_profile = nb.profile_report(elapsed)
     barrier_8dev = node_barrier_probe(cfg) if cfg.rank == 0 and gpu else None
@@ -1237,17 +1326,33 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
     util = _mean(nb.util_samples)
     raw = _mean(nb.raw_util_samples)
     pods = _mean(nb.pods_samples)
+    # BASELINE config 4 beside the headline (the sliced default): the same window on hardware partitions
+    part = partitions_window(cfg, gpu, distributed) if cfg.layout != "partitions" and cfg.partitions_window else None
+    dist_block = dist_report(cfg, barrier_8dev)
     from .models.workload.yolos import YolosSmall
     from .ops import kernels as K
     flops = YolosSmall().flops_per_inference(cfg.hw)
+    # rank 0's control-plane models, within a wall-clock budget (the other ranks wait for it)
+    budget = POST_WINDOW_BUDGET_S.get(cfg.gpus, 60.0)
+    t_post = time.perf_counter()
+    skipped: List[str] = []
+
+    def within(name: str, fn):
+        if cfg.rank != 0:
+            return {}
+        if time.perf_counter() - t_post > budget:
+            skipped.append(name)
+            return {"skipped": f"post-window budget of {budget:g} s spent"}
+        return fn()
     # a layout that flips is priced by its flips; sliced GPUs never flip, so their sensitivity is to
     # the pods' start-up instead
-    sens = (flip_sensitivity(cfg) if cfg.layout == "partitions" else pod_start_sensitivity(cfg)) \
-        if cfg.rank == 0 else {}
+    sens = within("sensitivity", lambda: flip_sensitivity(cfg) if cfg.layout == "partitions"
+                  else pod_start_sensitivity(cfg))
     # the window is one draw of the churn: its spread over other seeds (fewer on big nodes, whose
     # control plane takes longer per quantum)
-    seeds = seed_model(cfg, tuple(range(1, 11 if cfg.gpus <= 2 else 6))) if cfg.rank == 0 else {}
-    sustainable = sustainable_load_row(cfg) if cfg.rank == 0 else {}
+    seeds = within("seed_model", lambda: seed_model(cfg, tuple(range(1, 11 if cfg.gpus <= 2 else 6))))
+    sustainable = within("load_0.85", lambda: sustainable_load_row(cfg))
+    post = {"budget_s": budget, "spent_s": round(time.perf_counter() - t_post, 1), "skipped": skipped}
     life_s = cfg.mean_lifetime_quanta * cfg.cluster_s
     return {
         "metric": "aggregate GPU utilization % + schedulable pods/node, mixed fractional-GPU load",
@@ -1300,7 +1405,14 @@ def run_bench(cfg: BenchConfig) -> Dict[str, Any]:
         "seed_model": seeds,
         "load_0.85": sustainable,
         "commit_barrier_node": barrier_8dev,
-        "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items()},
+        "commit_barriers": commits_main,
+        "partitions_window": part,
+        "dist": dist_block,
+        "post_window": post,
+        "run_wall_s": round(time.perf_counter() - t_run, 1),
+        # what a default-configured node schedules (the chart's 8 slices per GPU); the beyond-the-cap
+        # figures are in ``density`` under *_threads_cap_lifted, labelled
+        "pods_per_gpu_saturation": {k: v["pods_per_gpu"] for k, v in density.items() if not k.endswith("_lifted")},
         "density": density,
         "achieved_tflops": round(value * flops / 1e12, 2),
         "host_ms_per_step": {k: round(1000.0 * v / cfg.steps, 2) for k, v in nb.host_s.items()},
