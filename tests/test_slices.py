@@ -385,31 +385,28 @@ def test_free_drain_reserves_room_no_waiting_pod_fits():
     assert run(False) is None
 
 
-def test_free_drain_lapses_when_a_smaller_pod_arrives_on_one_gpu():
-    """a free drain is held only while no waiting pod fits the GPU's room. On a one-GPU
-    cluster (where reservations are held) the free drain made for a half-GPU pod lapses on the next
-    pass once a 1/8 pod arrives that the free group fits — the small pod is placed at once."""
+def test_free_drain_is_held_on_small_clusters_and_lapses_on_bigger_ones():
+    """a free drain made on a one-GPU cluster is held like any reservation until a pod of
+    its profile is placed (a smaller pod arriving meanwhile waits — letting it lapse there measured
+    worse, sliced.py 3b); on a cluster of more sliced GPUs than ``slice_reserve_hold_max_gpus`` it is
+    re-decided each pass and lapses once the room fits a waiting pod."""
     p = PackParams(slice_reserve_after=900.0)
-    fd: set = set()                       # the controller's record of free drains, across passes
     g = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 7}, free={"cpx_nps1": 1})
-    ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"dpx_nps1": 1}, 10.0)], params=p, free_drains=fd)
+    ch = plan_cluster_pack({"n": _sliced_node(g)}, [({"dpx_nps1": 1}, 10.0)], params=p)
     assert ch["n"].gpus[0].target == {"cpx_nps1": 7, "dpx_nps1": 1}     # the free drain
-    assert fd == {("n", 0)}
 
-    def held():
-        h = new_sliced_gpu("MI355X", 0, used={"cpx_nps1": 7})
+    def held(i=0):
+        h = new_sliced_gpu("MI355X", i, used={"cpx_nps1": 7})
         h.target, h.target_sliced = {"cpx_nps1": 7, "dpx_nps1": 1}, True
         return h
-    # next pass: the model reports the reservation in force; a 1/8 pod now waits too
     pending = [({"dpx_nps1": 1}, 20.0), ({"cpx_nps1": 1}, 1.0)]
-    ch = plan_cluster_pack({"n": _sliced_node(held())}, list(pending), params=p, free_drains=fd)
+    ch = plan_cluster_pack({"n": _sliced_node(held())}, list(pending), params=p)
+    out = (ch.get("n") or _sliced_node(held())).gpus[0]
+    assert out.target == {"cpx_nps1": 7, "dpx_nps1": 1}                  # held: the 1/8 pod waits
+    full = [new_sliced_gpu("MI355X", i, used={"cpx_nps1": 8}) for i in (1, 2)]
+    ch = plan_cluster_pack({"n": _sliced_node(held(), *full)}, list(pending), params=p)
     out = ch["n"].gpus[0]
     assert out.target is None and out.used.get("cpx_nps1", 0) + out.free.get("cpx_nps1", 0) == 8
-    assert fd == set()                    # lapsed and forgotten
-    # the same reservation made by the threshold (not a free drain) is held: the small pod waits
-    ch = plan_cluster_pack({"n": _sliced_node(held())}, list(pending), params=p, free_drains=set())
-    out = (ch.get("n") or _sliced_node(held())).gpus[0]
-    assert out.target == {"cpx_nps1": 7, "dpx_nps1": 1}
 
 
 def test_reservation_threshold_in_learned_lifetimes():

@@ -316,7 +316,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
                       mode_age: Optional[Callable[[str, int], float]] = None,
                       last_served: Optional[Mapping[str, float]] = None,
                       pods_of: Optional[Callable[[str, int], List[Tuple[int, float]]]] = None,
-                      life: Any = None, free_drains: Optional[set] = None) -> Dict[str, NodeModel]:
+                      life: Any = None) -> Dict[str, NodeModel]:
     """Flip-aware packing for homogeneous compute partitions (the MI355X replacement of the
     reference's "first node that can change wins").
 
@@ -405,7 +405,7 @@ def plan_cluster_pack(models: Mapping[str, NodeModel], pending: List[Tuple[Dict[
         return changed
     if any(getattr(m, "layout", "partitions") != "partitions" for m in current.values()):
         from .sliced import plan_sliced
-        plan_sliced(current, models, changed, unserved, params, mode_age, pods_of, life, placed_on, free_drains)
+        plan_sliced(current, models, changed, unserved, params, mode_age, pods_of, life, placed_on)
         if not unserved:
             return changed
     # the homogeneous rules below only touch GPUs of nodes laid out as hardware partitions
@@ -608,7 +608,6 @@ class PodController:
         self._last_served: Dict[str, float] = {}  # profile -> last time a GPU was in its mode
         self.spx_demand = 0.0                     # EMA of whole-GPU demand (GPUs), pack policy
         self.lifetimes = LifetimeTracker()        # run times of finished pods (sliced-GPU drains)
-        self._free_drains: set = set()            # (node, GPU) reservations that are free drains
         self.partitioner = partitioner or Partitioner(client)
         self.clock = clock
         self.batch_timeout = batch_timeout
@@ -960,7 +959,7 @@ class PodController:
                 if any(getattr(m, "layout", "partitions") != "partitions" for m in models.values()) else None
             changed = plan_cluster_pack(models, pend or [(requested, 0.0)], incoming, self.pack, self.spx_demand,
                                         self._mode_ages(models, now), self._served(models, now),
-                                        pods_of, self.lifetimes.model, self._free_drains)
+                                        pods_of, self.lifetimes.model)
             need = requested
         elif self.policy in ("fifo", "simulate"):
             incoming: Dict[str, int] = {}
