@@ -1647,14 +1647,19 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
       };
       // (no reference or pointer is ever selected between two arrays below: such a select keeps
       // them out of registers — every choice is a branch on a value the unrolled loop folds)
+      // the exp of element r, and (a slot later, so no add waits on its transcendental) its add to
+      // the row sum — in r order, so the sum is attn_fwd_x3p's
       auto expo = [&](int t, int r) {
-        if (t) {
+        if (t)
           SB[r] = __builtin_amdgcn_exp2f(fmaf(SB[r], scale_log2e, -mcB));
-          psB += SB[r];
-        } else {
+        else
           SA[r] = __builtin_amdgcn_exp2f(fmaf(SA[r], scale_log2e, -mcA));
+      };
+      auto addp = [&](int t, int r) {
+        if (t)
+          psB += SB[r];
+        else
           psA += SA[r];
-        }
       };
       // split3_trunc8 of the pair (2q, 2q+1) of keys 16*s2.., in two slots
       auto split_a = [&](int t, int s2, int q) {
@@ -1730,6 +1735,12 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
           else ob1 = x3_step(k, vv[0], vv[1], vv[2], p0, p1, p2, ob1);
         }
         // ---- its vector work
+        // the row-sum adds trail their exps by one slot (A 0-7 in slots 1-8, B 0-7 in 9-16,
+        // A 8-15 in 33-40, B 8-15 in 41-48)
+        if constexpr ((q >= 1 && q <= 16) || (q >= 33 && q <= 48)) {
+          constexpr int e = q <= 16 ? q - 1 : q - 33;
+          addp(e / 8, (q <= 16 ? 0 : 8) + e % 8);
+        }
         if (q < 8) expo(0, q);
         else if (q < 16) expo(1, q - 8);
         else if (q < 32) {
@@ -1771,13 +1782,18 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
       };
       x3w_slots(slot, std::make_integer_sequence<int, 96>{});
     };
-    for (int i = 0; i < nb;) {
+    // two blocks per trip (the score registers swap roles), an odd last block after the loop: one
+    // back edge, so the O accumulators keep their registers across both halves
+    int i = 0;
+    for (; i + 1 < nb; i += 2) {
       iter(sca, scb, sna, snb, mxa, mxb, i);
       __syncthreads();
-      if (++i >= nb) break;
-      iter(sna, snb, sca, scb, mxa, mxb, i);
+      iter(sna, snb, sca, scb, mxa, mxb, i + 1);
       __syncthreads();
-      ++i;
+    }
+    if (i < nb) {
+      iter(sca, scb, sna, snb, mxa, mxb, i);
+      __syncthreads();
     }
 
     // the two tiles' results: whole key range -> normalised output, else a partial slot
