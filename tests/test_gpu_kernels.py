@@ -603,4 +603,4 @@ def test_attention_wide_kernel_bit_identical_to_two_wave_kernel(K, B, T, H, wave
             else:
                 f32 = outs[0]
     finally:
-        K.set_attention_x3_wide(os.environ.get("NOS_ATTN_WIDE") == "1")
+        K.set_attention_x3_wide(K.attention_x3_wide_default())

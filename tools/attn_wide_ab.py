@@ -40,7 +40,7 @@ def identical(qkv, waves_list) -> dict:
                 outs.append(out)
             torch.cuda.synchronize()
             res[f"w{waves}_{'x3' if x3 else 'f32'}"] = bool(torch.equal(outs[0], outs[1]))
-    K.set_attention_x3_wide(os.environ.get("NOS_ATTN_WIDE") == "1")
+    K.set_attention_x3_wide(K.attention_x3_wide_default())
     return res
 
 
@@ -90,7 +90,7 @@ def main() -> int:
                 for arm, v in mt.items():
                     r[f"model_{arm}_ms"] = round(min(v), 3)
                     r[f"model_{arm}_ms_all"] = [round(x, 3) for x in v]
-            K.set_attention_x3_wide(os.environ.get("NOS_ATTN_WIDE") == "1")
+            K.set_attention_x3_wide(K.attention_x3_wide_default())
         report[label] = r
         print(label, json.dumps(r), flush=True)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

@@ -21,7 +21,7 @@ import shutil
 import subprocess
 import sys
 from dataclasses import dataclass, field
-from typing import List, Sequence
+from typing import Dict, List, Sequence
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CSRC = os.path.join(ROOT, "csrc")
@@ -39,6 +39,9 @@ class Target:
     libs: List[str] = field(default_factory=list)
     headers: List[str] = field(default_factory=list)
     executable: bool = False   # a program (spawned by the agents), not a shared library
+    # options of one source only (its own object, linked into the target): code-generation choices
+    # that are right for one kernel and wrong for the rest (csrc/attn_wide.hip)
+    source_flags: Dict[str, List[str]] = field(default_factory=dict)
 
     @property
     def out(self) -> str:
@@ -61,7 +64,8 @@ class Target:
                     h.update(f.read())
         # the recipe without machine-specific paths: the tree is built here and run from another
         # checkout path on the GPU box
-        recipe = " ".join(self.command()[1:]).replace(CSRC, "<csrc>").replace(OUT, "<out>").replace(ROOT, "<root>")
+        recipe = " ".join(" ".join(c[1:]) for c in self.commands())
+        recipe = recipe.replace(CSRC, "<csrc>").replace(OUT, "<out>").replace(ROOT, "<root>")
         h.update(recipe.encode())
         with open(os.path.abspath(__file__), "rb") as f:
             h.update(f.read())
@@ -77,17 +81,31 @@ class Target:
     def stale(self) -> bool:
         return not os.path.exists(self.out) or self.read_stamp().get("sha256") != self.source_hash()
 
-    def command(self) -> List[str]:
-        srcs = [os.path.join(CSRC, s) for s in self.sources]
-        common = ["-O3", "-std=c++17", "-fPIC"] + ([] if self.executable else ["-shared"]) + \
-            [f"-I{ROCM}/include", f"-I{CSRC}"]
+    def _cc(self) -> List[str]:
         if self.compiler == "hipcc":
-            cc = [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-Wno-unused-result",
-                  "-Wno-unused-value"]
-        else:
-            cc = [shutil.which("g++") or "g++", "-Wall"]
+            return [os.path.join(ROCM, "bin", "hipcc"), f"--offload-arch={ARCH}", "-Wno-unused-result",
+                    "-Wno-unused-value"]
+        return [shutil.which("g++") or "g++", "-Wall"]
+
+    def _obj(self, src: str) -> str:
+        return os.path.join(OUT, f"{self.name}.{src}.o")
+
+    def commands(self) -> List[List[str]]:
+        """The compile commands, in order: one object per source with its own options, then the
+        target from the other sources and those objects."""
+        inc = ["-O3", "-std=c++17", "-fPIC", f"-I{ROCM}/include", f"-I{CSRC}"]
+        cmds = [self._cc() + inc + self.flags + self.source_flags[s] + ["-c", os.path.join(CSRC, s), "-o", self._obj(s)]
+                for s in self.sources if s in self.source_flags]
+        # the objects first: hipcc marks each .hip source `-x hip`, which would claim a later object
+        srcs = [self._obj(s) for s in self.sources if s in self.source_flags] + \
+            [os.path.join(CSRC, s) for s in self.sources if s not in self.source_flags]
         link = [f"-L{ROCM}/lib", f"-Wl,-rpath,{ROCM}/lib"] + [f"-l{lib}" for lib in self.libs]
-        return cc + common + self.flags + srcs + ["-o", self.out] + link
+        shared = [] if self.executable else ["-shared"]
+        return cmds + [self._cc() + inc + shared + self.flags + srcs + ["-o", self.out] + link]
+
+    def command(self) -> List[str]:
+        """The final (link) command."""
+        return self.commands()[-1]
 
 
 TARGETS: Sequence[Target] = (
@@ -96,7 +114,8 @@ TARGETS: Sequence[Target] = (
     Target("libnos_hbmlimit.so", ["hbm_limit.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"], libs=["dl"]),
     Target("libnos_barrier.so", ["rccl_barrier.cpp"], "g++", flags=["-D__HIP_PLATFORM_AMD__"],
            libs=["rccl", "amdhip64"]),
-    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip", "attn_proj.hip"], "hipcc"),
+    Target("libnos_kernels.so", ["kernels.hip", "gemm.hip", "gemm_x3.hip", "head.hip", "attn_proj.hip", "attn_wide.hip"],
+           "hipcc", source_flags={"attn_wide.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}),
     # the agent's commit-barrier helper as a native program: no interpreter start-up on the flip path
     Target("nos-gpuhelper", ["gpuhelper.cpp", "rccl_barrier.cpp", "p2p_barrier.hip"], "hipcc",
            libs=["rccl", "amdhip64"], executable=True),
@@ -110,10 +129,13 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 4) -> List[str]
     todo = [t for t in TARGETS if os.path.exists(os.path.join(CSRC, t.sources[0])) and (force or t.stale())]
 
     def run(t: Target) -> str:
-        cmd = t.command()
-        p = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True)
-        if p.returncode != 0:
-            raise RuntimeError(f"building {t.name} failed:\n{' '.join(cmd)}\n{p.stderr[-4000:]}")
+        for cmd in t.commands():
+            p = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True)
+            if p.returncode != 0:
+                raise RuntimeError(f"building {t.name} failed:\n{' '.join(cmd)}\n{p.stderr[-4000:]}")
+        for s in t.source_flags:
+            if os.path.exists(t._obj(s)):
+                os.remove(t._obj(s))
         with open(t.stamp_path, "w") as f:
             json.dump({"library": t.name, "sha256": t.source_hash(), "arch": ARCH, "sources": t.sources}, f)
         return t.name

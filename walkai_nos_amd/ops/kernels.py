@@ -181,10 +181,16 @@ def set_attention_x3_group(g: int) -> None:
 
 
 def set_attention_x3_wide(on: bool) -> None:
-    """fp32-input 8-tile attention: True (``NOS_ATTN_WIDE=1``) runs ``attn_fwd_x3w`` — one wave per
-    SIMD carrying two 32-query tiles — False (default) the two-waves-per-SIMD ``attn_fwd_x3p<8>``.
-    Same units, partials and per-tile arithmetic: the outputs are bit-identical."""
+    """fp32-input 8-tile attention: True (default) runs ``attn_fwd_x3w`` (``csrc/attn_wide.hip``) —
+    one wave per SIMD carrying two 32-query tiles — False (``NOS_ATTN_WIDE=0``) the
+    two-waves-per-SIMD ``attn_fwd_x3p<8>``. Same units, partials and per-tile arithmetic: the
+    outputs are bit-identical (``profiles/attn_wide_ab_r6.json``: the wide kernel 4-8% faster)."""
     _check(_L().nos_attention_x3_set_wide(1 if on else 0))
+
+
+def attention_x3_wide_default() -> bool:
+    """The process's setting at load time (``NOS_ATTN_WIDE``; A/B code restores it)."""
+    return os.environ.get("NOS_ATTN_WIDE", "1").strip() != "0"
 
 
 def attention_x3_wide() -> bool:
