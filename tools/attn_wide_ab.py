@@ -50,12 +50,17 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slices", default="spx,dpx,cpx")
     ap.add_argument("--model", action="store_true", help="also time the whole inference per arm")
+    ap.add_argument("--arms", default="wide,x3p8", help="arms to time (one arm for a counter pass)")
+    ap.add_argument("--no-check", action="store_true", help="skip the bit-identity check")
     ap.add_argument("--out", default="gpurun_out/attn_wide_ab.json")
     a = ap.parse_args()
     torch.manual_seed(0)
     qkv = torch.randn(1, T, 3 * D, device="cuda")
-    report = {"T": T, "H": H, "identical": identical(qkv, (K.attention_x3_waves(256, 1, T, H), 7, 64, 333))}
-    print(json.dumps(report["identical"]), flush=True)
+    report = {"T": T, "H": H}
+    if not a.no_check:
+        report["identical"] = identical(qkv, (K.attention_x3_waves(256, 1, T, H), 7, 64, 333))
+        print(json.dumps(report["identical"]), flush=True)
+    arms = [(arm, arm == "wide") for arm in a.arms.split(",")]
     flops_x3 = 4.0 * T * T * HD * H * 6
     for label in a.slices.split(","):
         cus = slice_cus(f"{label}_nps1", 0)
@@ -67,9 +72,9 @@ def main() -> int:
             waves = K.attention_x3_waves(n, 1, T, H)
             r["waves"] = waves
             out = torch.empty(3, 1, T, D, dtype=torch.bfloat16, device="cuda")
-            times = {"wide": [], "x3p8": []}
+            times = {arm: [] for arm, _ in arms}
             for _ in range(a.rounds):
-                for arm, wide in (("wide", True), ("x3p8", False)):
+                for arm, wide in arms:
                     K.set_attention_x3_wide(wide)
                     times[arm].append(timeit(lambda: K.attention_x3f(qkv, out, H, HD, 0.125, waves), s, a.iters))
             for arm, v in times.items():
@@ -81,10 +86,10 @@ def main() -> int:
                 with torch.cuda.stream(s):
                     m = YolosSmall().cuda().eval()
                     xin = demo_input(1, DEMO_INPUT_HW, "cuda")
-                mt = {"wide": [], "x3p8": []}
+                mt = {arm: [] for arm, _ in arms}
                 with torch.no_grad():
                     for _ in range(a.rounds):
-                        for arm, wide in (("wide", True), ("x3p8", False)):
+                        for arm, wide in arms:
                             K.set_attention_x3_wide(wide)
                             mt[arm].append(timeit(lambda: m(xin), s, 5) / 1000.0)
                 for arm, v in mt.items():

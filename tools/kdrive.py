@@ -1,7 +1,7 @@
 """Run one hot op of the YOLOS-small layer a few times, eagerly, on one slice — a driver for
 rocprofv3 PMC passes (one dispatch per call, no graph):
 
-    rocprofv3 --pmc <counters> --kernel-trace -- python3 tools/kdrive.py --op attn_x3 --slice spx
+    rocprofv3 --pmc <counters> --kernel-trace -- python3 tools/kdrive.py --op attn_x3f --slice spx
 """
 from __future__ import annotations
 
@@ -25,7 +25,7 @@ PROFILES = {"spx": "spx_nps1", "dpx": "dpx_nps1", "qpx": "qpx_nps1", "cpx": "cpx
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", default="attn_x3",
-                    choices=("attn_x3", "attn_f32", "qkv_x3", "proj_x3", "fc1_x3", "fc2_x3", "layernorm_x3"))
+                    choices=("attn_x3", "attn_x3f", "attn_f32", "qkv_x3", "proj_x3", "fc1_x3", "fc2_x3", "layernorm_x3"))
     ap.add_argument("--slice", default="spx", choices=tuple(PROFILES))
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--tile", type=int, default=None, help="force an x3 GEMM tile config (no autotune dispatches)")
@@ -49,6 +49,10 @@ def main() -> int:
             fn = lambda: G.gemm_x3(xa3, w, b, gelu=gelu, out_f32=not out3, out_x3=out3, tile=a.tile)  # noqa: E731
         elif a.op == "attn_x3":
             fn = lambda: K.attention_qkv_x3(planes, H, 64, 0.125)  # noqa: E731
+        elif a.op == "attn_x3f":  # the model's path: fp32 QKV in (attn_fwd_x3w unless NOS_ATTN_WIDE=0)
+            waves = K.attention_x3_waves(n, 1, T, H)
+            out = torch.empty(1, T, D, device="cuda")
+            fn = lambda: K.attention_x3f(qkv, out, H, 64, 0.125, waves)  # noqa: E731
         elif a.op == "attn_f32":
             K.set_fp32_matmul("f32")
             fn = lambda: K.attention_qkv(qkv, H, 64, 0.125)  # noqa: E731
