@@ -56,10 +56,11 @@ template <bool FDIV = false>
 __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__ qkv, float* __restrict__ out,
                                                        __bf16* __restrict__ outp, float* __restrict__ part_o,
                                                        float* __restrict__ part_ml, int B, int T, int H, int h0,
-                                                       int Ht, float scale_log2e, int Pk) {
+                                                       int Ht, float scale_log2e, int Pk, int* __restrict__ cnt) {
   constexpr int G = 8;  // query tiles per workgroup: 4 waves x 2
   __shared__ __attribute__((aligned(16))) __bf16 lds_k[2 * 3 * XK_PLANE];
   __shared__ __attribute__((aligned(16))) __bf16 lds_v[2 * 3 * XV_PLANE];
+  __shared__ int s_last;
   const int P = Pk & 0x3fffff;
   const PinnedBlock pb = pinned_block(unsigned(Pk >> 22) & 0xffu);
   if (pb.id < 0 || pb.id >= P) return;
@@ -377,32 +378,35 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
       __syncthreads();
     }
 
+    // tile t's normalised rows (a whole key range, or the merge of a split one)
+    const bool whole = kb0 == 0 && kb1 == NK;
+    auto store_tile = [&](int t, const f32x16& o0, const f32x16& o1, float l) {
+      const int q = (qg * G + 2 * wv + t) * 32 + j;
+      if (q >= T) return;
+      const float inv = 1.f / l;
+      const size_t orow = (size_t(b) * T + q) * D + head * HD;
+      if (outp) {
+        const size_t op = size_t(B) * T * D;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = key_of(r, hf);
+          store_x3(outp, op, orow + d, o0[r] * inv);
+          store_x3(outp, op, orow + 32 + d, o1[r] * inv);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int d = key_of(r, hf);
+          out[orow + d] = o0[r] * inv;
+          out[orow + 32 + d] = o1[r] * inv;
+        }
+      }
+    };
     // the two tiles' results: whole key range -> normalised output, else a partial slot
     auto finish = [&](bool active, int t, const f32x16& o0, const f32x16& o1, float m, float l) {
       if (!active) return;
-      const int qt = qg * G + 2 * wv + t;
-      if (kb0 == 0 && kb1 == NK) {
-        const int q = qt * 32 + j;
-        if (q < T) {
-          const float inv = 1.f / l;
-          const size_t orow = (size_t(b) * T + q) * D + head * HD;
-          if (outp) {
-            const size_t op = size_t(B) * T * D;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int d = key_of(r, hf);
-              store_x3(outp, op, orow + d, o0[r] * inv);
-              store_x3(outp, op, orow + 32 + d, o1[r] * inv);
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int d = key_of(r, hf);
-              out[orow + d] = o0[r] * inv;
-              out[orow + 32 + d] = o1[r] * inv;
-            }
-          }
-        }
+      if (whole) {
+        store_tile(t, o0, o1, l);
       } else {
         const size_t slot = (size_t(w) * 2 + (first ? 0 : 1)) * G + 2 * wv + t;
         float* po = part_o + slot * (HD * 32);
@@ -420,6 +424,58 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
     };
     finish(activeA, 0, oa0, oa1, ma, la);
     finish(activeB, 1, ob0, ob1, mb, lb);
+    if (!whole && cnt) {
+      // Stream-K merge in the kernel (cnt != nullptr): the row's contributors count themselves in
+      // cnt[grp] after their partials are visible device-wide, and the LAST to arrive merges every
+      // contributor's partials — in workgroup order, with attn_sk_lds_fixup's arithmetic, so the
+      // result is that kernel's bit for bit — and stores the normalised tiles. Nobody waits for
+      // anybody (no spin, whatever the residency), and the last arriver resets the counter, so the
+      // counters are zero again when the grid has drained. Replaces the fixup launch and its re-read
+      // of every partial. Opt-in (NOS_ATTN_MERGE=1): on the box it is slower than the fixup launch
+      // (profiles/attn_merge_ab_r6.json); likely the device-scope release / acquire below, which
+      // compile to a write-back and an invalidate of the XCD's L2 (the XCDs' L2s are not coherent).
+      const long long t0 = grp * NK, t1 = t0 + NK;
+      const long long wlo = ((t0 + 1) * P + U - 1) / U - 1, whi = (t1 * P + U - 1) / U - 1;
+      __threadfence();  // release: this workgroup's partials before its count
+      __syncthreads();
+      if (tid == 0) {
+        int n = 0;
+        for (long long x = wlo; x <= whi; ++x) n += (x * U / P != (x + 1) * U / P) ? 1 : 0;
+        const int last = atomicAdd(&cnt[grp], 1) == n - 1;
+        if (last) atomicExch(&cnt[grp], 0);
+        s_last = last;
+      }
+      __syncthreads();
+      if (s_last) {
+        __threadfence();  // acquire: every other contributor's partials
+        auto merge = [&](int t) {
+          float M = -INFINITY, L = 0.f;
+          f32x16 a0 = {0}, a1 = {0};
+          for (long long x = wlo; x <= whi; ++x) {
+            const long long s0 = x * U / P;
+            if (s0 == (x + 1) * U / P) continue;
+            const size_t slot = (size_t(x) * 2 + (s0 >= t0 ? 0 : 1)) * G + 2 * wv + t;
+            const float mw = part_ml[slot * 64 + j];
+            if (mw == -INFINITY) continue;
+            const float lw = part_ml[slot * 64 + 32 + j];
+            const float* po = part_o + slot * (HD * 32);
+            const float Mn = fmaxf(M, mw);
+            const float so = __builtin_amdgcn_exp2f(M - Mn), sn = __builtin_amdgcn_exp2f(mw - Mn);
+            L = fmaf(lw, sn, L * so);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int d = key_of(r, hf);
+              a0[r] = fmaf(po[d * 32 + j], sn, a0[r] * so);
+              a1[r] = fmaf(po[(32 + d) * 32 + j], sn, a1[r] * so);
+            }
+            M = Mn;
+          }
+          store_tile(t, a0, a1, L);
+        };
+        if (activeA) merge(0);
+        if (activeB) merge(1);
+      }
+    }
     u += kb1 - kb0;
     first = false;
   }
@@ -429,13 +485,13 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_x3w(const float* __restrict__
 
 int nos_attn_x3w_launch(bool fdiv, dim3 grid, hipStream_t s, const float* qkv, float* out, __bf16* outp,
                         float* part_o, float* part_ml, int B, int T, int H, int h0, int Ht, float scale_log2e,
-                        int Pk) {
+                        int Pk, int* cnt) {
   if (fdiv)
     hipLaunchKernelGGL(attn_fwd_x3w<true>, grid, dim3(256), 0, s, qkv, out, outp, part_o, part_ml, B, T, H, h0, Ht,
-                       scale_log2e, Pk);
+                       scale_log2e, Pk, cnt);
   else
     hipLaunchKernelGGL(attn_fwd_x3w<false>, grid, dim3(256), 0, s, qkv, out, outp, part_o, part_ml, B, T, H, h0, Ht,
-                       scale_log2e, Pk);
+                       scale_log2e, Pk, cnt);
   return int(hipPeekAtLastError());  // left set for the caller's check_launch
 }
 

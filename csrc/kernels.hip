@@ -717,9 +717,11 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
       if (mw[c] == -INFINITY) continue;
       const float Mn = fmaxf(M, mw[c]);
       const float so = __builtin_amdgcn_exp2f(M - Mn), sn = __builtin_amdgcn_exp2f(mw[c] - Mn);
-      L = L * so + lw[c] * sn;
+      // explicit fmas (no contraction left to the compiler): attn_fwd_x3w's in-kernel merge does
+      // the same operations and matches this kernel bit for bit
+      L = fmaf(lw[c], sn, L * so);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = acc[i] * so + ow[c][i] * sn;
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(ow[c][i], sn, acc[i] * so);
       M = Mn;
     }
   }
@@ -1487,7 +1489,7 @@ int nos_attention_x3_wg_per_cu() {
 // nos_attention_ws_bytes of the LDS variant (variant 0 layout), merged by the same fixup kernel.
 static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out, void* outp, float* ws, int B,
                                int T, int H, int h0, int hn, int head_dim, float scale, int waves, void* stream,
-                               bool f32in, bool fixup = true) {
+                               bool f32in, bool fixup = true, int* cnt = nullptr) {
   if ((out == nullptr) == (outp == nullptr)) {
     g_err = "attention x3: exactly one of out / outp";
     return -1;
@@ -1544,7 +1546,7 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
                        sl2, waves);
   else if (G == 8 && f32in && g_x3_wide)
     nos_attn_x3w_launch(fdiv, grid, s, reinterpret_cast<const float*>(qkv3), out, op, part_o, part_ml, B, T, hn, h0,
-                        H, sl2, pk);
+                        H, sl2, pk, fixup ? cnt : nullptr);
   else if (G == 8 && f32in && (g_x3_flags & 2))
     hipLaunchKernelGGL((attn_fwd_x3p<8, false, true, true>), grid, dim3(512), 0, s, q3, plane_stride, out, op,
                        part_o, part_ml, B, T, hn, h0, H, sl2, pk);
@@ -1565,6 +1567,7 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
                        T, hn, h0, H, sl2, pk);
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (!fixup) return 0;  // the partials are merged by the consumer (attn_proj.hip)
+  if (cnt && G == 8 && f32in && g_x3_wide && g_x3_pipelined) return 0;  // merged in the kernel
   const unsigned fpin = pin | ((g_x3_flags & 32) ? 0x100u : 0u);  // bit 8: the earlier 2-byte stores (A/B)
   if (G == 8)
     hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(B * hn * QG * 8, pin)), dim3(256), 0, s,
@@ -1586,6 +1589,20 @@ int nos_attention_x3_sk_heads(const void* qkv3, size_t plane_stride, float* out,
 int nos_attention_x3f_sk_heads(const float* qkv, float* out, void* outp, float* ws, int B, int T, int H, int h0,
                                int hn, int head_dim, float scale, int waves, void* stream) {
   return attention_x3_launch(qkv, 8, out, outp, ws, B, T, H, h0, hn, head_dim, scale, waves, stream, true);
+}
+
+// the same with the stream-K merge inside the wide kernel (attn_fwd_x3w) when it runs: cnt holds
+// ncnt >= B*hn*ceil(ceil(T/32)/8) row counters, zero before the first launch (every launch leaves
+// them zero); launches that share cnt must not run concurrently (one counter array per stream)
+int nos_attention_x3f_sk_heads_merged(const float* qkv, float* out, void* outp, float* ws, int* cnt, int ncnt, int B,
+                                      int T, int H, int h0, int hn, int head_dim, float scale, int waves,
+                                      void* stream) {
+  const int QG = ((T + 31) / 32 + 7) / 8;
+  if (cnt == nullptr || (long long)ncnt < (long long)B * hn * QG) {
+    g_err = "attention x3 merged: needs B*hn*QG row counters";
+    return -1;
+  }
+  return attention_x3_launch(qkv, 8, out, outp, ws, B, T, H, h0, hn, head_dim, scale, waves, stream, true, true, cnt);
 }
 
 // The x3 attention from fp32 QKV over all heads WITHOUT the stream-K fixup: split query tiles

@@ -93,7 +93,9 @@ constexpr int XK_PLANE = 32 * XK_STR, XV_PLANE = 32 * XV_STR;
 }  // namespace
 
 // attn_wide.hip: the one-wave-per-SIMD fp32-input x3 attention (attn_fwd_x3w) — launch (returns the
-// launch's hipError_t) and resident workgroups per CU
+// launch's hipError_t; cnt: B*H*QG zeroed row counters for the in-kernel stream-K merge, or nullptr
+// to leave split tiles' partials for attn_sk_lds_fixup) and resident workgroups per CU
 int nos_attn_x3w_launch(bool fdiv, dim3 grid, hipStream_t s, const float* qkv, float* out, __bf16* outp,
-                        float* part_o, float* part_ml, int B, int T, int H, int h0, int Ht, float scale_log2e, int Pk);
+                        float* part_o, float* part_ml, int B, int T, int H, int h0, int Ht, float scale_log2e, int Pk,
+                        int* cnt);
 int nos_attn_x3w_occupancy();

@@ -604,3 +604,31 @@ def test_attention_wide_kernel_bit_identical_to_two_wave_kernel(K, B, T, H, wave
                 f32 = outs[0]
     finally:
         K.set_attention_x3_wide(K.attention_x3_wide_default())
+
+
+@pytest.mark.parametrize("B,T,H,waves,hb", [(1, 3401, 6, None, None), (1, 3401, 6, 32, 2), (2, 300, 3, 64, None),
+                                            (1, 77, 1, 3, None), (1, 1000, 2, 333, 1)])
+def test_attention_in_kernel_merge_matches_fixup_launch(K, B, T, H, waves, hb):
+    # the wide kernel's in-kernel stream-K merge (the last workgroup of a row to finish merges its
+    # partials) against the separate attn_sk_lds_fixup launch: bit-identical, fp32 and x3 planes,
+    # for grids with empty ranges (333 workgroups for 256 units), head blocks, and back-to-back
+    # launches that reuse the row counters (each launch leaves them zero)
+    torch.manual_seed(22)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    w = waves or K.attention_x3_waves(K.slice_cus(), B, T, H)
+    try:
+        K.set_attention_x3_wide(True)
+        for x3 in (False, True):
+            outs = []
+            for merge in (True, False, True):
+                K.set_attention_merge(merge)
+                out = (torch.full((3, B, T, H * 64), float("nan"), dtype=torch.bfloat16, device="cuda") if x3
+                       else torch.full((B, T, H * 64), float("nan"), device="cuda"))
+                outs.append(K.attention_x3f(qkv, out, H, 64, 0.125, w, head_block=hb))
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (x3, w)
+            assert torch.equal(outs[2], outs[1]), (x3, w)
+        assert int(K._row_counters(qkv.device, 1).abs().sum().item()) == 0
+    finally:
+        K.set_attention_merge(None)
+        K.set_attention_x3_wide(K.attention_x3_wide_default())

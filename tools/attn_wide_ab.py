@@ -50,7 +50,9 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slices", default="spx,dpx,cpx")
     ap.add_argument("--model", action="store_true", help="also time the whole inference per arm")
-    ap.add_argument("--arms", default="wide,x3p8", help="arms to time (one arm for a counter pass)")
+    ap.add_argument("--arms", default="wide,wide_fixup,x3p8",
+                    help="arms to time (one arm for a counter pass): wide = attn_fwd_x3w merging in the kernel, "
+                         "wide_fixup = the same with the separate fixup launch, x3p8 = attn_fwd_x3p<8>")
     ap.add_argument("--no-check", action="store_true", help="skip the bit-identity check")
     ap.add_argument("--out", default="gpurun_out/attn_wide_ab.json")
     a = ap.parse_args()
@@ -60,7 +62,11 @@ def main() -> int:
     if not a.no_check:
         report["identical"] = identical(qkv, (K.attention_x3_waves(256, 1, T, H), 7, 64, 333))
         print(json.dumps(report["identical"]), flush=True)
-    arms = [(arm, arm == "wide") for arm in a.arms.split(",")]
+    arms = [(arm, arm.startswith("wide")) for arm in a.arms.split(",")]
+
+    def use(arm: str, wide: bool) -> None:
+        K.set_attention_x3_wide(wide)
+        K.set_attention_merge(arm == "wide")
     flops_x3 = 4.0 * T * T * HD * H * 6
     for label in a.slices.split(","):
         cus = slice_cus(f"{label}_nps1", 0)
@@ -75,7 +81,7 @@ def main() -> int:
             times = {arm: [] for arm, _ in arms}
             for _ in range(a.rounds):
                 for arm, wide in arms:
-                    K.set_attention_x3_wide(wide)
+                    use(arm, wide)
                     times[arm].append(timeit(lambda: K.attention_x3f(qkv, out, H, HD, 0.125, waves), s, a.iters))
             for arm, v in times.items():
                 r[f"{arm}_us"] = round(min(v), 2)
@@ -90,12 +96,13 @@ def main() -> int:
                 with torch.no_grad():
                     for _ in range(a.rounds):
                         for arm, wide in arms:
-                            K.set_attention_x3_wide(wide)
+                            use(arm, wide)
                             mt[arm].append(timeit(lambda: m(xin), s, 5) / 1000.0)
                 for arm, v in mt.items():
                     r[f"model_{arm}_ms"] = round(min(v), 3)
                     r[f"model_{arm}_ms_all"] = [round(x, 3) for x in v]
             K.set_attention_x3_wide(K.attention_x3_wide_default())
+            K.set_attention_merge(None)
         report[label] = r
         print(label, json.dumps(r), flush=True)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

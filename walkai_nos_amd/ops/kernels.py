@@ -24,7 +24,7 @@ import ctypes
 import math
 import os
 import threading
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -268,6 +268,40 @@ def attention_input_f32() -> bool:
     return os.environ.get("NOS_ATTN_F32IN", "1") != "0" and attention_x3_group() == 8
 
 
+_merge: Optional[bool] = None
+_row_cnt: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def set_attention_merge(on: Optional[bool]) -> None:
+    """True: the wide kernel merges split query tiles itself (the last workgroup of a row to finish
+    merges the row's partials, ``csrc/attn_wide.hip``); False: the separate ``attn_sk_lds_fixup``
+    launch. None: ``NOS_ATTN_MERGE`` (default off). Bit-identical outputs either way. Off because
+    it measured slower (``profiles/attn_merge_ab_r6.json``: 149 vs 96 us on the whole GPU); the
+    likely cause is the device-scope release / acquire around the hand-off, which compile to a
+    write-back and an invalidate of the XCD's L2 (the per-XCD L2s are not coherent)."""
+    global _merge
+    _merge = on
+
+
+def attention_merge_in_kernel() -> bool:
+    if _merge is not None:
+        return _merge
+    return os.environ.get("NOS_ATTN_MERGE", "0").strip() == "1"
+
+
+def _row_counters(device: torch.device, n: int) -> torch.Tensor:
+    """The in-kernel merge's row counters for the current stream: zeroed once, left zero by every
+    launch; one array per stream, because launches that share one must not overlap (launches on one
+    stream never do)."""
+    key = (device.index if device.index is not None else torch.cuda.current_device(), _stream())
+    with _lock:
+        c = _row_cnt.get(key)
+        if c is None or c.numel() < n:
+            c = torch.zeros(max(n, 1024), dtype=torch.int32, device=device)
+            _row_cnt[key] = c
+        return c
+
+
 def attention_x3f(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: int, scale: float, waves: int,
                   head_block: Optional[int] = None) -> torch.Tensor:
     """:func:`attention_x3` from an fp32 packed QKV tensor ``[B, T, 3*H*64]`` (split in-kernel)."""
@@ -276,10 +310,18 @@ def attention_x3f(qkv: torch.Tensor, out: torch.Tensor, heads: int, head_dim: in
     ws = torch.empty(waves * 2 * (64 * 32 + 64) * attention_x3_group(), dtype=torch.float32, device=qkv.device)
     x3_out = out.dtype == torch.bfloat16
     hb = heads if head_block is None else max(1, min(heads, int(head_block)))
+    L = _L()
+    rows = B * hb * (((T + 31) // 32 + 7) // 8)
+    cnt = _row_counters(qkv.device, rows) if attention_merge_in_kernel() and attention_x3_wide() else None
     for h0 in range(0, heads, hb):
-        _check(_L().nos_attention_x3f_sk_heads(qkv.data_ptr(), None if x3_out else out.data_ptr(),
-                                               out.data_ptr() if x3_out else None, ws.data_ptr(), B, T, heads, h0,
-                                               min(hb, heads - h0), head_dim, scale, waves, _stream()))
+        o, op = (None, out.data_ptr()) if x3_out else (out.data_ptr(), None)
+        if cnt is not None:
+            _check(L.nos_attention_x3f_sk_heads_merged(qkv.data_ptr(), o, op, ws.data_ptr(), cnt.data_ptr(),
+                                                       cnt.numel(), B, T, heads, h0, min(hb, heads - h0), head_dim,
+                                                       scale, waves, _stream()))
+        else:
+            _check(L.nos_attention_x3f_sk_heads(qkv.data_ptr(), o, op, ws.data_ptr(), B, T, heads, h0,
+                                                min(hb, heads - h0), head_dim, scale, waves, _stream()))
     return out
 
 
@@ -393,6 +435,8 @@ def _L() -> ctypes.CDLL:
             L.nos_attention_x3_sk_heads.argtypes = [vp, ctypes.c_size_t, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32,
                                                     i32, vp]
             L.nos_attention_x3f_sk_heads.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, f32, i32, vp]
+            L.nos_attention_x3f_sk_heads_merged.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32,
+                                                            i32, vp]
             L.nos_attention_x3f_partials.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, vp]
             L.nos_attn_merge_proj_ln.argtypes = [vp, i32, vp, i32, i32, i32, vp, ctypes.c_size_t, vp, vp, vp, vp, f32,
                                                  vp, vp, vp]
