@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import json
 import logging
-from typing import Any, Callable, Dict, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from ...api import v1alpha1 as api
 from ...kube import objects as ko
@@ -27,7 +27,8 @@ log = logging.getLogger("nos.agent.reporter")
 class Reporter:
     def __init__(self, client: Any, partition_client: Any, shared: SharedState, refresh_interval: float = 10.0,
                  profile_extractor: Callable[[str], Optional[str]] = extract_profile_name,
-                 extra_annotations: Optional[Callable[[], Dict[str, str]]] = None, slice_store: Any = None):
+                 extra_annotations: Optional[Callable[[], Dict[str, str]]] = None, slice_store: Any = None,
+                 observers: Optional[List[Callable[[], Any]]] = None):
         self.client = client
         self.pc = partition_client
         self.shared = shared
@@ -35,6 +36,7 @@ class Reporter:
         self.extract = profile_extractor
         self.extra = extra_annotations
         self.slice_store = slice_store
+        self.observers = list(observers or [])   # run after every report (e.g. sliceagent/balance.py)
 
     def reconcile(self, req: Request) -> Result:
         with self.shared.lock:
@@ -42,6 +44,11 @@ class Reporter:
                 return self._reconcile(req)
             finally:
                 self.shared.on_report_done()
+                for obs in self.observers:
+                    try:
+                        obs()
+                    except Exception as e:  # noqa: BLE001 - an observer never fails the report
+                        log.warning("report observer failed: %s", e)
 
     def _reconcile(self, req: Request) -> Result:
         try:

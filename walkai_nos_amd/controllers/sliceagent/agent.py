@@ -175,12 +175,17 @@ class SliceActuator:
 def setup_slice_agent(mgr: Manager, node_name: str, slicing_client: Any, store: Any, device_plugin: Any = None,
                       barrier_factory: Optional[Callable[[int], Any]] = None, refresh_interval: float = 10.0,
                       cu_count: int = 256, memory_gb: int = 288,
-                      probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None):
-    from ...models.slicing.profile import extract_profile_name
+                      probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None,
+                      skip_counts: Optional[List[int]] = None):
+    from ...models.slicing.profile import SKIP_SHARED_COUNTS, extract_profile_name
+    from .balance import SharedBalance, node_event
     shared = SharedState()
     extra = probe(shared) if probe is not None else None
+    balance = SharedBalance(node_name, store.load, slicing_client.used_ids, node_event(mgr.client, node_name),
+                            SKIP_SHARED_COUNTS if skip_counts is None else skip_counts)
     reporter = Reporter(mgr.client, slicing_client, shared, refresh_interval, profile_extractor=extract_profile_name,
-                        extra_annotations=extra)
+                        extra_annotations=extra, observers=[balance.check])
+    reporter.balance = balance
     actuator = SliceActuator(mgr.client, slicing_client, store, shared, node_name, device_plugin, barrier_factory,
                              cu_count, memory_gb)
     mgr.new_controller(constant.SLICE_AGENT_REPORTER_CONTROLLER, reporter.reconcile,
