@@ -85,3 +85,20 @@ def test_node_event_shape_and_reporter_wiring():
     _, reporter, _ = setup_slice_agent(mgr, "n3", SC(), Store())
     assert reporter.observers == [reporter.balance.check]
     assert reporter.balance.check() == {}
+
+
+def test_released_slices_are_forgotten_by_the_start_gate():
+    # a memory-only pod that left no longer holds the next start on its GPU back
+    from walkai_nos_amd.deviceplugin.startgate import StartGate
+
+    slices = _slices(3)
+    ids = [x.id for x in slices[0]]
+    used = set(ids)
+    gate = StartGate(ready=lambda sid: False, timeout=20.0, clock=lambda: 0.0, sleep=lambda s: None)
+    gate.enter(0, [ids[2]])                         # ids[2] let through last, never ready
+    b = SharedBalance("n4", lambda: slices, lambda: used, None, on_release=gate.forget)
+    b.check()
+    assert gate._last[0][0] == ids[2]
+    used.discard(ids[2])                            # its pod left
+    b.check()
+    assert 0 not in gate._last                      # the next start on GPU 0 does not wait for it

@@ -47,12 +47,11 @@ def main(argv=None) -> int:
     # render nodes and slice health come from the device map (a slice whose GPU left the map is
     # Unhealthy); the sysfs listing is only the fallback for a map without render minors
     from ..deviceplugin.startgate import StartGate
+    gate = StartGate(timeout=cfg.sharedSliceStartGateSeconds) if cfg.sharedSliceStartGateSeconds > 0 else None
     plugins = PluginManager(store, render_nodes_from_sysfs(), socket_dir=cfg.devicePluginDir,
                             kubelet_socket=os.path.join(cfg.devicePluginDir, "kubelet.sock"),
                             cu_count=gpus[0].cu_count or 256, shim_path=cfg.hbmLimitShimPath, device_map=smi.device_map,
-                            shared_hw_queues=cfg.sharedSliceHwQueues,
-                            start_gate=StartGate(timeout=cfg.sharedSliceStartGateSeconds)
-                            if cfg.sharedSliceStartGateSeconds > 0 else None)
+                            shared_hw_queues=cfg.sharedSliceHwQueues, start_gate=gate)
 
     class Notify:
         def restart(self, node_name, timeout=60):
@@ -65,7 +64,8 @@ def main(argv=None) -> int:
         from ..controllers.sliceagent.agent import slice_probe_targets
         probe = lambda shared: ProbeRunner(shared, node, targets=slice_probe_targets(store, cu_count)).annotations  # noqa: E731
     setup_slice_agent(mgr, node, sc, store, device_plugin=Notify(), refresh_interval=cfg.reportConfigIntervalSeconds,
-                      cu_count=cu_count, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288, probe=probe)
+                      cu_count=cu_count, memory_gb=int(gpus[0].vram_bytes // 10**9) or 288, probe=probe,
+                      on_release=gate.forget if gate is not None else None)
     stop = threading.Event()
     threading.Thread(target=run_forever, args=(plugins, 2.0, stop), daemon=True).start()
     from ..exporters.gpu_metrics import GpuMetricsPoller

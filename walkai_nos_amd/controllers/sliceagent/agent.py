@@ -176,13 +176,14 @@ def setup_slice_agent(mgr: Manager, node_name: str, slicing_client: Any, store: 
                       barrier_factory: Optional[Callable[[int], Any]] = None, refresh_interval: float = 10.0,
                       cu_count: int = 256, memory_gb: int = 288,
                       probe: Optional[Callable[[SharedState], Callable[[], dict]]] = None,
-                      skip_counts: Optional[List[int]] = None):
+                      skip_counts: Optional[List[int]] = None,
+                      on_release: Optional[Callable[[str], None]] = None):
     from ...models.slicing.profile import SKIP_SHARED_COUNTS, extract_profile_name
     from .balance import SharedBalance, node_event
     shared = SharedState()
     extra = probe(shared) if probe is not None else None
     balance = SharedBalance(node_name, store.load, slicing_client.used_ids, node_event(mgr.client, node_name),
-                            SKIP_SHARED_COUNTS if skip_counts is None else skip_counts)
+                            SKIP_SHARED_COUNTS if skip_counts is None else skip_counts, on_release=on_release)
     reporter = Reporter(mgr.client, slicing_client, shared, refresh_interval, profile_extractor=extract_profile_name,
                         extra_annotations=extra, observers=[balance.check])
     reporter.balance = balance

@@ -11,7 +11,9 @@ Nothing on the node can move a running process's queues, so that state is report
 per GPU, the gauge ``nos_shared_slices_uneven`` is 1 while the count of memory-only slices in use is
 one of the skipped counts, and each transition into it records a ``SharedSlicesUneven`` Warning
 event on the Node (back to even: a ``SharedSlicesEven`` Normal event). The slice agent's reporter
-runs the check on every report (``refresh_interval``).
+runs the check on every report (``refresh_interval``), and hands every memory-only slice whose pod
+left to ``on_release`` — the start gate's ``forget``, so a container that left (or never reached the
+GPU) holds no later start back.
 """
 from __future__ import annotations
 
@@ -50,17 +52,25 @@ class SharedBalance:
 
     def __init__(self, node: str, load_slices: Callable[[], Dict[int, Iterable[Any]]],
                  used_ids: Callable[[], set], event: Optional[Callable[[str, str, str], None]] = None,
-                 skip_counts: Iterable[int] = SKIP_SHARED_COUNTS):
+                 skip_counts: Iterable[int] = SKIP_SHARED_COUNTS, on_release: Optional[Callable[[str], None]] = None):
         self.node = node
         self.load_slices = load_slices
         self.used_ids = used_ids
         self.event = event
         self.skip = frozenset(int(n) for n in skip_counts)
+        self.on_release = on_release
         self.uneven: Dict[int, int] = {}   # GPU -> the uneven count it was last seen at
+        self.in_use: set = set()           # memory-only slice ids in use at the last check
 
     def check(self) -> Dict[int, int]:
         """Update the gauge and record transitions; returns GPU -> uneven count now."""
-        counts = shared_in_use(self.load_slices(), self.used_ids())
+        slices, used = self.load_slices(), self.used_ids()
+        shared_now = {s.id for ss in slices.values() for s in ss if s.id in used and not parse_profile(s.profile).dedicated}
+        if self.on_release is not None:
+            for sid in sorted(self.in_use - shared_now):
+                self.on_release(sid)
+        self.in_use = shared_now
+        counts = shared_in_use(slices, used)
         now = {g: n for g, n in counts.items() if n in self.skip}
         g_ = _metric()
         for g in counts:
