@@ -664,11 +664,38 @@ __global__ __launch_bounds__(256) void attn_sk_lds_fixup(const float* __restrict
   const int NK = (T + 31) / 32, QT = NK, QG = (QT + G - 1) / G;
   const long long U = (long long)B * H * QG * NK;
   const bool narrow_stores = (pin >> 8) & 1u;  // A/B: the earlier 2-byte plane stores
+  const bool xcd_local = (pin >> 9) & 1u;
   pin &= 0xffu;
   const PinnedBlock pb = pinned_block(pin);
   if (pb.id < 0) return;
+  // XCD-local order (unpinned launches, bit 9): a block merges tiles whose contributors ran on the
+  // block's own XCD (block b runs on XCD b % 8, as the attention's xcd_major_n order assumes), so
+  // their partials are read from that XCD's L2 rather than across the fabric. XCD x's workgroups
+  // are the logical range [ws(x), ws(x+1)), ws(x) = x*(P/8) + min(x, P%8); a row is XCD x's when its
+  // first contributor is, i.e. rows [rlo(x), rlo(x+1)) with rlo(x) = ceil((ws(x)*U + 1 - P) / (NK*P)).
+  // Only the order changes: every tile is still merged exactly once, with the same arithmetic.
+  // Opt-in (flag bit 6): measured no faster than the plain order (profiles/attn_fixup_order_ab_r6.json)
+  // — the partials are read from beyond the XCD's L2 either way after the kernel boundary.
+  const int R = B * H * QG;
+  int id0 = pb.id, idn = R * G, step = pb.n, base = 0;
+  if (xcd_local && !pin) {
+    const int x = int(blockIdx.x) % 8, qq = P / 8, rr = P % 8;
+    auto rlo = [&](int xx) -> int {
+      if (xx >= 8) return R;
+      const long long ws = (long long)xx * qq + min(xx, rr);
+      const long long num = ws * U + 1 - P, den = (long long)NK * P;
+      const long long r0 = num <= 0 ? 0 : (num + den - 1) / den;
+      return int(min<long long>(r0, R));
+    };
+    const int r0 = rlo(x), r1 = rlo(x + 1);
+    base = r0 * G;
+    idn = max(0, r1 - r0) * G;
+    id0 = int(blockIdx.x) / 8;
+    step = int(gridDim.x) / 8;
+  }
   // grid-stride over the (group, query tile) units: a pinned launch runs a few workgroups per CU
-  for (int id = pb.id; id < B * H * QG * G; id += pb.n) {
+  for (int id_ = id0; id_ < idn; id_ += step) {
+  const int id = base + id_;
   const int wv = id % G;
   const long long grp = id / G;
   const int qg = int(grp % QG);
@@ -1429,7 +1456,8 @@ static int g_x3_pipelined = 1;
 static int g_x3_flags = 0;  // A/B switches: bit 0 explicit vmcnt(0) after a segment's prologue (planes input),
                             // bit 1 static s_setprio 1 for waves 4-7 (fp32 input), bit 3 64-bit
                             // stream-K bookkeeping (no reciprocal divisions), bit 5 the fixup's
-                            // 2-byte plane stores
+                            // 2-byte plane stores, bit 6 the fixup's XCD-local tile order (measured
+                            // no faster: profiles/attn_fixup_order_ab_r6.json)
 
 int nos_attention_x3_set_flags(int f) {
   g_x3_flags = f;
@@ -1568,9 +1596,10 @@ static int attention_x3_launch(const void* qkv3, size_t plane_stride, float* out
   if (int rc = check_launch("attn_fwd_x3")) return rc;
   if (!fixup) return 0;  // the partials are merged by the consumer (attn_proj.hip)
   if (cnt && G == 8 && f32in && g_x3_wide && g_x3_pipelined) return 0;  // merged in the kernel
-  const unsigned fpin = pin | ((g_x3_flags & 32) ? 0x100u : 0u);  // bit 8: the earlier 2-byte stores (A/B)
+  // bit 8: the earlier 2-byte stores (A/B); bit 9: XCD-local tile order (unpinned launches, flag bit 6)
+  const unsigned fpin = pin | ((g_x3_flags & 32) ? 0x100u : 0u) | ((!pin && (g_x3_flags & 64)) ? 0x200u : 0u);
   if (G == 8)
-    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(B * hn * QG * 8, pin)), dim3(256), 0, s,
+    hipLaunchKernelGGL(attn_sk_lds_fixup<8>, dim3(pinned_grid(8 * ((B * hn * QG * 8 + 7) / 8), pin)), dim3(256), 0, s,
                        part_o, part_ml,
                        out, B, T, hn, waves, op, h0, H, fpin);
   else

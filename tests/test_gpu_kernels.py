@@ -632,3 +632,27 @@ def test_attention_in_kernel_merge_matches_fixup_launch(K, B, T, H, waves, hb):
     finally:
         K.set_attention_merge(None)
         K.set_attention_x3_wide(K.attention_x3_wide_default())
+
+
+@pytest.mark.parametrize("B,T,H,waves,hb", [(1, 3401, 6, None, None), (1, 3401, 6, 126, None), (1, 3401, 6, 32, 2),
+                                            (2, 300, 3, 64, None), (1, 77, 1, 3, None), (1, 1000, 2, 333, 1)])
+def test_attention_fixup_xcd_local_order_is_bit_identical(K, B, T, H, waves, hb):
+    # the stream-K fixup merges every split tile once whichever order its blocks take them in: the
+    # plain order (default) against the XCD-local one (flag bit 6), fp32 and x3 planes
+    torch.manual_seed(23)
+    qkv = torch.randn(B, T, 3 * H * 64, device="cuda")
+    w = waves or K.attention_x3_waves(K.slice_cus(), B, T, H)
+    L = K._L()
+    try:
+        for x3 in (False, True):
+            outs = []
+            for flags in (0, 64):
+                L.nos_attention_x3_set_flags(flags)
+                out = (torch.full((3, B, T, H * 64), float("nan"), dtype=torch.bfloat16, device="cuda") if x3
+                       else torch.full((B, T, H * 64), float("nan"), device="cuda"))
+                outs.append(K.attention_x3f(qkv, out, H, 64, 0.125, w, head_block=hb))
+            torch.cuda.synchronize()
+            assert not torch.isnan(outs[0].float()).any(), (x3, w)
+            assert torch.equal(outs[0], outs[1]), (x3, w)
+    finally:
+        L.nos_attention_x3_set_flags(int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))

@@ -50,9 +50,10 @@ def main() -> int:
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--slices", default="spx,dpx,cpx")
     ap.add_argument("--model", action="store_true", help="also time the whole inference per arm")
-    ap.add_argument("--arms", default="wide,wide_fixup,x3p8",
-                    help="arms to time (one arm for a counter pass): wide = attn_fwd_x3w merging in the kernel, "
-                         "wide_fixup = the same with the separate fixup launch, x3p8 = attn_fwd_x3p<8>")
+    ap.add_argument("--arms", default="wide,x3p8",
+                    help="arms to time (one arm for a counter pass): wide = attn_fwd_x3w + the fixup launch "
+                         "(production), wide_xfix = the same with the fixup's XCD-local tile order, wide_merge = "
+                         "the merge inside the kernel, x3p8 = attn_fwd_x3p<8>")
     ap.add_argument("--no-check", action="store_true", help="skip the bit-identity check")
     ap.add_argument("--out", default="gpurun_out/attn_wide_ab.json")
     a = ap.parse_args()
@@ -66,7 +67,9 @@ def main() -> int:
 
     def use(arm: str, wide: bool) -> None:
         K.set_attention_x3_wide(wide)
-        K.set_attention_merge(arm == "wide")
+        K.set_attention_merge(arm == "wide_merge")
+        # wide_xfix: the fixup's XCD-local tile order (flag bit 6)
+        K._L().nos_attention_x3_set_flags(64 if arm == "wide_xfix" else int(os.environ.get("NOS_ATTN_X3_FLAGS", "0")))
     flops_x3 = 4.0 * T * T * HD * H * 6
     for label in a.slices.split(","):
         cus = slice_cus(f"{label}_nps1", 0)
