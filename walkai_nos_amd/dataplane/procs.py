@@ -81,7 +81,7 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
              cu_count: int = 256, stagger_s: float = 0.0,
              per_pod_env: Optional[Sequence[Dict[str, str]]] = None, sequential: bool = False,
              gate: bool = False, churn: Optional[Tuple[Sequence[int], Sequence[str]]] = None,
-             gate_timeout: float = 20.0) -> Dict[str, Any]:
+             gate_timeout: float = 20.0, settle_s: float = 0.0) -> Dict[str, Any]:
     """Start one process per profile, release them together, collect their JSON lines.
     ``stagger_s``: wait this long between pod starts (pods of a node start at different times);
     ``per_pod_env``: env overrides of pod i (after ``extra_env``); ``sequential``: start pod i+1
@@ -92,7 +92,8 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
     profiles) — once the first pods are READY, stop those pods and start new ones of those profiles
     (through the gate when ``gate``; the indices are then positions in the gate's start order, so
     "three pods of one start parity" is ``[0, 2, 4]``); the window measures the pods running after
-    the churn."""
+    the churn. ``settle_s``: after stopping them, wait (at most this long) until the KFD lists that
+    many fewer processes with compute queues — a process's queues can outlive its exit for a while."""
     from ..device.protos import dp
     from ..deviceplugin.startgate import StartGate
     new_profiles = list(churn[1]) if churn else []
@@ -155,9 +156,19 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
             if gate:                    # start-order positions -> pod indices (slice s<i> is pod i)
                 order = [int(sid.rsplit("::s", 1)[1]) for _, sid in start_gate.order]
                 stopped = [order[k] for k in stopped]
+            kfd = None
+            if settle_s > 0:
+                from ..deviceplugin.startgate import KfdProbe
+                kfd = KfdProbe()
+                before = len(kfd.ready_pids())
             for i in stopped:
                 procs[i].proc.kill()
                 procs[i].proc.wait()
+            if kfd is not None:
+                t0 = time.time()
+                while len(kfd.ready_pids()) > before - len(stopped) and time.time() - t0 < settle_s:
+                    time.sleep(0.02)
+                settled = (round(time.time() - t0, 3), len(kfd.ready_pids()), before)
             later = list(range(len(profiles), len(all_profiles)))
             start_all(later)
             _wait_ready([procs[i] for i in later], [procs[i] for i in later], [logs[i] for i in later],
@@ -189,6 +200,9 @@ def run_pods(profiles: Sequence[str], seconds: float = 10.0, shim: bool = True, 
                        "timeouts": start_gate.timeouts}
     if churn:
         out["churn"] = {"stopped": stopped, "started": list(range(len(profiles), len(all_profiles)))}
+        if settle_s > 0:
+            out["churn"]["settle"] = {"waited_s": settled[0], "kfd_ready_after": settled[1],
+                                      "kfd_ready_before": settled[2]}
     return out
 
 
