@@ -220,6 +220,24 @@ def test_native_libraries_are_stamped_with_their_source_hash():
     assert t.source_hash() != b.Target("x", ["probe.hip"], "hipcc", flags=["-DX"]).source_hash()
 
 
+def test_per_source_flags_build_their_own_object():
+    # csrc/attn_wide.hip is compiled alone with its code-generation options and linked first (hipcc
+    # marks every .hip source `-x hip`, which would claim an object listed after it); its flags are
+    # part of the stamp
+    from walkai_nos_amd.ops import build as b
+    t = b.target("libnos_kernels.so")
+    cmds = t.commands()
+    assert len(cmds) == 2
+    obj_cmd, link = cmds
+    assert "-c" in obj_cmd and obj_cmd[obj_cmd.index("-c") + 1].endswith("attn_wide.hip")
+    assert "-amdgpu-mfma-vgpr-form=1" in obj_cmd and "-amdgpu-mfma-vgpr-form=1" not in link
+    srcs = [x for x in link if x.endswith((".hip", ".o"))]
+    assert srcs[0].endswith("attn_wide.hip.o") and all(x.endswith(".hip") for x in srcs[1:])
+    assert "-shared" in link and "-shared" not in obj_cmd
+    plain = b.Target(t.name, t.sources, t.compiler)
+    assert plain.source_hash() != t.source_hash()
+
+
 # -- the chart rendered (hack/helmlite.py: a Go-template subset interpreter; no helm binary here) --
 def _chart(values=None, namespace="nos-system", lookup=None):
     import sys
