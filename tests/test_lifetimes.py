@@ -188,3 +188,31 @@ def test_drain_victim_avoids_hiding_slices_pods_wait_for():
                        slice_strand_weight=w)
         ch = plan_cluster_pack({"n": node()}, list(pending), params=p, pods_of=lambda n, g: pods[g], life=life)
         assert [g.target is not None for g in ch["n"].gpus] == want
+
+
+def test_declared_bounds_cap_the_residuals_of_a_drain():
+    # spec.activeDeadlineSeconds: kubelet ends the pod that long after its start, so a pod near its
+    # deadline frees its groups soon whatever the learned run times say
+    from walkai_nos_amd.controllers.partitioner.lifetimes import declared_bound
+    m = _model([600.0] * 32)
+    free = drain_cost([(4, 100.0), (4, 100.0)], capacity=8, need=8, model=m)
+    near = drain_cost([(4, 100.0, 130.0), (4, 100.0, 160.0)], capacity=8, need=8, model=m)
+    assert free[1] == pytest.approx(500.0) and near[1] == pytest.approx(60.0)
+    assert near[0] == pytest.approx(4 * 30.0)      # one pod's 4 groups idle from its deadline to the other's
+    # a bound already passed: the pod is as good as gone; a loose bound changes nothing
+    assert drain_cost([(8, 100.0, 90.0)], capacity=8, need=8, model=m)[1] == 0.0
+    assert drain_cost([(4, 100.0, 10_000.0), (4, 100.0)], capacity=8, need=8, model=m) == free
+    assert declared_bound({"spec": {"activeDeadlineSeconds": 360}}) == 360.0
+    assert declared_bound({"spec": {}}) is None and declared_bound({"spec": {"activeDeadlineSeconds": "x"}}) is None
+
+
+def test_the_pod_controller_reads_declared_bounds():
+    # the sim's pods carry the bound the bench gives them; _gpu_pods hands it to drain_cost
+    from walkai_nos_amd.bench_core import BenchConfig, NodeBench
+    nb = NodeBench(BenchConfig(gpus=1, layout="slices", declared_bound_quanta=6.0, data_plane=False),
+                   gpu_data_plane=False)
+    for _ in range(6):
+        nb.control_step()
+        nb.end_step()
+    pods = [p for p in nb.cluster.api.list("Pod") if (p.get("spec") or {}).get("activeDeadlineSeconds")]
+    assert pods and all(p["spec"]["activeDeadlineSeconds"] >= 360 for p in pods)

@@ -20,11 +20,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def run(job):
-    gpus, load, seed, steps, pack, layout = job
+    gpus, load, seed, steps, pack, layout, bound = job
     import logging
     logging.disable(logging.CRITICAL)
     from walkai_nos_amd.bench_core import BenchConfig, control_only
-    r = control_only(BenchConfig(gpus=gpus, offered_load=load, seed=seed, pack=pack or None, layout=layout), steps)
+    r = control_only(BenchConfig(gpus=gpus, offered_load=load, seed=seed, pack=pack or None, layout=layout,
+                                 declared_bound_quanta=bound), steps)
     pp = r["per_profile"]
     return {"gpus": gpus, "load": load, "seed": seed, "util_pct": r["util_pct"], "flips": r["flips"],
             "time_in_flip_pct": r["time_in_flip_pct"], "pending_mean": r["pending_mean"],
@@ -43,11 +44,14 @@ def main() -> int:
     ap.add_argument("--pack", default="{}", help="PackParams overrides as JSON")
     ap.add_argument("--workers", type=int, default=6)
     ap.add_argument("--layout", default="slices", help="xcp-layout of the node: partitions | slices | auto")
+    ap.add_argument("--declared-bound", type=float, default=0.0,
+                    help="every pod declares spec.activeDeadlineSeconds of this many quanta (0: none)")
     ap.add_argument("--out", default="profiles/planner_sweep_r5_slices.json")
     a = ap.parse_args()
     pack = json.loads(a.pack)
     jobs = list(itertools.product([int(g) for g in a.gpus.split(",")], [float(x) for x in a.loads.split(",")],
-                                  [int(s) for s in a.seeds.split(",")], [a.steps], [pack], [a.layout]))
+                                  [int(s) for s in a.seeds.split(",")], [a.steps], [pack], [a.layout],
+                                  [a.declared_bound]))
     with mp.Pool(a.workers) as pool:
         rows = pool.map(run, jobs)
     cells = {}
@@ -65,7 +69,8 @@ def main() -> int:
             "idle_pct_mean": {k: round(sum(r["idle_pct"][k] for r in grp) / len(grp), 2) for k in grp[0]["idle_pct"]},
             "tts_p99_lifetimes_worst_seed": tts}
         print(f"{g}gpu/load{l}", json.dumps(cells[f"{g}gpu/load{l}"]), flush=True)
-    out = {"steps": a.steps, "seeds": a.seeds, "pack_overrides": pack, "layout": a.layout, "cells": cells, "rows": rows}
+    out = {"steps": a.steps, "seeds": a.seeds, "pack_overrides": pack, "layout": a.layout,
+           "declared_bound_quanta": a.declared_bound, "cells": cells, "rows": rows}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)

@@ -179,6 +179,8 @@ class BenchConfig:
     partitions_window: bool = True       # also time the same window on hardware partitions (config 4)
     pod_start_s: float = -1.0            # cluster seconds a newly bound pod holds its slice before it serves
                                          # (<0: POD_START_S; bench.py measures it on the box before the window)
+    declared_bound_quanta: float = 0.0   # >0: every pod declares spec.activeDeadlineSeconds = this many quanta
+                                         # (plus its start-up), no tighter than the churn's longest lifetime
 
     def __post_init__(self) -> None:
         #: the flip cost is the components' sum (so a measured commit barrier replaces its constant)
@@ -741,7 +743,9 @@ class NodeBench:
         now = c.clock()
         for prof in self.churn.arrivals():
             name = f"p{self.churn.seq}"
-            c.submit({f"amd.com/{prof}": 1}, name=name)
+            bound = (self.cfg.declared_bound_quanta * self.cfg.cluster_s + self.cfg.pod_start_s
+                     if self.cfg.declared_bound_quanta > 0 else None)
+            c.submit({f"amd.com/{prof}": 1}, name=name, deadline_s=bound)
             self.profile_of[name] = prof
             self.offered_gpu_quanta += self.cfg.mean_lifetime_quanta / COMPUTE_MODES[prof.split("_")[0]]
             self.created[name] = now

@@ -19,7 +19,9 @@ run times of the pods that already finished and from how long each running pod h
   given its age again (a heavy tail's expected residual, not the half-age of an exhausted sample);
 * :func:`drain_cost` — Monte Carlo over those residuals (a fixed seed: the planner is
   deterministic): expected idle group-seconds until ``need`` groups are free, and the expected
-  time until then;
+  time until then. A pod that declares a bound (``spec.activeDeadlineSeconds``: kubelet ends it
+  that long after its start) has its residual capped at what is left of the bound, so a GPU whose
+  pods are about to hit their deadlines is priced as the cheap drain it is;
 * :class:`LifetimeTracker` — the pod controller's bookkeeping: running pods it has seen (start
   times), and the run time of every one that has since finished or vanished.
 """
@@ -32,8 +34,17 @@ from typing import Any, Deque, Dict, Iterable, List, Optional, Sequence, Tuple
 
 from ...kube import objects as ko
 
-#: (groups the pod holds, seconds it has run)
-PodAge = Tuple[int, float]
+#: (groups the pod holds, seconds it has run[, its declared bound: spec.activeDeadlineSeconds])
+PodAge = Tuple  # (int, float) or (int, float, Optional[float])
+
+
+def declared_bound(pod: Dict[str, Any]) -> Optional[float]:
+    """``spec.activeDeadlineSeconds`` (kubelet ends the pod that long after its start), or None."""
+    v = (pod.get("spec") or {}).get("activeDeadlineSeconds")
+    try:
+        return float(v) if v is not None and float(v) > 0 else None
+    except (TypeError, ValueError):
+        return None
 
 
 class LifetimeModel:
@@ -151,9 +162,10 @@ def drain_cost(pods: Sequence[PodAge], capacity: int, need: int, model: Lifetime
     for — a pod bound but not yet Running, or one the agent's status-pods annotation does not list
     yet — count as a pod that has just started, so a stale annotation never makes a busy GPU look
     free (and the cheapest drain victim)."""
-    held = sum(g for g, _ in pods)
+    pods = [(p[0], p[1], p[2] if len(p) > 2 else None) for p in pods]
+    held = sum(g for g, _, _ in pods)
     if used is not None and used > held:
-        pods = list(pods) + [(used - held, 0.0)]
+        pods = pods + [(used - held, 0.0, None)]
         held = used
     free0 = capacity - held
     if free0 >= need:
@@ -161,7 +173,7 @@ def drain_cost(pods: Sequence[PodAge], capacity: int, need: int, model: Lifetime
     rng = random.Random(seed)
     cost = wait = 0.0
     for _ in range(samples):
-        ends = sorted((model.sample_residual(a, rng), g) for g, a in pods)
+        ends = sorted((_bounded(model.sample_residual(a, rng), a, b), g) for g, a, b in pods)
         free, t, c = free0, 0.0, 0.0
         for r, g in ends:
             c += free * (r - t)
@@ -172,6 +184,11 @@ def drain_cost(pods: Sequence[PodAge], capacity: int, need: int, model: Lifetime
         cost += c
         wait += t
     return cost / samples, wait / samples
+
+
+def _bounded(residual: float, age: float, bound: Optional[float]) -> float:
+    """A residual run time no longer than what is left of the pod's declared bound."""
+    return residual if bound is None else min(residual, max(0.0, bound - age))
 
 
 class LifetimeTracker:

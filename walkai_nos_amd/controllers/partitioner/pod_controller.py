@@ -819,27 +819,32 @@ class PodController:
                     self._mode_since[(name, g.index)] = (mode, now)
         return lambda name, idx: now - self._mode_since.get((name, idx), (None, float("-inf")))[1]
 
-    def _gpu_pods(self, nodes: List[Dict[str, Any]], now: float) -> Callable[[str, int], List[Tuple[int, float]]]:
-        """(groups, seconds run) of the pods on each GPU: the agents' ``status-pods`` annotation
-        names them, their ``startTime`` dates them; feeds the lifetime model as pods finish."""
+    def _gpu_pods(self, nodes: List[Dict[str, Any]], now: float) -> Callable[[str, int], List[Tuple]]:
+        """(groups, seconds run, declared bound) of the pods on each GPU: the agents' ``status-pods``
+        annotation names them, their ``startTime`` dates them, ``spec.activeDeadlineSeconds`` bounds
+        them (None when not declared); feeds the lifetime model as pods finish."""
         import json
 
         from ...models.xcp.slices import groups_of
+        from .lifetimes import declared_bound
         names = {ko.name(n) for n in nodes}
         # running AND terminal pods: a pod that finished is a run time for the lifetime model (with
         # its own finishedAt), however briefly it ran between two passes
         pods = [p for p in self.client.list("Pod", field_selector="status.phase!=Pending", copy=False)
                 if ko.pod_node_name(p) in names]
         groups: Dict[str, int] = {}
+        bounds: Dict[str, Optional[float]] = {}
         mine = []
         for p in pods:
             r = requested_profiles(self.kind, p)
             if r:
                 mine.append(p)
                 if ko.pod_phase(p) == "Running":
-                    groups["/".join(ko.key(p))] = sum(groups_of(k) * q for k, q in r.items())
+                    k = "/".join(ko.key(p))
+                    groups[k] = sum(groups_of(x) * q for x, q in r.items())
+                    bounds[k] = declared_bound(p)
         ages = self.lifetimes.update(mine, now)
-        by: Dict[Tuple[str, int], List[Tuple[int, float]]] = {}
+        by: Dict[Tuple[str, int], List[Tuple]] = {}
         for n in nodes:
             try:
                 doc = json.loads(ko.annotations(n).get(api.ANNOTATION_GPU_PODS_STATUS) or "{}")
@@ -847,7 +852,8 @@ class PodController:
                 continue
             for g, keys in doc.items():
                 if str(g).isdigit():
-                    by[(ko.name(n), int(g))] = [(groups[k], ages[k]) for k in keys if k in ages and k in groups]
+                    by[(ko.name(n), int(g))] = [(groups[k], ages[k], bounds.get(k)) for k in keys
+                                                if k in ages and k in groups]
         return lambda name, idx: by.get((name, idx), [])
 
     def _update_spx_demand(self, nodes: List[Dict[str, Any]], pending: List[Tuple[Dict[str, int], float]]) -> None:

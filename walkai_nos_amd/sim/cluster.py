@@ -456,10 +456,15 @@ class SimCluster:
     # -- workload -----------------------------------------------------------------------
     def submit(self, requests: Dict[str, int], name: Optional[str] = None, namespace: str = "default",
                labels: Optional[Dict[str, str]] = None, scheduler_name: str = "default-scheduler",
-               priority: int = 0) -> Dict[str, Any]:
+               priority: int = 0, deadline_s: Optional[float] = None) -> Dict[str, Any]:
+        """``deadline_s``: the pod's declared bound, ``spec.activeDeadlineSeconds`` (the workload
+        ends it no later; the simulation does not kill pods that outrun it)."""
         name = name or f"pod-{next(self.pod_seq)}"
-        return self.api.create(ko.new_pod(name, namespace, requests=requests, labels_=labels,
-                                          scheduler_name=scheduler_name, priority=priority))
+        pod = ko.new_pod(name, namespace, requests=requests, labels_=labels, scheduler_name=scheduler_name,
+                         priority=priority)
+        if deadline_s:
+            pod["spec"]["activeDeadlineSeconds"] = int(deadline_s)
+        return self.api.create(pod)
 
     def complete(self, name: str, namespace: str = "default", phase: str = "Succeeded") -> None:
         pod = self.api.get("Pod", name, namespace)
