@@ -21,8 +21,26 @@ def main() -> int:
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--settle", default="0,10", help="settle_s values to alternate")
     ap.add_argument("--seconds", type=float, default=4.0)
+    ap.add_argument("--hold-context", action="store_true",
+                    help="this process opens a HIP context (its own compute queues) before the pods start")
+    ap.add_argument("--hold-streams", type=int, default=0,
+                    help="... and keeps this many CU-masked streams (hardware queues) alive, each used once")
     ap.add_argument("--out", default="gpurun_out/churn_probe.json")
     a = ap.parse_args()
+    if a.hold_context:
+        import torch
+        x = torch.ones(1024, device="cuda")
+        torch.cuda.synchronize()
+        print("holding a HIP context:", float(x.sum()), flush=True)
+        from walkai_nos_amd.ops.probe import Stream
+        held = []
+        for k in range(a.hold_streams):
+            st = Stream(0, list(range(32 * (k % 8), 32 * (k % 8) + 32)))
+            with torch.cuda.stream(st.torch_stream()):
+                x.add_(1.0)
+            held.append(st)
+        torch.cuda.synchronize()
+        print("holding", len(held), "CU-masked streams", flush=True)
     runs = []
     for rep in range(a.reps):
         for settle in (float(x) for x in a.settle.split(",")):
@@ -31,7 +49,7 @@ def main() -> int:
             order = [int(s.rsplit("::s", 1)[1]) for s in r["gate"]["order"]]
             by_pod = {p["pod"]: p["inf_per_s"] for p in r["per_pod"]}
             rates = [p["inf_per_s"] for p in r["per_pod"]]
-            row = {"rep": rep, "settle_s": settle, "rates": rates, "max_over_min": round(max(rates) / min(rates), 3),
+            row = {"rep": rep, "settle_s": settle, "hold_context": a.hold_context, "hold_streams": a.hold_streams, "rates": rates, "max_over_min": round(max(rates) / min(rates), 3),
                    "aggregate": r.get("aggregate_inf_per_s"), "gate_order": order, "churn": r["churn"],
                    "by_pod": by_pod}
             runs.append(row)
