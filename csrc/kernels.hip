@@ -1,9 +1,11 @@
 // nos workload kernels for gfx950 (MI355X): the hot ops of the fp32 YOLOS-small fractional-GPU
 // workload (the GEMMs are in gemm.hip / gemm_x3.hip).
 //
-//  * attn_fwd_x3p (production): fp32-accurate flash attention on the bf16 matrix cores over the
-//    exact three-bf16-plane ("x3") form of Q/K/V, software-pipelined — see "fp32 as three bf16
-//    planes" below; attn_fwd_x3 is its block-at-a-time A/B reference;
+//  * attn_fwd_x3p: fp32-accurate flash attention on the bf16 matrix cores over the exact
+//    three-bf16-plane ("x3") form of Q/K/V, software-pipelined — see "fp32 as three bf16 planes"
+//    below; attn_fwd_x3 is its block-at-a-time A/B reference. For fp32 QKV input (the model's path)
+//    the production kernel is attn_fwd_x3w in attn_wide.hip (same units, partials and arithmetic,
+//    one wave per SIMD carrying two query tiles), dispatched by attention_x3_launch below;
 //  * attn_fwd_f32 / attn_fwd_sk / attn_fwd_sk_lds (the f32-MFMA path, set_fp32_matmul("f32")): flash attention over a packed [B, T, 3*H*64] fp32 QKV tensor on the exact-fp32
 //    matrix cores (v_mfma_f32_32x32x2_f32, 64 FLOP/clk/SIMD). One wave owns 32 queries of one head.
 //    It computes S^T = K Q^T so that every lane owns ONE query column: the softmax row reductions
