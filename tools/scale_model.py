@@ -29,6 +29,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--pod-start", type=float, default=3.09, help="cluster seconds of pod start-up (measured on the box)")
+    ap.add_argument("--declared-bound", type=float, default=None,
+                    help="pods' activeDeadlineSeconds in quanta (default: the bench's BenchConfig default)")
     ap.add_argument("--out", default="profiles/scale_model_r6.json")
     a = ap.parse_args()
     out = {"what": "the driver's bench window (seed %d, %d steps x 2 quanta after %d warm-up steps) on 1/2/4/8-GPU "
@@ -38,8 +40,9 @@ def main() -> int:
     for layout in a.layouts.split(","):
         rows = {}
         for g in (int(x) for x in a.gpus.split(",")):
+            kw = {} if a.declared_bound is None else {"declared_bound_quanta": a.declared_bound}
             cfg = BenchConfig(gpus=g, steps=a.steps, warmup=a.warmup, seed=a.seed, layout=layout,
-                              pod_start_s=a.pod_start)
+                              pod_start_s=a.pod_start, **kw)
             t0 = time.time()
             r = control_only(cfg, cfg.warmup_quanta + cfg.window_quanta, skip=cfg.warmup_quanta)
             rows[str(g)] = {"util_pct": r["util_pct"], "inf_per_s_model": r["inf_per_s_model"],
