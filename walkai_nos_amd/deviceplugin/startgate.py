@@ -57,24 +57,23 @@ def kfd_compute_queues(pid: int, root: str = KFD_PROC) -> int:
     return n
 
 
+def slice_ids_of(pid: int, proc: str = "/proc") -> frozenset:
+    """The slice ids in a process's ``NOS_SLICE_IDS`` (empty when it has none or is gone)."""
+    try:
+        with open(os.path.join(proc, str(pid), "environ"), "rb") as f:
+            env = f.read()
+    except OSError:
+        return frozenset()
+    for kv in env.split(b"\0"):
+        if kv.startswith(b"NOS_SLICE_IDS="):
+            return frozenset(x.decode(errors="replace") for x in kv[len(b"NOS_SLICE_IDS="):].split(b",") if x)
+    return frozenset()
+
+
 def pids_with_slice(slice_id: str, proc: str = "/proc") -> List[int]:
     """Processes whose environment carries ``slice_id`` in ``NOS_SLICE_IDS`` (the env ``Allocate``
     gives a slice's container; the agent runs with hostPID, so it sees every container's processes)."""
-    out = []
-    want = slice_id.encode()
-    for d in os.listdir(proc):
-        if not d.isdigit():
-            continue
-        try:
-            with open(os.path.join(proc, d, "environ"), "rb") as f:
-                env = f.read()
-        except OSError:
-            continue
-        for kv in env.split(b"\0"):
-            if kv.startswith(b"NOS_SLICE_IDS=") and want in kv[len(b"NOS_SLICE_IDS="):].split(b","):
-                out.append(int(d))
-                break
-    return out
+    return [int(d) for d in os.listdir(proc) if d.isdigit() and slice_id in slice_ids_of(int(d), proc)]
 
 
 def kfd_slice_ready(slice_id: str, min_queues: int = 2, proc: str = "/proc", kfd: str = KFD_PROC) -> bool:
@@ -150,12 +149,16 @@ class KfdProbe:
         return self.ready_pids(bdf)
 
     def ready(self, slice_id: str, bdf: Optional[str], snap: frozenset) -> bool:
+        # only the few KFD processes with their queues are candidates: their environments are read
+        # (not every process of the node, every poll)
         now = self.ready_pids(bdf)
-        mine = set(pids_with_slice(slice_id, self.proc))
-        if mine & now:
+        envs = {pid: slice_ids_of(pid, self.proc) for pid in now}
+        if any(slice_id in ids for ids in envs.values()):
             return True
-        # a PID namespace of our own: the container's process is the one that appeared since
-        return bool(now - snap - mine)
+        # a PID namespace of our own (the KFD's PIDs are not ours, their environments unreadable):
+        # the container's process is a ready one that appeared since it was let through and carries
+        # no other slice
+        return any(pid not in snap and not ids for pid, ids in envs.items())
 
 
 class _CallableProbe:
