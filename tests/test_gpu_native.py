@@ -366,8 +366,9 @@ def test_eight_pod_processes_share_one_gpu_evenly(gpu):
 
 @pytest.mark.xfail(strict=False, reason=(
     "not guaranteed: after a churn the replacements' compute queues can land on a pipe set of their own "
-    "— in the whole GPU suite (after the kernel tests, whose streams this process still holds) every churned "
-    "set measured 2.5x max/min, while the fairness tests run alone passed at 1.02 "
+    "— in the whole GPU suite run after the kernel tests (whose streams this process still holds) every "
+    "churned set measured 2.5x max/min, so the process-sharing tests now run first (tests/conftest.py); "
+    "the fairness tests run alone passed at 1.02 "
     "(profiles/pytest_fair_r6_churn_alone.log), sets run by tools/churn_probe.py on a fresh box shared within "
     "1.1x, and 1.2x when the probe process held 8 CU-masked streams: foreign queues on the GPU perturb it "
     "(profiles/churn_probe_r6.json)"))
