@@ -337,13 +337,15 @@ _tuned: Optional[Dict[str, int]] = None
 def tuned_table() -> Dict[str, int]:
     """Tiles measured on CONCURRENT sibling partitions (``tools/contention.py --emit-table``): the
     isolated autotuner cannot see what a slice's neighbours cost it, so where the table has the
-    exact (shape, epilogue, outputs, slice size) key its tile wins. ``NOS_X3_TUNED=0`` ignores it."""
+    exact (shape, epilogue, outputs, slice size) key its tile wins. ``NOS_X3_TUNED=0`` ignores it,
+    ``NOS_X3_TUNED_PATH`` reads another table."""
     global _tuned
     if _tuned is None:
         table: Dict[str, int] = {}
-        if os.environ.get("NOS_X3_TUNED", "1") != "0" and os.path.exists(_TUNED_PATH):
+        path = os.environ.get("NOS_X3_TUNED_PATH", _TUNED_PATH)  # another table (A/B runs)
+        if os.environ.get("NOS_X3_TUNED", "1") != "0" and os.path.exists(path):
             import json
-            with open(_TUNED_PATH) as f:
+            with open(path) as f:
                 table = {k: int(v["tile"]) for k, v in json.load(f).items() if int(v["tile"]) in X3_TILES}
         _tuned = table
     return _tuned
