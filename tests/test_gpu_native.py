@@ -526,9 +526,21 @@ def test_cu_guard_flags_only_the_process_outside_its_cu_mask(gpu):
     # starts, children started one at a time
     host_to_local = {}
     procs, samples, found = [], [], []
+
+    def quiet_list(still=2.0, limit=30.0):
+        """The GPU's process list once it has not changed for ``still`` seconds: a helper an earlier
+        test's agent spawned (its probe after a commit) may still be starting or exiting."""
+        t0 = cur = time.time()
+        last = set(smi.process_info(0))
+        while time.time() - cur < still and time.time() - t0 < limit:
+            time.sleep(0.2)
+            now = set(smi.process_info(0))
+            if now != last:
+                last, cur = now, time.time()
+        return last
     try:
         for e in envs:
-            before = set(smi.process_info(0))
+            before = quiet_list()
             p = subprocess.Popen([sys.executable, "-u", "-c", CU_HOG_CHILD % {"root": ROOT, "seconds": 20.0}],
                                  env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
             procs.append(p)
